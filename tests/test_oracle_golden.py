@@ -1,0 +1,47 @@
+"""Pin the CPU oracle: bit-for-bit against the reference's own outputs.
+
+Fixtures (tests/golden/*.npz) hold the reference's full hierarchy computed by
+tests/golden/make_golden.py from the reference itself (oracle/_ref).  The
+oracle must reproduce every C/F mask, id list, CSR pattern AND every double
+exactly.  The bundled amgdmp_{i,j,p}.dat is the reference's own test matrix
+(serial_amg.c:64-91; Makefile `check` target).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, golden_cases
+from omp_amg_amd import abi, parity, problems
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_oracle_matches_reference_fixture(oracle_lib, case):
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    h = abi.run_setup(oracle_lib, z["in_Ai"], z["in_Aj"], z["in_Av"])
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
+def test_amgdmp_reference_known_answers(oracle_lib):
+    """Known answers printed by the reference's serial_amg on its bundled data
+    (4 levels 49/13/4/1, singular => nullspace 1, level-1 coarsening n = 13,
+    Chebyshev rho = 0.542924, final W skeleton 101 nonzeros)."""
+    Ai, Aj, Av = problems.load_amgdmp(GOLD)
+    h = abi.run_setup(oracle_lib, Ai, Aj, Av)
+    assert [int(l.n) for l in h.levels] == [49, 13, 4, 1]
+    assert h.nullspace == 1
+    assert int(h.levels[0].C.sum()) == 13
+    assert abs(h.levels[0].rho - 0.542924) < 5e-7
+    assert h.levels[0].W.nnz == 101
+    assert int(h.levels[0].m) == 2
+
+
+def test_amgdmp_files_match_reference_loader():
+    """The bundled .dat files decode (3.14159 endian marker, 1-based ids)."""
+    Ai, Aj, Av = problems.load_amgdmp(GOLD)
+    assert len(Av) == 361 and Ai.min() == 0 and Ai.max() == 48
+    # assembled, symmetric pattern
+    pairs = set(zip(Ai.tolist(), Aj.tolist()))
+    assert all((j, i) in pairs for (i, j) in pairs)
