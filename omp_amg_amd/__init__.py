@@ -1,1 +1,219 @@
-"""omp_amg_amd: MI355X-native AMG setup (HIP) behind the gslib crs/amg_setup C ABI."""
+"""omp_amg_amd -- MI355X-native AMG setup (hand-written HIP for gfx950) behind
+the gslib C ABI of nicooff/omp_amg (amg_setup.h / crs.h).
+
+Python here is only a ctypes mirror of that C ABI for tests and the bench:
+
+  lib()                      -> ctypes.CDLL of omp_amg_amd/libomp_amg_amd.so (built in-tree)
+  amg_setup(Ai, Aj, Av)      -> abi.Hierarchy     (reference amg_setup.h:5, host COO in)
+  DeviceSetup                -> device-resident COO -> hierarchy in HBM (omp_amg_amd.h)
+  stats()                    -> per-phase times of the last setup
+
+The product path is the HIP library only: if it is missing or no GPU is
+visible these functions raise -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libomp_amg_amd.so")
+_lib = None
+
+
+class AmgdStats(C.Structure):
+    _fields_ = [("t_total_ms", C.c_double), ("t_build_ms", C.c_double),
+                ("t_coarsen_ms", C.c_double), ("t_smoother_ms", C.c_double),
+                ("t_interp_ms", C.c_double), ("t_rap_ms", C.c_double),
+                ("t_copy_ms", C.c_double), ("rap_kernel_ms", C.c_double),
+                ("rap_out_nnz", C.c_uint64), ("rap_bytes", C.c_uint64),
+                ("rows0", C.c_uint64), ("nnz0", C.c_uint64),
+                ("nlevels", C.c_uint32), ("ub_events", C.c_uint32),
+                ("peak_bytes", C.c_size_t)]
+
+
+class HCsr(C.Structure):
+    """host CSR used by the kernel test hooks (amgd_testapi.c)"""
+    _fields_ = [("rn", C.c_uint32), ("cn", C.c_uint32), ("nnz", C.c_uint64),
+                ("ro", C.POINTER(C.c_uint64)), ("col", C.POINTER(C.c_uint32)),
+                ("a", C.POINTER(C.c_double))]
+
+
+def build(force: bool = False, jobs: int = 8) -> str:
+    """Compile the HIP library in-tree for gfx950 (make -C omp_amg_amd/csrc)."""
+    args = ["make", "-C", os.path.join(HERE, "csrc"), f"-j{jobs}"]
+    if force:
+        subprocess.run(["make", "-C", os.path.join(HERE, "csrc"), "clean"], check=True)
+    subprocess.run(args, check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run omp_amg_amd.build() (no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        abi.bind_setup(L)
+        L.amgd_set_exact_dots.argtypes = [C.c_int]
+        L.amgd_init.argtypes = [C.c_int]
+        L.amgd_init.restype = C.c_int
+        L.amgd_error.restype = C.c_char_p
+        L.amgd_setup_device.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.POINTER(C.c_void_p), C.c_int]
+        L.amgd_setup_device.restype = C.c_int
+        L.amgd_hier_export.argtypes = [C.c_void_p, C.POINTER(abi.AmgSetupData)]
+        L.amgd_hier_free.argtypes = [C.POINTER(C.c_void_p)]
+        L.amgd_get_stats.argtypes = [C.POINTER(AmgdStats)]
+        L.amgd_dev_alloc.argtypes = [C.c_size_t]
+        L.amgd_dev_alloc.restype = C.c_void_p
+        L.amgd_dev_free.argtypes = [C.c_void_p]
+        L.amgd_dev_upload.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.amgd_dev_download.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.amgd_test_csr.argtypes = [C.c_int, C.POINTER(HCsr), C.POINTER(HCsr), C.c_double,
+                                    C.c_double, C.POINTER(HCsr)]
+        L.amgd_test_spmv.argtypes = [C.POINTER(HCsr), C.c_void_p, C.c_double, C.c_void_p,
+                                     C.c_double, C.c_void_p]
+        L.amgd_test_build.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.POINTER(HCsr)]
+        L.amgd_test_math.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.amgd_test_free.argtypes = [C.POINTER(HCsr)]
+        _lib = L
+    return _lib
+
+
+def init(device: int = 0) -> None:
+    L = lib()
+    if L.amgd_init(device) != 0:
+        raise RuntimeError("omp_amg_amd: no usable HIP device: " + L.amgd_error().decode())
+
+
+def amg_setup(Ai, Aj, Av, *, seed: int = 1) -> abi.Hierarchy:
+    """Drop-in `amg_setup` (amg_setup.h:5) on host COO, through the C ABI."""
+    init()
+    return abi.run_setup(lib(), Ai, Aj, Av, seed=seed, quiet=False)
+
+
+def stats() -> dict:
+    st = AmgdStats()
+    lib().amgd_get_stats(C.byref(st))
+    return {f: getattr(st, f) for f, _ in AmgdStats._fields_}
+
+
+class DeviceSetup:
+    """COO resident in HBM -> hierarchy resident in HBM (omp_amg_amd.h)."""
+
+    def __init__(self, Ai, Aj, Av):
+        init()
+        L = lib()
+        self.nz = len(Av)
+        Ai = np.ascontiguousarray(Ai, dtype=np.uint32)
+        Aj = np.ascontiguousarray(Aj, dtype=np.uint32)
+        Av = np.ascontiguousarray(Av, dtype=np.float64)
+        self.di = L.amgd_dev_alloc(Ai.nbytes + 8)
+        self.dj = L.amgd_dev_alloc(Aj.nbytes + 8)
+        self.dv = L.amgd_dev_alloc(Av.nbytes + 8)
+        L.amgd_dev_upload(self.di, Ai.ctypes.data, Ai.nbytes)
+        L.amgd_dev_upload(self.dj, Aj.ctypes.data, Aj.nbytes)
+        L.amgd_dev_upload(self.dv, Av.ctypes.data, Av.nbytes)
+        self.h = C.c_void_p()
+
+    def run(self, seed: int = 1, exact_dots: bool = True) -> dict:
+        L = lib()
+        L.amgd_set_exact_dots(1 if exact_dots else 0)
+        if self.h:
+            L.amgd_hier_free(C.byref(self.h))
+        abi.srand(seed)
+        rc = L.amgd_setup_device(self.nz, self.di, self.dj, self.dv, C.byref(self.h), 0)
+        if rc != 0:
+            raise RuntimeError("amgd_setup_device failed: " + L.amgd_error().decode())
+        return stats()
+
+    def export(self) -> abi.Hierarchy:
+        L = lib()
+        libc = C.CDLL(None)
+        libc.malloc.restype = C.c_void_p
+        raw = libc.malloc(C.sizeof(abi.AmgSetupData))
+        C.memset(raw, 0, C.sizeof(abi.AmgSetupData))
+        dp = C.cast(raw, C.POINTER(abi.AmgSetupData))
+        L.amgd_hier_export(self.h, dp)
+        h = abi.read_setup_data(dp.contents)
+        L.free_data(C.pointer(dp))
+        return h
+
+    def close(self):
+        L = lib()
+        if self.h:
+            L.amgd_hier_free(C.byref(self.h))
+        for p in (self.di, self.dj, self.dv):
+            if p:
+                L.amgd_dev_free(p)
+        self.di = self.dj = self.dv = None
+
+
+# ---------------------------------------------------------------- test hooks
+def _to_hcsr(ro, col, a, rn, cn):
+    ro = np.ascontiguousarray(ro, dtype=np.uint64)
+    col = np.ascontiguousarray(col, dtype=np.uint32)
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    h = HCsr(rn, cn, int(ro[-1]), ro.ctypes.data_as(C.POINTER(C.c_uint64)),
+             col.ctypes.data_as(C.POINTER(C.c_uint32)), a.ctypes.data_as(C.POINTER(C.c_double)))
+    h._keep = (ro, col, a)
+    return h
+
+
+def _from_hcsr(h):
+    rn, nz = h.rn, h.nnz
+    ro = np.ctypeslib.as_array(h.ro, shape=(rn + 1,)).astype(np.int64)
+    col = np.ctypeslib.as_array(h.col, shape=(max(nz, 1),))[:nz].astype(np.int64)
+    a = np.ctypeslib.as_array(h.a, shape=(max(nz, 1),))[:nz].copy()
+    out = abi.Csr(rn, h.cn, ro, col, a)
+    lib().amgd_test_free(C.byref(h))
+    return out
+
+
+def test_csr_op(op: int, A: abi.Csr, B: abi.Csr | None = None, alpha=1.0, beta=1.0) -> abi.Csr:
+    """op: 0 spgemm, 1 transpose, 2 mpm, 3 mxmpoint, 4 min_skel (kernel test hooks)."""
+    init()
+    ha = _to_hcsr(A.row_off, A.col, A.a, A.rn, A.cn)
+    hb = _to_hcsr(B.row_off, B.col, B.a, B.rn, B.cn) if B is not None else None
+    hx = HCsr()
+    rc = lib().amgd_test_csr(op, C.byref(ha), C.byref(hb) if hb else None, alpha, beta, C.byref(hx))
+    if rc != 0:
+        raise RuntimeError(f"amgd_test_csr({op}) failed rc={rc}")
+    return _from_hcsr(hx)
+
+
+def test_spmv(A: abi.Csr, x, alpha=0.0, y=None, beta=1.0):
+    init()
+    ha = _to_hcsr(A.row_off, A.col, A.a, A.rn, A.cn)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    z = np.zeros(A.rn)
+    yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64)
+    lib().amgd_test_spmv(C.byref(ha), x.ctypes.data, alpha, None if yy is None else yy.ctypes.data,
+                         beta, z.ctypes.data)
+    return z
+
+
+def test_build(Ai, Aj, Av) -> abi.Csr:
+    init()
+    Ai = np.ascontiguousarray(Ai, dtype=np.uint32)
+    Aj = np.ascontiguousarray(Aj, dtype=np.uint32)
+    Av = np.ascontiguousarray(Av, dtype=np.float64)
+    hx = HCsr()
+    lib().amgd_test_build(len(Av), Ai.ctypes.data, Aj.ctypes.data, Av.ctypes.data, C.byref(hx))
+    return _from_hcsr(hx)
+
+
+def test_math(op: int, a, b=None):
+    init()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
+    out = np.zeros_like(a)
+    lib().amgd_test_math(op, len(a), a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out

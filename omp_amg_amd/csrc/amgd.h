@@ -1,0 +1,159 @@
+/*
+ * amgd.h -- the thin internal C ABI between the host setup driver (amgd_setup.c,
+ * plain C) and the hand-written HIP kernels (amgd_*.hip).  No HIP or torch type
+ * appears here: device memory is passed as plain pointers, matrices as `dcsr`.
+ *
+ * Device CSR layout in HBM (DESIGN.md "Data layout"):
+ *   ro  : u64[rn+1]  row offsets (64-bit: coarse operators exceed 2^32 nnz at scale)
+ *   col : u32[nnz]   column indices, ascending within a row (reference invariant)
+ *   a   : f64[nnz]   values
+ * Masks (C/F sets, strength filters) are u8 {0,1} arrays; the reference keeps
+ * them as doubles (amg_setup.c:175-180) but every use is a !=0 test or a
+ * multiply by 0/1 of a non-negative value, which the u8 form reproduces exactly.
+ */
+#ifndef AMGD_H
+#define AMGD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  uint32_t rn, cn;
+  uint64_t nnz;
+  uint64_t *ro;
+  uint32_t *col;
+  double *a;
+} dcsr;
+
+/* ---------------- runtime (amgd_rt.hip) ---------------- */
+int amgd_rt_init(int device);            /* idempotent; 0 on success */
+const char *amgd_last_error(void);
+void *amgd_alloc(size_t bytes);          /* caching pool; aborts loudly on OOM */
+void amgd_free(void *p);
+void amgd_pool_release(void);            /* return every cached block to the driver */
+size_t amgd_pool_bytes_in_use(void);
+size_t amgd_pool_peak_bytes(void);
+void amgd_h2d(void *d, const void *h, size_t n);
+void amgd_d2h(void *h, const void *d, size_t n);
+void amgd_d2d(void *d, const void *s, size_t n);
+void amgd_memset(void *d, int v, size_t n);
+void amgd_sync(void);
+double amgd_wtime(void);
+void *amgd_stream(void);                 /* hipStream_t of the library */
+void amgd_set_stream(void *stream);
+/* event timers on the library stream, for kernel-level throughput */
+void amgd_timer_start(int slot);
+void amgd_timer_stop(int slot);
+double amgd_timer_ms(int slot);          /* accumulated, syncs */
+void amgd_timer_reset(void);
+
+dcsr *dcsr_new(uint32_t rn, uint32_t cn, uint64_t nnz);
+void dcsr_free(dcsr **A);
+dcsr *dcsr_copy(const dcsr *A);
+dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
+
+/* scans: counts[0..n-1] -> exclusive prefix in counts[0..n], returns total */
+uint64_t amgd_scan_u64(uint64_t *counts, uint64_t n);
+uint32_t amgd_scan_u32(uint32_t *counts, uint64_t n);
+/* compaction map for a u8 mask: map[i] = rank of i among set entries (or ~0) */
+uint32_t amgd_mask_rank(const uint8_t *mask, uint32_t n, uint32_t *map);
+
+/* ---------------- reductions (return host values, sync) ---------------- */
+void amgd_set_exact(int on);     /* 1: reference-order (sequential) dots -- default; 0: tree */
+int amgd_get_exact(void);
+double amgd_dot(const double *a, const double *b, uint64_t n);
+double amgd_norm2(const double *a, uint64_t n);
+double amgd_max_first(const double *a, uint64_t n, uint64_t *idx);  /* first argmax */
+uint64_t amgd_count_gt(const double *a, uint64_t n, double thr, double *maxv);
+double amgd_fro_minus_eye(const dcsr *A);                          /* ||A - I||_F^2 */
+
+/* ---------------- sparse (amgd_sparse.hip) ---------------- */
+dcsr *amgd_build_csr(uint64_t nz, const uint32_t *Ai, const uint32_t *Aj, const double *Av);
+dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V,
+                   uint32_t rn, uint32_t cn, int drop_zero);
+dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *vc);
+dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out);  /* perm: CSC idx -> CSR idx */
+dcsr *amgd_spgemm(const dcsr *A, const dcsr *B);           /* A*B, reference semantics */
+dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *B);
+dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B);
+/* z = (y ? alpha*y + beta*t : beta*t) [* f] with t = M x summed in column order */
+void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
+               double beta, const uint8_t *f);
+/* z = M^T x, per column in ascending row order; Mt = transpose(M) */
+void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
+void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */
+void amgd_diag(const dcsr *A, double *D);
+enum { AMGD_DPLUS = 0, AMGD_DMINUS = 1, AMGD_DMULT = 2, AMGD_MULTD = 3 };
+void amgd_diag_op(dcsr *A, const double *D, int op);
+void amgd_vals_abs(dcsr *A);
+void amgd_vals_sqr(dcsr *A);
+void amgd_vals_scale(dcsr *A, double s);
+void amgd_rowsum_sq_inv(const dcsr *A, double *s);     /* s_i = 1/sum_j a_ij^2 (row order) */
+uint64_t amgd_to_host_cols(const dcsr *A, unsigned long *h_ro, unsigned long *h_col, double *h_a);
+
+/* ---------------- vectors (amgd_vec.hip) ---------------- */
+enum {
+  AMGD_V_FILL, AMGD_V_INV, AMGD_V_SQRT, AMGD_V_MUL, AMGD_V_ADD, AMGD_V_SUB, AMGD_V_DIV
+};
+void amgd_vfill(double *a, uint64_t n, double v);
+void amgd_vop(double *c, const double *a, const double *b, uint64_t n, int op); /* c = a op b */
+void amgd_vunary(double *a, uint64_t n, int op);                                /* a = op(a) */
+void amgd_vscale(double *a, uint64_t n, double s);                              /* a = a*s */
+void amgd_u8_to_f64(const uint8_t *m, double *d, uint64_t n);
+void amgd_compact_ids(const unsigned long *id, const uint8_t *vc, uint32_t n,
+                      unsigned long *idc, unsigned long *idf);
+void amgd_lanczos_step(const double *r, double rbeta_inv, double *qk, double *qkm1, uint64_t n);
+void amgd_lanczos_resid(double *r, const double *Aqk, const double *qk, double alpha,
+                        double *qkm1, double beta, uint64_t n);
+/* pcg pieces */
+void amgd_pcg_p(double *p, const double *z, double beta, uint64_t n);
+void amgd_pcg_xrz(double *x, double *r, double *z, const double *p, const double *w,
+                  const double *M, double alpha, uint64_t n);
+void amgd_vmul_dot_prep(double *z, const double *M, const double *r, uint64_t n);
+double amgd_dot3(const double *M, const double *b, uint64_t n);  /* sum (M.*b).*b */
+
+/* ---------------- coarsening (amgd_coarsen.hip) ---------------- */
+void amgd_coarsen_w(const double *w1, const double *w2, double *w, uint32_t n);
+void amgd_coarsen_mask1(const double *w, double ctol2, const double *g, uint8_t *mask,
+                        double *x, uint32_t n);
+void amgd_mat_max(const dcsr *S, const dcsr *St, const uint8_t *f, const double *x, double tol,
+                  double *amax_tmp, double *y);
+void amgd_coarsen_mask2(double *g, const double *m, uint8_t *mask, double *x, uint32_t n);
+void amgd_coarsen_mask3(const double *m, uint8_t *mask, uint8_t *vc, uint8_t *vf, double *vfd,
+                        uint32_t n, uint32_t *anyvc);
+
+/* ---------------- interpolation (amgd_interp.hip) ---------------- */
+dcsr *amgd_min_skel(const dcsr *R);
+/* Q factors of A restricted to each row-support of Wt (packed upper triangles) */
+double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out, uint64_t *qtotal);
+void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
+                 const double *u, const double *lambda, double *out);
+void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff, const double *u);
+uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, const double *rs,
+                        const double *w, const double *sumR, double thr,
+                        uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
+uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad);
+uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_t **pi, uint32_t **pj);
+void amgd_skel_binarize(dcsr *A, int mode);
+void amgd_scale_diag_match(dcsr *W, const double *v, const double *wuc);
+void amgd_csc_gemv(const dcsr *Rt, const uint64_t *perm, const double *a, const double *x,
+                   double *z);
+/* misc vector kernels */
+void amgd_vdiv_guard(double *r, const double *num, const double *den, uint64_t n); /* r=num/den, 0 where den==0 */
+void amgd_alpha_update(double *alpha, const double *Dc, const double *w2, uint64_t n);
+void amgd_u8_not(const uint8_t *a, uint8_t *b, uint64_t n);
+void amgd_u8_nonzero(const double *a, uint8_t *m, uint64_t n);
+uint64_t amgd_u8_count(const uint8_t *m, uint64_t n);
+void amgd_vcompact(double *dst, const double *src, const uint8_t *mask, uint64_t n);
+void amgd_vexpand_add(double *dst, const double *src, const uint8_t *mask, uint64_t n);
+void amgd_vzero_where(double *a, const uint8_t *mask_keep, uint64_t n);
+void amgd_ids_iota(unsigned long *id, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

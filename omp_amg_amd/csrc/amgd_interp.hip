@@ -1,0 +1,572 @@
+// amgd_interp.hip -- energy-minimising interpolation kernels (amg_setup.c:598-1493).
+//
+// Per coarse point c (row c of Wt = W_skel^T) the reference builds an
+// A-orthonormal packed upper-triangular Q of A restricted to the support
+// Qj = Wt(c,:) (interp / interp_lmop, amg_setup.c:2053, 1589).  Q depends only
+// on (A, support), so it is factored once per skeleton here (amgd_qfactor) and
+// re-applied for W0, the constraint operator S and W.  Within a column the
+// k-steps are sequential; the 64..256 threads of a block take distinct output
+// entries of mv_utt / mv_ut (amg_setup.c:2122/2138), each summed in the
+// reference's order, so every Q entry is bit-identical to the reference.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <vector>
+
+#include "amgd.h"
+#include "amgd_dev.h"
+
+__device__ __forceinline__ uint64_t tri(uint64_t i) { return i * (i + 1) / 2; }
+
+// value of row [a0,a1) at column j (first match), or 0  -- sp_restrict_sorted
+__device__ __forceinline__ double row_lookup(const uint32_t *col, const double *a, uint64_t a0,
+                                             uint64_t a1, uint32_t j) {
+  uint64_t lo = a0, hi = a1;
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (col[mid] < j) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < a1 && col[lo] == j) ? a[lo] : 0.0;
+}
+
+// ---------------------------------------------------------------------------
+// min_skel (amg_setup.c:2198)
+// ---------------------------------------------------------------------------
+__global__ void k_min_skel(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
+                           uint64_t *wro, uint32_t *wcol, double *wa) {
+  GRID_STRIDE(i, rn) {
+    double ym = -DBL_MAX;
+    uint32_t j = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++)
+      if (a[k] > ym) { ym = a[k]; j = col[k]; }
+    wa[i] = ym > 0.0 ? 1.0 : 0.0;
+    wcol[i] = j;
+    wro[i + 1] = i + 1;
+    if (i == 0) wro[0] = 0;
+  }
+}
+extern "C" dcsr *amgd_min_skel(const dcsr *R) {
+  dcsr *W = dcsr_new(R->rn, R->cn, R->rn);
+  if (R->rn)
+    k_min_skel<<<grid_for(R->rn), 256, 0, amgd_s()>>>(R->ro, R->col, R->a, R->rn, W->ro, W->col, W->a);
+  else
+    amgd_memset(W->ro, 0, 8);
+  KCHECK();
+  return W;
+}
+
+// ---------------------------------------------------------------------------
+// Q factor: one block per support, NT threads; scratch (3*nz doubles) in LDS
+// for small supports, in a global slab for large ones.
+// ---------------------------------------------------------------------------
+#define QF_LDS_NZ 512
+template <int NT, bool GSCR>
+__global__ __launch_bounds__(NT) void k_qfactor(const uint32_t *rows, uint32_t nrows,
+                                                const uint64_t *wro, const uint32_t *wcol,
+                                                const uint64_t *aro, const uint32_t *acol,
+                                                const double *aa, const uint64_t *qoff, double *Q,
+                                                double *gscr, uint64_t gstride) {
+  __shared__ double lds[GSCR ? 1 : 3 * QF_LDS_NZ];
+  __shared__ double sh_alpha;
+  const int tid = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    uint32_t c = rows[r];
+    uint64_t w0 = wro[c];
+    uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t *Qj = wcol + w0;
+    double *Qc = Q + qoff[c];
+    double *sqv1, *sqv2, *qk;
+    if (GSCR) {
+      sqv1 = gscr + (uint64_t)blockIdx.x * gstride;
+      sqv2 = sqv1 + nz;
+      qk = sqv2 + nz;
+    } else {
+      sqv1 = lds;
+      sqv2 = lds + QF_LDS_NZ;
+      qk = lds + 2 * QF_LDS_NZ;
+    }
+    for (uint32_t k = 0; k < nz; k++) {
+      uint32_t s = Qj[k];
+      uint64_t a0 = aro[s], a1 = aro[s + 1];
+      for (uint32_t m = tid; m <= k; m += NT) sqv1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+      __syncthreads();
+      for (uint32_t i = tid; i < k; i += NT) {        // sqv2 = Q^t sqv1  (mv_utt)
+        const double *U = Qc + tri(i);
+        double v = 0;
+        for (uint32_t j = 0; j <= i; j++) v += U[j] * sqv1[j];
+        sqv2[i] = v;
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < k; i += NT) {        // qk = Q sqv2  (mv_ut)
+        double y = 0;
+        for (uint32_t j = i; j < k; j++) y += Qc[tri(j) + i] * sqv2[j];
+        qk[i] = y;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        double al = sqv1[k];
+        for (uint32_t m = 0; m < k; m++) al -= sqv1[m] * qk[m];
+        sh_alpha = -1.0 / sqrt(al);
+      }
+      __syncthreads();
+      double al = sh_alpha;
+      double *out = Qc + tri(k);
+      for (uint32_t i = tid; i < k; i += NT) out[i] = qk[i] * al;
+      if (tid == 0) out[k] = -al;
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
+  GRID_STRIDE(c, rn) {
+    uint64_t nz = wro[c + 1] - wro[c];
+    sz[c] = nz * (nz + 1) / 2;
+  }
+}
+__global__ void k_split_by_nz(const uint64_t *wro, uint32_t rn, uint32_t cap, uint32_t *sl,
+                              uint32_t *bl, unsigned *cnt) {
+  GRID_STRIDE(c, rn) {
+    uint64_t nz = wro[c + 1] - wro[c];
+    if (nz == 0) continue;
+    if (nz <= cap) sl[atomicAdd(&cnt[0], 1u)] = (uint32_t)c;
+    else bl[atomicAdd(&cnt[1], 1u)] = (uint32_t)c;
+  }
+}
+__global__ void k_max_nz(const uint64_t *wro, uint32_t rn, unsigned long long *mx) {
+  unsigned long long m = 0;
+  GRID_STRIDE(c, rn) m = max(m, (unsigned long long)(wro[c + 1] - wro[c]));
+  atomicMax(mx, m);
+}
+
+struct RowSplit {
+  uint32_t *sl, *bl;
+  unsigned ns, nb;
+  uint64_t maxnz;
+};
+static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
+  RowSplit rs;
+  rs.sl = (uint32_t *)amgd_alloc(((size_t)Wt->rn + 1) * 4);
+  rs.bl = (uint32_t *)amgd_alloc(((size_t)Wt->rn + 1) * 4);
+  unsigned *cnt = (unsigned *)amgd_alloc(16);
+  amgd_memset(cnt, 0, 16);
+  if (Wt->rn) {
+    k_split_by_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, rs.sl, rs.bl, cnt);
+    k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 2));
+  }
+  unsigned h[4];
+  amgd_d2h(h, cnt, 16);
+  amgd_free(cnt);
+  rs.ns = h[0];
+  rs.nb = h[1];
+  uint64_t mx;
+  memcpy(&mx, &h[2], 8);
+  rs.maxnz = mx;
+  return rs;
+}
+static void free_split(RowSplit &rs) { amgd_free(rs.sl); amgd_free(rs.bl); }
+
+extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
+                                uint64_t *qtotal) {
+  hipStream_t s = amgd_s();
+  uint64_t *qoff = (uint64_t *)amgd_alloc(((size_t)Wt->rn + 1) * 8);
+  if (Wt->rn) k_qsize<<<grid_for(Wt->rn), 256, 0, s>>>(Wt->ro, Wt->rn, qoff);
+  uint64_t tot = amgd_scan_u64(qoff, Wt->rn);
+  double *Q = (double *)amgd_alloc(tot * 8 + 8);
+  RowSplit rs = split_rows(Wt, QF_LDS_NZ);
+  if (rs.ns) {
+    int g = (int)std::min<unsigned>(rs.ns, 65536u);
+    k_qfactor<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, A->ro, A->col, A->a, qoff,
+                                          Q, nullptr, 0);
+    KCHECK();
+  }
+  if (rs.nb) {
+    int g = (int)std::min<unsigned>(rs.nb, 1024u);
+    uint64_t stride = 3 * rs.maxnz + 8;
+    double *scr = (double *)amgd_alloc((size_t)g * stride * 8);
+    k_qfactor<256, true><<<g, 256, 0, s>>>(rs.bl, rs.nb, Wt->ro, Wt->col, A->ro, A->col, A->a, qoff,
+                                           Q, scr, stride);
+    KCHECK();
+    amgd_free(scr);
+  }
+  free_split(rs);
+  *qoff_out = qoff;
+  if (qtotal) *qtotal = tot;
+  return Q;
+}
+
+// ---------------------------------------------------------------------------
+// Q application (the tail of interp, amg_setup.c:2100-2108):
+//   out(c, :) = Q Q^t ( Bt(c, Qj) + u_c * lambda(Qj) )
+// ---------------------------------------------------------------------------
+template <int NT, bool GSCR>
+__global__ __launch_bounds__(NT) void k_qapply(const uint32_t *rows, uint32_t nrows,
+                                               const uint64_t *wro, const uint32_t *wcol,
+                                               const double *Q, const uint64_t *qoff,
+                                               const uint64_t *bro, const uint32_t *bcol,
+                                               const double *ba, const double *u,
+                                               const double *lambda, double *out, double *gscr,
+                                               uint64_t gstride) {
+  __shared__ double lds[GSCR ? 1 : 2 * QF_LDS_NZ];
+  const int tid = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    uint32_t c = rows[r];
+    uint64_t w0 = wro[c];
+    uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t *Qj = wcol + w0;
+    const double *Qc = Q + qoff[c];
+    double *sqv1 = GSCR ? gscr + (uint64_t)blockIdx.x * gstride : lds;
+    double *sqv2 = GSCR ? sqv1 + nz : lds + QF_LDS_NZ;
+    uint64_t b0 = bro[c], b1 = bro[c + 1];
+    double uc = u[c];
+    for (uint32_t m = tid; m < nz; m += NT) {
+      double v = row_lookup(bcol, ba, b0, b1, Qj[m]);
+      sqv1[m] = v + uc * lambda[Qj[m]];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nz; i += NT) {
+      const double *U = Qc + tri(i);
+      double v = 0;
+      for (uint32_t j = 0; j <= i; j++) v += U[j] * sqv1[j];
+      sqv2[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nz; i += NT) {
+      double y = 0;
+      for (uint32_t j = i; j < nz; j++) y += Qc[tri(j) + i] * sqv2[j];
+      out[w0 + i] = y;
+    }
+    __syncthreads();
+  }
+}
+extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
+                            const double *u, const double *lambda, double *out) {
+  hipStream_t s = amgd_s();
+  RowSplit rs = split_rows(Wt, QF_LDS_NZ);
+  if (rs.ns) {
+    int g = (int)std::min<unsigned>(rs.ns, 65536u);
+    k_qapply<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
+                                         Bt->a, u, lambda, out, nullptr, 0);
+  }
+  if (rs.nb) {
+    int g = (int)std::min<unsigned>(rs.nb, 1024u);
+    uint64_t stride = 2 * rs.maxnz + 8;
+    double *scr = (double *)amgd_alloc((size_t)g * stride * 8);
+    k_qapply<256, true><<<g, 256, 0, s>>>(rs.bl, rs.nb, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
+                                          Bt->a, u, lambda, out, scr, stride);
+    amgd_free(scr);
+  }
+  KCHECK();
+  free_split(rs);
+}
+
+// ---------------------------------------------------------------------------
+// interp_lmop (amg_setup.c:1589): S := sum over coarse c (ascending) of
+// u_c * QQt_c scattered with sp_add's forward walk (amg_setup.c:1665).
+// Contribution (c, k, m) = u_c * sum_{t>=max(k,m)} q_t[k]*q_t[m] lands where
+// the walk over row Qj[k] of S meets column Qj[m] (or, if absent, the next
+// stored entry -- the reference's behaviour).  Contributions are generated in
+// (c, k, m) order, stably radix-sorted by landing position and added to S in
+// that order: bit-identical to the reference's sequential accumulation.
+// ---------------------------------------------------------------------------
+__global__ void k_lmop_contrib(const uint32_t *erow, uint64_t e0, uint64_t e1,
+                               const uint64_t *wro, const uint32_t *wcol, const double *Q,
+                               const uint64_t *qoff, const double *u, const uint64_t *sro,
+                               const uint32_t *scol, uint64_t snnz, const uint64_t *coff,
+                               uint64_t cbase, uint64_t *key, double *val) {
+  for (uint64_t e = e0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e1;
+       e += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t c = erow[e];
+    uint64_t w0 = wro[c];
+    uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    uint32_t k = (uint32_t)(e - w0);
+    const uint32_t *Qj = wcol + w0;
+    const double *Qc = Q + qoff[c];
+    double uc = u[c];
+    uint64_t o = coff[c] - cbase + (uint64_t)k * nz;
+    uint32_t j = Qj[k];
+    uint64_t t = sro[j];
+    bool live = sro[j + 1] != t;   // sp_add returns at once on an empty row
+    for (uint32_t m = 0; m < nz; m++) {
+      uint64_t land = snnz;          // "no landing" sorts after every real position
+      if (live) {
+        uint32_t xm = Qj[m];
+        while (t < snnz && scol[t] < xm) t++;
+        if (t >= snnz) live = false;   // reference runs off the end of St (UB)
+        else land = t++;
+      }
+      double q = 0.0;
+      uint32_t t0 = k > m ? k : m;
+      for (uint32_t tt = t0; tt < nz; tt++) {
+        const double *qt = Qc + tri(tt);
+        q += qt[k] * qt[m];
+      }
+      key[o + m] = land;
+      val[o + m] = uc * q;
+    }
+  }
+}
+__global__ void k_seg_accum(const uint64_t *key, const double *val, uint64_t n, uint64_t snnz,
+                            double *sa) {
+  GRID_STRIDE(i, n) {
+    uint64_t kk = key[i];
+    if (kk >= snnz) continue;
+    if (i > 0 && key[i - 1] == kk) continue;     // not the head of its run
+    double acc = sa[kk];
+    for (uint64_t t = i; t < n && key[t] == kk; t++) acc = acc + val[t];
+    sa[kk] = acc;
+  }
+}
+__global__ void k_csq(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
+  GRID_STRIDE(c, rn) {
+    uint64_t nz = wro[c + 1] - wro[c];
+    sz[c] = nz * nz;
+  }
+}
+extern void amgd_row_of_entry_launch(const uint64_t *ro, uint32_t rn, uint32_t *row);
+
+extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff,
+                          const double *u) {
+  hipStream_t s = amgd_s();
+  amgd_memset(S->a, 0, S->nnz * 8);
+  uint32_t rn = Wt->rn;
+  if (rn == 0 || Wt->nnz == 0) return;
+  uint64_t *coff = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  k_csq<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, coff);
+  uint64_t total = amgd_scan_u64(coff, rn);
+  std::vector<uint64_t> hcoff(rn + 1), hro(rn + 1);
+  amgd_d2h(hcoff.data(), coff, (rn + 1) * 8);
+  amgd_d2h(hro.data(), Wt->ro, (rn + 1) * 8);
+  uint32_t *erow = (uint32_t *)amgd_alloc(Wt->nnz * 4 + 4);
+  amgd_row_of_entry_launch(Wt->ro, rn, erow);
+  const uint64_t CH = std::min<uint64_t>(total, 1ull << 26);   // contributions per chunk
+  uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);
+  double *val = (double *)amgd_alloc(CH * 8 + 8), *val2 = (double *)amgd_alloc(CH * 8 + 8);
+  size_t tb = 0;
+  int eb = 1;
+  while (eb < 64 && (S->nnz >> eb) != 0) eb++;   // keys are 0..S->nnz
+  HIPCK(rocprim::radix_sort_pairs(nullptr, tb, key, key2, val, val2, (size_t)CH, 0, eb, s));
+  void *tmp = amgd_alloc(tb + 16);
+  uint32_t c0 = 0;
+  while (c0 < rn) {
+    uint32_t c1 = c0;
+    // take whole coarse rows while they fit (a single oversized row gets its own chunk)
+    while (c1 < rn && (hcoff[c1 + 1] - hcoff[c0] <= CH || c1 == c0)) c1++;
+    uint64_t n = hcoff[c1] - hcoff[c0];
+    if (n > CH) {   // one huge support: grow buffers for it
+      amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2); amgd_free(tmp);
+      key = (uint64_t *)amgd_alloc(n * 8); key2 = (uint64_t *)amgd_alloc(n * 8);
+      val = (double *)amgd_alloc(n * 8); val2 = (double *)amgd_alloc(n * 8);
+      tb = 0;
+      HIPCK(rocprim::radix_sort_pairs(nullptr, tb, key, key2, val, val2, (size_t)n, 0, eb, s));
+      tmp = amgd_alloc(tb + 16);
+    }
+    uint64_t e0 = hro[c0], e1 = hro[c1];
+    if (n && e1 > e0) {
+      k_lmop_contrib<<<grid_for(e1 - e0, 256, 65536), 256, 0, s>>>(
+          erow, e0, e1, Wt->ro, Wt->col, Q, qoff, u, S->ro, S->col, S->nnz, coff, hcoff[c0], key,
+          val);
+      KCHECK();
+      size_t tb2 = 0;
+      HIPCK(rocprim::radix_sort_pairs(nullptr, tb2, key, key2, val, val2, (size_t)n, 0, eb, s));
+      if (tb2 > tb) { amgd_free(tmp); tmp = amgd_alloc(tb2 + 16); tb = tb2; }
+      HIPCK(rocprim::radix_sort_pairs(tmp, tb2, key, key2, val, val2, (size_t)n, 0, eb, s));
+      k_seg_accum<<<grid_for(n), 256, 0, s>>>(key2, val2, n, S->nnz, S->a);
+      KCHECK();
+    }
+    c0 = c1;
+  }
+  amgd_free(tmp); amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2);
+  amgd_free(erow); amgd_free(coff);
+}
+
+// ---------------------------------------------------------------------------
+// find_support pieces (amg_setup.c:1260).  Removed entries are zeroed in place
+// (equivalent for every later use: DESIGN.md "find_support").
+// ---------------------------------------------------------------------------
+__global__ void k_csc_gemv(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
+                           const double *a, const double *x, uint32_t n, double *z) {
+  GRID_STRIDE(c, n) {
+    double t = 0.0;
+    for (uint64_t q = tro[c]; q < tro[c + 1]; q++) {
+      double v = a[perm[q]];
+      t += x ? v * x[trow[q]] : v;
+    }
+    z[c] = t;
+  }
+}
+extern "C" void amgd_csc_gemv(const dcsr *Rt, const uint64_t *perm, const double *a,
+                              const double *x, double *z) {
+  if (Rt->rn)
+    k_csc_gemv<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, a, x, Rt->rn, z);
+  KCHECK();
+}
+__global__ void k_fs_select(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
+                            double *a, const double *rs, const double *w, const double *sumR,
+                            double thr, uint32_t n, uint32_t *si, uint32_t *sj, unsigned *cnt) {
+  GRID_STRIDE(c, n) {
+    if (!(w[c] > thr && sumR[c] != 0.)) continue;
+    double mx = -DBL_MAX;
+    uint32_t mi = 0;
+    uint64_t best = ~0ull;
+    for (uint64_t q = tro[c]; q < tro[c + 1]; q++) {
+      uint32_t i = trow[q];
+      double x = a[perm[q]] * rs[i];
+      if (x > mx) { mx = x; mi = i; best = q; }
+    }
+    unsigned p = atomicAdd(&cnt[0], 1u);
+    si[p] = mi;
+    sj[p] = (uint32_t)c;
+    if (best != ~0ull) { a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
+  }
+}
+extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
+                                   const double *rs, const double *w, const double *sumR,
+                                   double thr, uint32_t *sel_i, uint32_t *sel_j,
+                                   uint32_t *nremoved) {
+  unsigned *cnt = (unsigned *)amgd_alloc(8);
+  amgd_memset(cnt, 0, 8);
+  if (Rt->rn)
+    k_fs_select<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, Rl->a, rs, w, sumR,
+                                                         thr, Rt->rn, sel_i, sel_j, cnt);
+  KCHECK();
+  unsigned h[2];
+  amgd_d2h(h, cnt, 8);
+  amgd_free(cnt);
+  *nremoved = h[1];
+  return h[0];
+}
+
+// ---------------------------------------------------------------------------
+// expand_support pieces (amg_setup.c:907)
+// ---------------------------------------------------------------------------
+__global__ void k_bad_rows(const uint64_t *ro, const double *a, uint32_t rn, uint8_t *bad,
+                           unsigned *nbad) {
+  GRID_STRIDE(i, rn) {
+    uint8_t b = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++)
+      if (a[k] == 2.) { b = 1; break; }
+    bad[i] = b;
+    if (b) atomicAdd(nbad, 1u);
+  }
+}
+extern "C" uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad) {
+  uint8_t *bad = (uint8_t *)amgd_alloc((size_t)ns->rn + 1);
+  unsigned *c = (unsigned *)amgd_alloc(4);
+  amgd_memset(c, 0, 4);
+  if (ns->rn) k_bad_rows<<<grid_for(ns->rn), 256, 0, amgd_s()>>>(ns->ro, ns->a, ns->rn, bad, c);
+  unsigned h;
+  amgd_d2h(&h, c, 4);
+  amgd_free(c);
+  *nbad = h;
+  return bad;
+}
+
+// Per bad row (one wavefront): |X| entries ranked by descending value, stable
+// in column order (glibc qsort = merge sort, cmp_coo_v_revert amg_setup.c:1252);
+// S = running sum over ranks, V = sum/2, N = 1 + #{S - V < 0}; pick ranks < N.
+__global__ __launch_bounds__(64) void k_expand_pick(const uint64_t *ro, const uint32_t *col,
+                                                    const double *a, uint32_t rn,
+                                                    const uint8_t *bad, uint32_t *scol,
+                                                    double *sval, uint32_t *pj, uint64_t *cnt) {
+  const int lane = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < rn; i += gridDim.x) {
+    if (!bad[i]) { if (lane == 0) cnt[i] = 0; continue; }
+    uint64_t r0 = ro[i];
+    uint32_t L = (uint32_t)(ro[i + 1] - r0);
+    for (uint32_t e = lane; e < L; e += 64) {
+      double ve = fabs(a[r0 + e]);
+      uint32_t rank = 0;
+      for (uint32_t f = 0; f < L; f++) {
+        double vf = fabs(a[r0 + f]);
+        rank += (vf > ve) || (vf == ve && f < e);
+      }
+      scol[r0 + rank] = col[r0 + e];
+      sval[r0 + rank] = ve;
+    }
+    __syncthreads();
+    __shared__ uint32_t Nsh;
+    if (lane == 0) {
+      double tot = 0.0;
+      for (uint32_t p = 0; p < L; p++) if (sval[r0 + p] != 0.) tot += sval[r0 + p];
+      double V = tot * 0.5;
+      uint32_t c = 0;
+      if (V != 0.) {
+        double s = 0.0;
+        for (uint32_t p = 0; p < L; p++) {
+          if (sval[r0 + p] != 0.) s += sval[r0 + p];
+          if (s - V < 0) c++;
+        }
+      }
+      uint32_t N = c + 1;
+      Nsh = N < L ? N : L;
+      cnt[i] = Nsh;
+    }
+    __syncthreads();
+    uint32_t N = Nsh;
+    for (uint32_t p = lane; p < N; p += 64) pj[r0 + p] = scol[r0 + p];
+    __syncthreads();
+  }
+}
+__global__ void k_pick_compact(const uint64_t *ro, const uint64_t *off, const uint32_t *pj,
+                               uint32_t rn, uint32_t *oi, uint32_t *oj) {
+  GRID_STRIDE(i, rn) {
+    uint64_t n = off[i + 1] - off[i];
+    for (uint64_t t = 0; t < n; t++) {
+      oi[off[i] + t] = (uint32_t)i;
+      oj[off[i] + t] = pj[ro[i] + t];
+    }
+  }
+}
+extern "C" uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_t **pi,
+                                     uint32_t **pj) {
+  hipStream_t s = amgd_s();
+  uint32_t *scol = (uint32_t *)amgd_alloc(Xf->nnz * 4 + 4);
+  double *sval = (double *)amgd_alloc(Xf->nnz * 8 + 8);
+  uint32_t *tj = (uint32_t *)amgd_alloc(Xf->nnz * 4 + 4);
+  uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)Xf->rn + 1) * 8);
+  if (Xf->rn) {
+    int g = (int)std::min<uint32_t>(Xf->rn, 65536u);
+    k_expand_pick<<<g, 64, 0, s>>>(Xf->ro, Xf->col, Xf->a, Xf->rn, bad, scol, sval, tj, cnt);
+    KCHECK();
+  }
+  uint64_t n = amgd_scan_u64(cnt, Xf->rn);
+  uint32_t *oi = (uint32_t *)amgd_alloc(n * 4 + 4), *oj = (uint32_t *)amgd_alloc(n * 4 + 4);
+  if (Xf->rn) k_pick_compact<<<grid_for(Xf->rn), 256, 0, s>>>(Xf->ro, cnt, tj, Xf->rn, oi, oj);
+  KCHECK();
+  amgd_free(scol); amgd_free(sval); amgd_free(tj); amgd_free(cnt);
+  *pi = oi;
+  *pj = oj;
+  return n;
+}
+
+__global__ void k_binarize(double *a, uint64_t n, int mode) {
+  GRID_STRIDE(k, n) {
+    if (mode == 0) { if (a[k] == 2.) a[k] = 1.; }
+    else if (a[k] != 0.) a[k] = 1.;
+  }
+}
+extern "C" void amgd_skel_binarize(dcsr *A, int mode) {
+  if (A->nnz) k_binarize<<<grid_for(A->nnz), 256, 0, amgd_s()>>>(A->a, A->nnz, mode);
+}
+// amg_setup.c:821-837: scale entries whose COLUMN equals the row index
+__global__ void k_scale_diag_match(const uint64_t *ro, const uint32_t *col, double *a, uint32_t rn,
+                                   const double *v, const double *wuc) {
+  GRID_STRIDE(i, rn) {
+    if (wuc[i] != 0.)
+      for (uint64_t j = ro[i]; j < ro[i + 1]; j++)
+        if (col[j] == i) {
+          double vw = v[i] / wuc[i];
+          a[j] = vw * a[j];
+        }
+  }
+}
+extern "C" void amgd_scale_diag_match(dcsr *W, const double *v, const double *wuc) {
+  if (W->rn) k_scale_diag_match<<<grid_for(W->rn), 256, 0, amgd_s()>>>(W->ro, W->col, W->a, W->rn, v, wuc);
+}

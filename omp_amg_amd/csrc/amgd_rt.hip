@@ -1,0 +1,503 @@
+// amgd_rt.hip -- runtime for the MI355X AMG setup: stream, caching HBM pool,
+// copies, event timers, scans (rocPRIM), deterministic reductions.
+//
+// Reductions are two-stage with a fixed grid, so every result is run-to-run
+// reproducible; they are NOT the reference's left-to-right sums (amg_setup.c:3193),
+// which is the one documented source of last-bit differences (DESIGN.md "Parity").
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <rocprim/device/device_scan.hpp>
+
+#include <cfloat>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+#include <chrono>
+
+#include "amgd.h"
+#include "amgd_dev.h"
+
+static hipStream_t g_stream = nullptr;
+static bool g_inited = false;
+static char g_err[512];
+
+void amgd_check(hipError_t e, const char *what, const char *file, int line) {
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof g_err, "%s failed at %s:%d: %s", what, file, line, hipGetErrorString(e));
+    fprintf(stderr, "omp_amg_amd: %s\n", g_err);
+    fflush(stderr);
+    abort();
+  }
+}
+
+extern "C" const char *amgd_last_error(void) { return g_err; }
+
+// The reference's Lanczos start vector comes from the process-wide libc rand()
+// stream (amg_setup.c:2447).  The HIP runtime may draw from that stream while it
+// initialises, so runtime start-up runs on a scratch random(3) state and the
+// caller's state is restored untouched afterwards.
+static char g_rand_scratch[256];
+extern "C" int amgd_rt_init(int device) {
+  if (g_inited) return 0;
+  char *saved = initstate(12345u, g_rand_scratch, sizeof g_rand_scratch);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    snprintf(g_err, sizeof g_err, "no HIP device visible");
+    setstate(saved);
+    return -1;
+  }
+  HIPCK(hipSetDevice(device));
+  HIPCK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+  // touch the device once so lazy code-object loading also happens here
+  void *p = nullptr;
+  HIPCK(hipMalloc(&p, 256));
+  HIPCK(hipMemsetAsync(p, 0, 256, g_stream));
+  HIPCK(hipStreamSynchronize(g_stream));
+  HIPCK(hipFree(p));
+  g_inited = true;
+  setstate(saved);
+  return 0;
+}
+
+hipStream_t amgd_s() {
+  if (!g_inited && amgd_rt_init(0) != 0) {
+    fprintf(stderr, "omp_amg_amd: HIP runtime unavailable: %s\n", g_err);
+    abort();
+  }
+  return g_stream;
+}
+extern "C" void *amgd_stream(void) { return (void *)amgd_s(); }
+extern "C" void amgd_set_stream(void *s) { amgd_s(); g_stream = (hipStream_t)s; }
+
+// ---------------- caching pool ----------------
+// hipFree synchronises the device and hipMalloc costs tens of us; the setup
+// allocates thousands of short-lived buffers per level, so freed blocks are
+// cached by size and reused (first fit within 2x).
+struct Blk { void *p; size_t sz; };
+static std::vector<Blk> g_free, g_used;
+static size_t g_inuse = 0, g_peak = 0;
+
+extern "C" void *amgd_alloc(size_t bytes) {
+  amgd_s();
+  size_t sz = (bytes + 511) & ~(size_t)511;
+  if (sz == 0) sz = 512;
+  int best = -1;
+  for (int i = 0; i < (int)g_free.size(); i++)
+    if (g_free[i].sz >= sz && g_free[i].sz <= 2 * sz + (1 << 20) &&
+        (best < 0 || g_free[i].sz < g_free[best].sz)) best = i;
+  Blk b;
+  if (best >= 0) {
+    b = g_free[best];
+    g_free[best] = g_free.back();
+    g_free.pop_back();
+  } else {
+    b.sz = sz;
+    hipError_t e = hipMalloc(&b.p, sz);
+    if (e != hipSuccess) {
+      // release the cache and retry once before failing loudly
+      (void)hipGetLastError();
+      amgd_pool_release();
+      HIPCK(hipMalloc(&b.p, sz));
+    }
+  }
+  g_used.push_back(b);
+  g_inuse += b.sz;
+  if (g_inuse > g_peak) g_peak = g_inuse;
+  return b.p;
+}
+
+extern "C" void amgd_free(void *p) {
+  if (!p) return;
+  for (size_t i = g_used.size(); i-- > 0;)
+    if (g_used[i].p == p) {
+      g_inuse -= g_used[i].sz;
+      g_free.push_back(g_used[i]);
+      g_used[i] = g_used.back();
+      g_used.pop_back();
+      return;
+    }
+  fprintf(stderr, "omp_amg_amd: amgd_free of unknown pointer %p\n", p);
+  abort();
+}
+
+extern "C" void amgd_pool_release(void) {
+  if (!g_inited) return;
+  HIPCK(hipStreamSynchronize(g_stream));
+  for (auto &b : g_free) HIPCK(hipFree(b.p));
+  g_free.clear();
+}
+extern "C" size_t amgd_pool_bytes_in_use(void) { return g_inuse; }
+extern "C" size_t amgd_pool_peak_bytes(void) { return g_peak; }
+
+extern "C" void amgd_h2d(void *d, const void *h, size_t n) {
+  if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, amgd_s()));
+  HIPCK(hipStreamSynchronize(g_stream));
+}
+extern "C" void amgd_d2h(void *h, const void *d, size_t n) {
+  if (n) HIPCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(g_stream));
+}
+extern "C" void amgd_d2d(void *d, const void *s, size_t n) {
+  if (n) HIPCK(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, amgd_s()));
+}
+extern "C" void amgd_memset(void *d, int v, size_t n) {
+  if (n) HIPCK(hipMemsetAsync(d, v, n, amgd_s()));
+}
+extern "C" void amgd_sync(void) { HIPCK(hipStreamSynchronize(amgd_s())); }
+extern "C" double amgd_wtime(void) {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+// ---------------- event timers ----------------
+#define NTIMERS 16
+static hipEvent_t g_t0[NTIMERS], g_t1[NTIMERS];
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pend[NTIMERS];
+static double g_acc[NTIMERS];
+static bool g_tinit = false;
+static void tinit() {
+  if (g_tinit) return;
+  for (int i = 0; i < NTIMERS; i++) g_acc[i] = 0;
+  g_tinit = true;
+}
+extern "C" void amgd_timer_start(int s) {
+  tinit();
+  hipEvent_t a;
+  HIPCK(hipEventCreate(&a));
+  HIPCK(hipEventRecord(a, amgd_s()));
+  g_t0[s] = a;
+}
+extern "C" void amgd_timer_stop(int s) {
+  hipEvent_t b;
+  HIPCK(hipEventCreate(&b));
+  HIPCK(hipEventRecord(b, amgd_s()));
+  g_pend[s].push_back({g_t0[s], b});
+}
+extern "C" double amgd_timer_ms(int s) {
+  tinit();
+  for (auto &pr : g_pend[s]) {
+    HIPCK(hipEventSynchronize(pr.second));
+    float ms = 0;
+    HIPCK(hipEventElapsedTime(&ms, pr.first, pr.second));
+    g_acc[s] += ms;
+    HIPCK(hipEventDestroy(pr.first));
+    HIPCK(hipEventDestroy(pr.second));
+  }
+  g_pend[s].clear();
+  return g_acc[s];
+}
+extern "C" void amgd_timer_reset(void) {
+  tinit();
+  for (int i = 0; i < NTIMERS; i++) { (void)amgd_timer_ms(i); g_acc[i] = 0; }
+}
+
+// ---------------- dcsr helpers ----------------
+extern "C" dcsr *dcsr_new(uint32_t rn, uint32_t cn, uint64_t nnz) {
+  dcsr *A = (dcsr *)malloc(sizeof(dcsr));
+  A->rn = rn; A->cn = cn; A->nnz = nnz;
+  A->ro = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  A->col = (uint32_t *)amgd_alloc(nnz * 4 + 4);
+  A->a = (double *)amgd_alloc(nnz * 8 + 8);
+  return A;
+}
+extern "C" void dcsr_free(dcsr **A) {
+  if (!A || !*A) return;
+  amgd_free((*A)->ro); amgd_free((*A)->col); amgd_free((*A)->a);
+  free(*A);
+  *A = nullptr;
+}
+extern "C" dcsr *dcsr_copy(const dcsr *A) {
+  dcsr *B = dcsr_new(A->rn, A->cn, A->nnz);
+  amgd_d2d(B->ro, A->ro, ((size_t)A->rn + 1) * 8);
+  amgd_d2d(B->col, A->col, A->nnz * 4);
+  amgd_d2d(B->a, A->a, A->nnz * 8);
+  return B;
+}
+extern "C" dcsr *dcsr_empty_like_pattern(const dcsr *A) {
+  dcsr *B = dcsr_new(A->rn, A->cn, A->nnz);
+  amgd_d2d(B->ro, A->ro, ((size_t)A->rn + 1) * 8);
+  amgd_d2d(B->col, A->col, A->nnz * 4);
+  return B;
+}
+
+// ---------------- scans ----------------
+template <typename T>
+static T scan_impl(T *counts, uint64_t n) {
+  hipStream_t s = amgd_s();
+  T *tmpout = (T *)amgd_alloc((n + 1) * sizeof(T));
+  size_t tb = 0;
+  HIPCK(rocprim::exclusive_scan(nullptr, tb, counts, tmpout, (T)0, (size_t)(n + 1),
+                                rocprim::plus<T>(), s));
+  void *tmp = amgd_alloc(tb + 16);
+  // counts[n] must be a valid slot: callers allocate n+1; set it to 0 first
+  HIPCK(hipMemsetAsync(counts + n, 0, sizeof(T), s));
+  HIPCK(rocprim::exclusive_scan(tmp, tb, counts, tmpout, (T)0, (size_t)(n + 1),
+                                rocprim::plus<T>(), s));
+  HIPCK(hipMemcpyAsync(counts, tmpout, (n + 1) * sizeof(T), hipMemcpyDeviceToDevice, s));
+  T total;
+  HIPCK(hipMemcpyAsync(&total, tmpout + n, sizeof(T), hipMemcpyDeviceToHost, s));
+  HIPCK(hipStreamSynchronize(s));
+  amgd_free(tmp);
+  amgd_free(tmpout);
+  return total;
+}
+extern "C" uint64_t amgd_scan_u64(uint64_t *c, uint64_t n) { return scan_impl<uint64_t>(c, n); }
+extern "C" uint32_t amgd_scan_u32(uint32_t *c, uint64_t n) { return scan_impl<uint32_t>(c, n); }
+
+__global__ void k_mask_to_u32(const uint8_t *m, uint32_t n, uint32_t *o) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    o[i] = m[i] ? 1u : 0u;
+}
+__global__ void k_rank_fix(const uint8_t *m, uint32_t n, uint32_t *o) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (!m[i]) o[i] = 0xffffffffu;
+}
+extern "C" uint32_t amgd_mask_rank(const uint8_t *mask, uint32_t n, uint32_t *map) {
+  // map must hold n+1 entries
+  k_mask_to_u32<<<grid_for(n), 256, 0, amgd_s()>>>(mask, n, map);
+  uint32_t tot = amgd_scan_u32(map, n);
+  k_rank_fix<<<grid_for(n), 256, 0, amgd_s()>>>(mask, n, map);
+  return tot;
+}
+
+// ---------------- deterministic reductions ----------------
+// Stage 1: RED_BLOCKS fixed blocks, grid-stride partial sums in a fixed order;
+// stage 2: one block reduces the partials.  Same n -> same bits every run.
+#define RED_BLOCKS 1024
+#define RED_THREADS 256
+
+template <typename Op>
+__device__ double block_reduce(double v, Op op) {
+  __shared__ double sh[RED_THREADS / 64];
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_down(v, o, 64));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    v = threadIdx.x < RED_THREADS / 64 ? sh[threadIdx.x] : 0.0;
+    for (int o = 32; o > 0; o >>= 1) {
+      double u = __shfl_down(v, o, 64);
+      if (threadIdx.x + o < RED_THREADS / 64) v = op(v, u);
+    }
+  }
+  return v;
+}
+struct AddOp { __device__ double operator()(double a, double b) const { return a + b; } };
+
+__global__ void k_dot_partial(const double *a, const double *b, uint64_t n, double *part) {
+  double s = 0.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    s += a[i] * (b ? b[i] : a[i]);
+  s = block_reduce(s, AddOp());
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ void k_dot3_partial(const double *M, const double *b, uint64_t n, double *part) {
+  double s = 0.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    s += (M[i] * b[i]) * b[i];
+  s = block_reduce(s, AddOp());
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+__global__ void k_sum_final(const double *part, int np, double *out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) s += part[i];
+  s = block_reduce(s, AddOp());
+  if (threadIdx.x == 0) *out = s;
+}
+static double *g_red = nullptr;  // RED_BLOCKS partials + scalars
+static double *g_red_h = nullptr;
+static double *red_buf() {
+  if (!g_red) {
+    HIPCK(hipMalloc(&g_red, (RED_BLOCKS * 2 + 64) * sizeof(double)));
+    HIPCK(hipHostMalloc(&g_red_h, 64 * sizeof(double)));
+  }
+  return g_red;
+}
+static int red_grid(uint64_t n) {
+  uint64_t b = (n + RED_THREADS - 1) / RED_THREADS;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(b, RED_BLOCKS));
+}
+static double sum_finish(int nb) {
+  double *p = red_buf();
+  k_sum_final<<<1, RED_THREADS, 0, amgd_s()>>>(p, nb, p + 2 * RED_BLOCKS);
+  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 8, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  return g_red_h[0];
+}
+// Reference-order ("exact") dot products.  The reference sums left to right
+// (vv_dot amg_setup.c:3193, norm2 :3309, pcg's rho_0 :2265-2267).  Its
+// constraint solve runs PCG on an indefinite, non-symmetric S whenever
+// sp_add lands off-pattern (DESIGN.md "Reference UB"); there the iteration is
+// chaotic and only the reference's own summation order reproduces it.  In
+// exact mode (default) one wavefront carries the sequential sum while three
+// others stage the next tile of products through LDS: latency-bound
+// (one dependent f64 add per element), bit-identical to the reference.
+#define SEQ_TILE 2048
+template <int MODE>   // 0: a.b  1: a.a  2: (M.*b).*b
+__global__ __launch_bounds__(256) void k_dot_seq(const double *a, const double *b, uint64_t n,
+                                                 double *out) {
+  __shared__ double buf[2][SEQ_TILE];
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  uint64_t ntile = (n + SEQ_TILE - 1) / SEQ_TILE;
+  // prologue: stage tile 0 with every thread
+  for (uint64_t j = tid; j < SEQ_TILE && j < n; j += 256) {
+    double x = a[j];
+    buf[0][j] = MODE == 0 ? x * b[j] : MODE == 1 ? x * x : (x * b[j]) * b[j];
+  }
+  __syncthreads();
+  for (uint64_t t = 0; t < ntile; t++) {
+    int cur = (int)(t & 1);
+    uint64_t base = t * SEQ_TILE;
+    if (tid < 64) {
+      if (tid == 0) {
+        uint64_t m = n - base < SEQ_TILE ? n - base : SEQ_TILE;
+        const double *p = buf[cur];
+        for (uint64_t j = 0; j < m; j++) s += p[j];
+      }
+    } else if (t + 1 < ntile) {
+      uint64_t nb = base + SEQ_TILE;
+      for (uint64_t j = tid - 64; j < SEQ_TILE; j += 192) {
+        uint64_t i = nb + j;
+        if (i < n) {
+          double x = a[i];
+          buf[cur ^ 1][j] = MODE == 0 ? x * b[i] : MODE == 1 ? x * x : (x * b[i]) * b[i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *out = s;
+}
+static int g_exact = -1;
+extern "C" void amgd_set_exact(int on) { g_exact = on ? 1 : 0; }
+extern "C" int amgd_get_exact(void) {
+  if (g_exact < 0) {
+    const char *e = getenv("AMGD_FAST_DOTS");
+    g_exact = (e && *e && *e != '0') ? 0 : 1;
+  }
+  return g_exact;
+}
+static double seq_finish() {
+  double *p = red_buf();
+  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 8, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  return g_red_h[0];
+}
+extern "C" double amgd_dot(const double *a, const double *b, uint64_t n) {
+  if (n == 0) return 0.0;
+  if (amgd_get_exact()) {
+    if (b) k_dot_seq<0><<<1, 256, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
+    else k_dot_seq<1><<<1, 256, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
+    return seq_finish();
+  }
+  int nb = red_grid(n);
+  k_dot_partial<<<nb, RED_THREADS, 0, amgd_s()>>>(a, b, n, red_buf());
+  return sum_finish(nb);
+}
+extern "C" double amgd_norm2(const double *a, uint64_t n) { return sqrt(amgd_dot(a, nullptr, n)); }
+extern "C" double amgd_dot3(const double *M, const double *b, uint64_t n) {
+  if (n == 0) return 0.0;
+  if (amgd_get_exact()) {
+    k_dot_seq<2><<<1, 256, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
+    return seq_finish();
+  }
+  int nb = red_grid(n);
+  k_dot3_partial<<<nb, RED_THREADS, 0, amgd_s()>>>(M, b, n, red_buf());
+  return sum_finish(nb);
+}
+
+// first argmax: larger value wins, ties -> smaller index (extr_op, amg_setup.c:3281)
+struct VI { double v; uint64_t i; };
+__device__ inline VI vi_best(VI a, VI b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+__global__ void k_argmax_partial(const double *a, const uint64_t *ia, uint64_t n, double *pv,
+                                 uint64_t *pi) {
+  VI best{-DBL_MAX, ~0ull};
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    VI c{a[i], ia ? ia[i] : i};
+    best = vi_best(best, c);
+  }
+  __shared__ double sv[RED_THREADS];
+  __shared__ uint64_t si[RED_THREADS];
+  sv[threadIdx.x] = best.v; si[threadIdx.x] = best.i;
+  __syncthreads();
+  for (int o = RED_THREADS / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      VI x{sv[threadIdx.x], si[threadIdx.x]}, y{sv[threadIdx.x + o], si[threadIdx.x + o]};
+      VI r = vi_best(x, y);
+      sv[threadIdx.x] = r.v; si[threadIdx.x] = r.i;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { pv[blockIdx.x] = sv[0]; pi[blockIdx.x] = si[0]; }
+}
+extern "C" double amgd_max_first(const double *a, uint64_t n, uint64_t *idx) {
+  if (n == 0) { if (idx) *idx = 0; return -DBL_MAX; }
+  int nb = red_grid(n);
+  double *p = red_buf();
+  uint64_t *pi = (uint64_t *)(p + RED_BLOCKS);
+  k_argmax_partial<<<nb, RED_THREADS, 0, amgd_s()>>>(a, nullptr, n, p, pi);
+  k_argmax_partial<<<1, RED_THREADS, 0, amgd_s()>>>(p, pi, nb, p + 2 * RED_BLOCKS,
+                                                    (uint64_t *)(p + 2 * RED_BLOCKS + 1));
+  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 16, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  uint64_t gi;
+  memcpy(&gi, &g_red_h[1], 8);
+  if (idx) *idx = gi;
+  return g_red_h[0];
+}
+
+__global__ void k_count_gt(const double *a, uint64_t n, double thr, double *pc, double *pm) {
+  double c = 0.0, m = 0.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    c += a[i] > thr ? 1.0 : 0.0;
+    m = a[i] > m ? a[i] : m;
+  }
+  c = block_reduce(c, AddOp());
+  struct MaxOp { __device__ double operator()(double x, double y) const { return x > y ? x : y; } };
+  __syncthreads();
+  m = block_reduce(m, MaxOp());
+  if (threadIdx.x == 0) { pc[blockIdx.x] = c; pm[blockIdx.x] = m; }
+}
+extern "C" uint64_t amgd_count_gt(const double *a, uint64_t n, double thr, double *maxv) {
+  if (n == 0) { if (maxv) *maxv = 0; return 0; }
+  int nb = red_grid(n);
+  double *p = red_buf();
+  k_count_gt<<<nb, RED_THREADS, 0, amgd_s()>>>(a, n, thr, p, p + RED_BLOCKS);
+  std::vector<double> hc(nb), hm(nb);
+  HIPCK(hipMemcpyAsync(hc.data(), p, nb * 8, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipMemcpyAsync(hm.data(), p + RED_BLOCKS, nb * 8, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  double c = 0, m = 0;
+  for (int i = 0; i < nb; i++) { c += hc[i]; m = hm[i] > m ? hm[i] : m; }
+  if (maxv) *maxv = m;
+  return (uint64_t)c;
+}
+
+// ||A - I||_F^2 over stored values, I subtracted at the first diagonal entry
+__global__ void k_fro_rows(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
+                           double *part) {
+  double s = 0.0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < rn; i += gridDim.x * blockDim.x) {
+    bool done = false;
+    for (uint64_t j = ro[i]; j < ro[i + 1]; j++) {
+      double v = a[j];
+      if (!done && col[j] == i) { v = v - 1.0; done = true; }
+      s += v * v;
+    }
+  }
+  s = block_reduce(s, AddOp());
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+extern "C" double amgd_fro_minus_eye(const dcsr *A) {
+  int nb = red_grid(A->rn);
+  k_fro_rows<<<nb, RED_THREADS, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, red_buf());
+  return sum_finish(nb);
+}

@@ -1,0 +1,962 @@
+/*
+ * amgd_setup.c -- host driver (C) of the MI355X-native AMG setup.
+ *
+ * Follows the reference setup loop (nicooff/omp_amg amg_setup.c:60-400) level
+ * by level; every array operation is a HIP kernel behind the thin C ABI of
+ * amgd.h, all data stays in HBM, and the host only steers: it reads back the
+ * scalars that decide control flow (coarsening norm bound, Lanczos alpha/beta,
+ * PCG rho, skeleton-expansion counts) and runs the small tridiagonal
+ * eigen-solve of Lanczos (tdeig, amg_setup.c:2712) on the CPU.
+ *
+ * Parity contract (DESIGN.md "Parity"): integer structure -- C/F sets, ids,
+ * every CSR pattern -- is identical to the reference; values agree to the last
+ * bit except where a global dot product feeds them (PCG / Lanczos use a
+ * fixed-order tree reduction on the GPU, the reference sums left to right).
+ *
+ * Compiled with -ffp-contract=off so host arithmetic (chebsim, tdeig,
+ * threshold expressions) rounds exactly like the reference's ISO-C build.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "amgd.h"
+#include "amg_setup.h"
+#include "crs.h"
+#include "omp_amg_amd.h"
+
+#define API __attribute__((visibility("default")))
+
+static double *dalloc(uint64_t n) { return (double *)amgd_alloc(n * 8 + 8); }
+static double *dones(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 1.0); return p; }
+static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0); return p; }
+#define SWAPD(a, b) do { double *t_ = (a); (a) = (b); (b) = t_; } while (0)
+
+static amgd_stats g_st;
+static uint64_t g_ub;                  /* reference-undefined events (non-termination) */
+static int g_verbose = -1;
+static int verbose(void) {
+  if (g_verbose < 0) { const char *e = getenv("AMGD_VERBOSE"); g_verbose = e && *e && *e != '0'; }
+  return g_verbose;
+}
+
+/* debug dumps of intermediates (AMGD_DUMP=<dir>), compared against the oracle's */
+static int g_lvl = 0, g_it = 0;
+static void dump_dev(const char *name, const void *d, size_t bytes) {
+  const char *dir = getenv("AMGD_DUMP");
+  if (!dir || !*dir) return;
+  char fn[512];
+  snprintf(fn, sizeof fn, "%s/L%d_it%d_%s.bin", dir, g_lvl, g_it, name);
+  void *h = malloc(bytes + 8);
+  amgd_d2h(h, d, bytes);
+  FILE *f = fopen(fn, "wb");
+  if (f) { fwrite(h, 1, bytes, f); fclose(f); }
+  free(h);
+}
+static void dump_csr(const char *name, const dcsr *A) {
+  char n2[256];
+  snprintf(n2, sizeof n2, "%s_ro", name); dump_dev(n2, A->ro, ((size_t)A->rn + 1) * 8);
+  snprintf(n2, sizeof n2, "%s_col", name); dump_dev(n2, A->col, A->nnz * 4);
+  snprintf(n2, sizeof n2, "%s_a", name); dump_dev(n2, A->a, A->nnz * 8);
+}
+
+/* ------------------------------------------------------------------------ */
+/* coarsen (amg_setup.c:2737)                                                */
+/* ------------------------------------------------------------------------ */
+static dcsr *strength(const dcsr *A) {
+  /* D = 1/sqrt(diag(A)); S = |D A D|; S = S - diag(S)  (amg_setup.c:2741-2758) */
+  double *D = dalloc(A->cn);
+  amgd_diag(A, D);
+  amgd_vunary(D, A->rn, AMGD_V_SQRT);
+  amgd_vunary(D, A->rn, AMGD_V_INV);
+  dcsr *S = dcsr_copy(A);
+  amgd_diag_op(S, D, AMGD_DMULT);
+  amgd_diag_op(S, D, AMGD_MULTD);
+  amgd_vals_abs(S);
+  amgd_diag(S, D);
+  amgd_diag_op(S, D, AMGD_DMINUS);
+  amgd_free(D);
+  return S;
+}
+
+static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
+  uint32_t n = A->cn;
+  dcsr *S = strength(A);
+  dcsr *St = amgd_transpose(S, NULL);
+  uint8_t *vf = (uint8_t *)amgd_alloc(n + 1), *mask = (uint8_t *)amgd_alloc(n + 1);
+  double *vfd = dones(n), *g = dalloc(n), *w1 = dalloc(n), *w2 = dalloc(n), *tmp = dalloc(n);
+  double *w = dalloc(n), *x = dalloc(n), *m = dalloc(n), *amax = dalloc(n);
+  uint32_t *anyvc = (uint32_t *)amgd_alloc(4);
+  amgd_memset(vc, 0, n);
+  amgd_memset(vf, 1, n);
+  amgd_memset(anyvc, 0, 4);
+  int it = 0;
+  for (;;) {
+    it++;
+    amgd_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);      /* g  = vf.*(S*vf)   */
+    amgd_spmv(S, g, w1, 0.0, NULL, 1.0, vf);       /* w1 = vf.*(S*g)    */
+    amgd_spmv(S, w1, w2, 0.0, NULL, 1.0, vf);      /* w2 = vf.*(S*w1)   */
+    amgd_spmv(S, w2, tmp, 0.0, NULL, 1.0, vf);     /* w2 = vf.*(S*w2)   */
+    SWAPD(w2, tmp);
+    amgd_coarsen_w(w1, w2, w, n);                  /* w = (1./w1).*w2   */
+    uint64_t mi = 0;
+    double w1m = amgd_max_first(w1, n, &mi), wm = amgd_max_first(w, n, NULL);
+    double b = (w1m < wm) ? sqrt(w1m) : sqrt(wm);
+    if (b <= ctol) {
+      uint32_t any = 0;
+      amgd_d2h(&any, anyvc, 4);
+      if (!any) { uint8_t one = 1; amgd_h2d(vc + mi, &one, 1); }
+      if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
+      break;
+    }
+    amgd_coarsen_mask1(w, ctol * ctol, g, mask, x, n);
+    amgd_mat_max(S, St, vf, x, 0.1, amax, m);      /* m = mat_max(S,vf,mask.*g)  */
+    amgd_coarsen_mask2(g, m, mask, x, n);
+    amgd_mat_max(S, St, vf, x, 0.1, amax, m);      /* m = mat_max(S,vf,mask.*id) */
+    amgd_coarsen_mask3(m, mask, vc, vf, vfd, n, anyvc);
+  }
+  dcsr_free(&S); dcsr_free(&St);
+  amgd_free(vf); amgd_free(mask); amgd_free(vfd); amgd_free(g); amgd_free(w1); amgd_free(w2);
+  amgd_free(tmp); amgd_free(w); amgd_free(x); amgd_free(m); amgd_free(amax); amgd_free(anyvc);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Lanczos + tdeig (amg_setup.c:2435-2726); tdeig runs on the host           */
+/* ------------------------------------------------------------------------ */
+#define EPS (128 * DBL_EPSILON)
+static double sum_3(double a, double b, double c) {
+  if ((a >= 0 && b >= 0) || (a <= 0 && b <= 0)) return (a + b) + c;
+  if ((a >= 0 && c >= 0) || (a <= 0 && c <= 0)) return (a + c) + b;
+  return a + (b + c);
+}
+static double rat_root(double a, double b, double c, double sign) {
+  double bh = (fabs(b) + sqrt(b * b + 4 * a * c)) / 2;
+  return sign * (b * sign <= 0 ? bh / a : c / bh);
+}
+/* secular-equation root in [d[ri], d[ri+1]] (amg_setup.c:2638) */
+static double sec_root(double *y, const double *d, const double *v, int ri, int n) {
+  double dl = d[ri], dr = d[ri + 1], L = dr - dl, x0l = L / 2, x0r = -L / 2;
+  double tol = L;
+  if (fabs(dl) > tol) tol = fabs(dl);
+  if (fabs(dr) > tol) tol = fabs(dr);
+  tol *= EPS;
+  for (;;) {
+    double al = 0, ar = 0, cl = 0, cr = 0, bln = 0, blp = 0, brn = 0, brp = 0, fn = 0, fp = 0;
+    double lambda0, lambda;
+    if (fabs(x0l) == 0 || x0l < 0) { *y = 0; return dl; }
+    if (fabs(x0r) == 0 || x0r > 0) { *y = 0; return dr; }
+    lambda0 = fabs(x0l) < fabs(x0r) ? dl + x0l : dr + x0r;
+    for (int i = 1; i <= ri; ++i) {
+      double den = (d[i] - dl) - x0l, fac = v[i] / den, num = sum_3(d[i], -dr, -2 * x0r);
+      fn += v[i] * fac; fac *= fac; ar += fac;
+      if (num > 0) brp += fac * num; else brn += fac * num;
+      bln += fac * (d[i] - dl);
+      cl += fac * x0l * x0l;
+    }
+    for (int i = ri + 1; i <= n; ++i) {
+      double den = (d[i] - dr) - x0r, fac = v[i] / den, num = sum_3(d[i], -dl, -2 * x0l);
+      fp += v[i] * fac; fac *= fac; al += fac;
+      if (num > 0) blp += fac * num; else bln += fac * num;
+      brp += fac * (d[i] - dr);
+      cr += fac * x0r * x0r;
+    }
+    if (lambda0 > 0) fp += lambda0; else fn += lambda0;
+    if (v[0] < 0) fp -= v[0], blp -= v[0], brp -= v[0];
+    else fn -= v[0], bln -= v[0], brn -= v[0];
+    if (fp + fn > 0) {
+      x0l = rat_root(1 + al, sum_3(dl, blp, bln), cl, 1);
+      lambda = dl + x0l; x0r = x0l - L;
+    } else {
+      x0r = rat_root(1 + ar, sum_3(dr, brp, brn), cr, -1);
+      lambda = dr + x0r; x0l = x0r + L;
+    }
+    if (fabs(lambda - lambda0) < tol) {
+      double ty = 0, fac;
+      for (int i = 1; i <= ri; ++i) fac = v[i] / ((d[i] - dl) - x0l), ty += fac * fac;
+      for (int i = ri + 1; i <= n; ++i) fac = v[i] / ((d[i] - dr) - x0r), ty += fac * fac;
+      *y = 1 / sqrt(1 + ty);
+      return lambda;
+    }
+  }
+}
+static void tdeig(double *lambda, double *y, double *d, const double *v, int n) {
+  double v1 = 0, mn = v[0], mx = v[0];
+  for (int i = 1; i <= n; ++i) {
+    double vi = fabs(v[i]), a = d[i] - vi, b = d[i] + vi;
+    v1 += vi;
+    if (a < mn) mn = a;
+    if (b > mx) mx = b;
+  }
+  d[0] = v[0] - v1 < mn ? v[0] - v1 : mn;
+  d[n + 1] = v[0] + v1 > mx ? v[0] + v1 : mx;
+  for (int i = 0; i <= n; ++i) lambda[i] = sec_root(&y[i], d, v, i, n);
+}
+
+#define KMAX 299
+static uint32_t lanczos(const dcsr *A, double *out) {
+  uint32_t rn = A->rn;
+  /* start vector: libc rand()/RAND_MAX, like the reference (amg_setup.c:2445-2448),
+     so the process-wide rand() stream advances identically */
+  double *rh = (double *)malloc((size_t)rn * 8 + 8);
+  for (uint32_t i = 0; i < rn; i++) rh[i] = (double)rand() / (double)RAND_MAX;
+  double *r = dalloc(rn);
+  amgd_h2d(r, rh, (size_t)rn * 8);
+  free(rh);
+  double l[KMAX + 2], y[KMAX + 2], d[KMAX + 2], v[KMAX + 2];
+  double beta = amgd_norm2(r, rn), beta2 = beta * beta, change;
+  beta = sqrt(beta2);
+  uint32_t k = 0;
+  {
+    double fr = amgd_fro_minus_eye(A), fro = sqrt(fr), fro2 = fro * fro;
+    fro = sqrt(fro2);
+    if (fro < 1e-11) { l[0] = 1; l[1] = 1; y[0] = 0; y[1] = 0; k = 2; change = 0.0; }
+    else change = 1.0;
+  }
+  if (rn == 1) {
+    double a00;
+    amgd_d2h(&a00, A->a, 8);
+    l[0] = a00; l[1] = a00; y[0] = 0; y[1] = 0; k = 2; change = 0.0;
+  }
+  double *qk = dzeros(A->cn), *qkm1 = dalloc(rn), *Aqk = dalloc(rn);
+  while (k < KMAX && (change > 1e-5 || y[0] > 1e-3 || y[k - 1] > 1e-3)) {
+    k++;
+    amgd_lanczos_step(r, 1. / beta, qk, qkm1, rn);           /* qkm1 = qk; qk = r/beta */
+    amgd_spmv(A, qk, Aqk, 0, NULL, 1, NULL);
+    double alpha = amgd_dot(qk, Aqk, rn);
+    amgd_lanczos_resid(r, Aqk, qk, alpha, qkm1, beta, rn);    /* r = Aqk - a qk - b qkm1 */
+    if (k == 1) { l[0] = alpha; y[0] = 1; }
+    else {
+      double l0 = l[0], lkm2 = l[k - 2];
+      d[0] = 0;
+      for (uint32_t i = 1; i < k; i++) d[i] = l[i - 1];
+      d[k] = 0;
+      v[0] = alpha;
+      for (uint32_t i = 1; i < k; i++) v[i] = beta * y[i - 1];
+      tdeig(l, y, d, v, (int)k - 1);
+      change = fabs(l0 - l[0]) + fabs(lkm2 - l[k - 1]);
+    }
+    beta = amgd_norm2(r, rn);
+    beta2 = beta * beta;
+    beta = sqrt(beta2);
+    if (beta == 0) break;
+  }
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < k; i++) if (y[i] < 0.01) out[n++] = l[i];
+  amgd_free(r); amgd_free(qk); amgd_free(qkm1); amgd_free(Aqk);
+  return n;
+}
+
+static void chebsim(double *m, double *c, double rho, double tol) {   /* amg_setup.c:2412 */
+  double alpha = 0.25 * rho * rho, cp = 1, gamma = 1, d, cn;
+  *m = 1; *c = rho;
+  while (*c > tol) {
+    *m += 1;
+    d = alpha * (1 + gamma);
+    gamma = d / (1 - d);
+    cn = (1 + gamma) * rho * (*c) - gamma * cp;
+    cp = *c; *c = cn;
+  }
+}
+
+/* PCG (amg_setup.c:2242): z = M.*r, at most min(n,100) iterations; r is overwritten */
+static uint32_t pcg(double *x, const dcsr *A, double *r, const double *M, double tol, const double *b) {
+  uint32_t rn = A->rn;
+  amgd_vfill(x, rn, 0.0);
+  if (rn == 0) return 0;
+  double *p = dzeros(A->cn), *z = dalloc(rn), *w = dalloc(rn);
+  amgd_vmul_dot_prep(z, M, r, rn);
+  double rho = amgd_dot(r, z, rn);
+  double rho_0 = amgd_dot3(M, b, rn);
+  double rho_stop = tol * tol * rho_0, rho_old = 1, alpha, beta;
+  uint32_t n = rn <= 100 ? rn : 100, k = 0;
+  while (rho > rho_stop && k < n) {
+    k++;
+    beta = rho / rho_old;
+    amgd_pcg_p(p, z, beta, rn);                  /* p = p*beta + z */
+    amgd_spmv(A, p, w, 0, NULL, 1, NULL);
+    alpha = amgd_dot(p, w, rn);
+    alpha = rho / alpha;
+    amgd_pcg_xrz(x, r, z, p, w, M, alpha, rn);   /* x += p*a; r -= w*a; z = M.*r */
+    rho_old = rho;
+    rho = amgd_dot(r, z, rn);
+  }
+  amgd_free(p); amgd_free(z); amgd_free(w);
+  return k;
+}
+
+/* ------------------------------------------------------------------------ */
+/* interpolation (amg_setup.c:598-1493)                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  dcsr *Wt;          /* W_skel^T: coarse x fine pattern */
+  double *Q;         /* packed Q factors per coarse column */
+  uint64_t *qoff;
+} skel_factor;
+
+static void factor_free(skel_factor *f) {
+  dcsr_free(&f->Wt);
+  amgd_free(f->Q);
+  amgd_free(f->qoff);
+}
+
+/* solve_constraint (amg_setup.c:1499) */
+static void solve_constraint(double *lam, const dcsr *W_skel, const skel_factor *fac, const dcsr *W0,
+                             const double *alpha, const double *u, const double *v, double tol) {
+  uint32_t nf = W_skel->rn, nc = W_skel->cn;
+  double *au2 = dalloc(nc);
+  amgd_vop(au2, u, u, nc, AMGD_V_MUL);
+  amgd_vop(au2, au2, alpha, nc, AMGD_V_MUL);
+  dcsr *S = amgd_spgemm(W_skel, fac->Wt);            /* W_skel * W_skel' (mxm iftrsp=1) */
+  amgd_lmop(S, fac->Wt, fac->Q, fac->qoff, au2);
+  dump_csr("S", S);
+  double *resid = dalloc(nf), *d = dalloc(nf);
+  amgd_spmv(W0, u, resid, 1.0, v, -1.0, NULL);        /* resid = v - W0*u */
+  amgd_diag(S, d);
+  uint8_t *dl = (uint8_t *)amgd_alloc(nf + 1);
+  amgd_u8_nonzero(d, dl, nf);
+  uint64_t ncond = amgd_u8_count(dl, nf);
+  double *q = dalloc(ncond), *xx = dalloc(ncond);
+  if (ncond != nf) {                                   /* S = S(i,i); lam(~i) = 0 */
+    amgd_vzero_where(lam, dl, nf);
+    dcsr *Ss = amgd_sub_mat(S, dl, dl);
+    dcsr_free(&S);
+    S = Ss;
+    double *rc = dalloc(nf), *dc = dalloc(nf), *lc = dalloc(nf);
+    amgd_vcompact(rc, resid, dl, nf);
+    amgd_vcompact(dc, d, dl, nf);
+    amgd_vcompact(lc, lam, dl, nf);
+    amgd_spmv(S, lc, q, 1., rc, -1., NULL);
+    amgd_vunary(dc, ncond, AMGD_V_INV);
+    pcg(xx, S, q, dc, tol, rc);
+    amgd_vexpand_add(lam, xx, dl, nf);
+    amgd_free(rc); amgd_free(dc); amgd_free(lc);
+  } else {
+    amgd_spmv(S, lam, q, 1., resid, -1., NULL);       /* q = resid - S*lam */
+    amgd_vunary(d, nf, AMGD_V_INV);
+    pcg(xx, S, q, d, tol, resid);
+    amgd_vop(lam, lam, xx, nf, AMGD_V_ADD);
+  }
+  dcsr_free(&S);
+  amgd_free(au2); amgd_free(resid); amgd_free(d); amgd_free(dl); amgd_free(q); amgd_free(xx);
+}
+
+/* solve_weights (amg_setup.c:1437): W0 (lambda = 0), constraint lam, W */
+static void solve_weights(dcsr **W, dcsr **W0, double *lam, const dcsr *W_skel,
+                          const skel_factor *fac, const dcsr *Amt, const double *alpha,
+                          const double *u, const double *v, double tol) {
+  uint32_t nf = W_skel->rn, nc = W_skel->cn;
+  double *au = dalloc(nc), *zeros = dzeros(nf);
+  amgd_vop(au, alpha, u, nc, AMGD_V_MUL);
+  dcsr *W0t = dcsr_empty_like_pattern(fac->Wt);
+  amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, zeros, W0t->a);
+  *W0 = amgd_transpose(W0t, NULL);
+  dcsr_free(&W0t);
+  solve_constraint(lam, W_skel, fac, *W0, alpha, u, v, tol);
+  dcsr *Wt = dcsr_empty_like_pattern(fac->Wt);
+  amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, lam, Wt->a);
+  *W = amgd_transpose(Wt, NULL);
+  dcsr_free(&Wt);
+  amgd_free(au); amgd_free(zeros);
+}
+
+
+
+/* find_support (amg_setup.c:1260) */
+static dcsr *find_support(const dcsr *R, double goal) {
+  uint32_t nf = R->rn, nc = R->cn;
+  dcsr *Rl = dcsr_copy(R);
+  uint64_t *perm = NULL;
+  dcsr *Rt = amgd_transpose(R, &perm);
+  double *onec = dones(nc), *rs = dalloc(nf), *w = dalloc(nc), *w2 = dalloc(nc), *tmp = dalloc(nf);
+  double *vv = dalloc(nc), *sumR = dalloc(nc);
+  uint64_t cap = R->nnz + nc + 16, ns = 0;
+  uint32_t *si = (uint32_t *)amgd_alloc(cap * 4), *sj = (uint32_t *)amgd_alloc(cap * 4);
+  double theta = 0.5;
+  int it = 0;
+  for (;;) {
+    it++;
+    amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);          /* rs = R*1 */
+    amgd_csc_gemv(Rt, perm, Rl->a, rs, w);                /* w = R'*rs (row order) */
+    amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
+    amgd_csc_gemv(Rt, perm, Rl->a, tmp, w2);              /* w2 = R'*(R*w) */
+    amgd_vdiv_guard(vv, w2, w, nc);
+    double mv = amgd_max_first(vv, nc, NULL), mw = mv;   /* max(v) twice, amg_setup.c:1316-1317 */
+    if (mv < goal || mw < goal) break;
+    while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
+    if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
+    if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
+    amgd_csc_gemv(Rt, perm, Rl->a, NULL, sumR);
+    uint32_t nrem = 0;
+    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    ns += nsel;
+    if (nrem == 0) { g_ub++; break; }                    /* no progress: reference loops */
+    if (ns + nc > cap) { g_ub++; break; }
+  }
+  double *ones = dones(ns);
+  dcsr *Sk = amgd_coo2csr(ns, si, sj, ones, nf, nc, 1);
+  if (verbose()) printf("    find_support: %d sweeps, %lu entries\n", it, (unsigned long)ns);
+  amgd_free(ones);
+  dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
+  amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
+  amgd_free(sumR); amgd_free(si); amgd_free(sj);
+  return Sk;
+}
+
+/* expand_support (amg_setup.c:907) */
+static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, double gamma) {
+  dcsr *M = find_support(R, gamma);
+  dcsr *ns = amgd_mpm(1., M, 1., W_skel);
+  dcsr_free(&M);
+  uint32_t nbad = 0;
+  uint8_t *bad = amgd_bad_rows(ns, &nbad);
+  if (nbad == 0) {
+    amgd_skel_binarize(ns, 0);
+    amgd_free(bad);
+    return ns;
+  }
+  dcsr *R0W = amgd_mxmpoint(R0, W_skel);
+  dcsr *Xf = amgd_mpm(1., R0, -1., R0W);
+  dcsr_free(&R0W);
+  uint32_t *pi = NULL, *pj = NULL;
+  uint64_t np = amgd_expand_pick(Xf, bad, &pi, &pj);
+  double *ones = dones(np);
+  dcsr *N = amgd_coo2csr(np, pi, pj, ones, W_skel->rn, W_skel->cn, 1);
+  dcsr *out = amgd_mpm(1., ns, 1., N);
+  amgd_skel_binarize(out, 1);
+  dcsr_free(&N); dcsr_free(&ns); dcsr_free(&Xf);
+  amgd_free(ones); amgd_free(pi); amgd_free(pj); amgd_free(bad);
+  return out;
+}
+
+static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr) {
+  dcsr *R = dcsr_copy(X);
+  amgd_diag_op(R, Dl, AMGD_DMULT);
+  amgd_vals_abs(R);
+  amgd_diag_op(R, Dr, AMGD_MULTD);
+  return R;
+}
+
+static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, double gamma2, double tol) {
+  uint32_t rnf = Af->rn, rnc = Ac->rn, cnc = Ac->cn, cnr = Ar->cn;
+  double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
+  amgd_diag(Af, Df);
+  amgd_diag(Af, Dfinv);
+  amgd_vunary(Dfinv, rnf, AMGD_V_INV);
+  double *uc = dones(cnr), *tmp = dalloc(rnf), *v = dalloc(rnf), *b = dones(rnf);
+  amgd_spmv(Ar, uc, tmp, 0, NULL, -1, NULL);          /* tmp = -Ar*uc */
+  pcg(v, Af, tmp, Df, 1e-16, b);                     /* v = pcg(Af, -Ar*uc, diag(Af)) */
+  g_it = 0;
+  dump_dev("v", v, (size_t)rnf * 8);
+  double *Dc = dalloc(cnc), *Dcinv = dalloc(cnc);
+  amgd_diag(Ac, Dc);
+  amgd_diag(Ac, Dcinv);
+  amgd_vunary(Dcinv, rnc, AMGD_V_INV);
+  dcsr *ArD = dcsr_copy(Ar);
+  amgd_vals_sqr(ArD);
+  amgd_diag_op(ArD, Dfinv, AMGD_DMULT);
+  amgd_diag_op(ArD, Dcinv, AMGD_MULTD);
+  dcsr *W_skel = amgd_min_skel(ArD);                 /* one strongest C per F row */
+  dcsr_free(&ArD);
+  double *lam = dzeros(rnf), *alpha = dalloc(cnc);
+  amgd_d2d(alpha, Dc, (size_t)cnc * 8);
+  double *Dfsqrti = Dfinv;
+  amgd_vunary(Dfsqrti, rnf, AMGD_V_SQRT);
+  dcsr *Amt = amgd_transpose(Ar, NULL);              /* -Ar' */
+  amgd_vals_scale(Amt, -1.0);
+  double *Dcs = dalloc(cnc), *w1 = dalloc(cnc), *w2 = dalloc(cnc), *onesc = dones(cnc), *r = dalloc(cnc);
+  dcsr *W = NULL;
+  uint64_t prev_nnz = (uint64_t)-1;
+  int it = 0;
+  for (;;) {
+    it++;
+    skel_factor fac;
+    fac.Wt = amgd_transpose(W_skel, NULL);
+    fac.Q = amgd_qfactor(fac.Wt, Af, &fac.qoff, NULL);
+    dcsr *Wtmp, *W0;
+    g_it = it;
+    dump_csr("Wskel", W_skel);
+    dump_dev("alpha", alpha, (size_t)cnc * 8);
+    dump_dev("lam_in", lam, (size_t)rnf * 8);
+    solve_weights(&Wtmp, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
+    dump_csr("W0", W0);
+    dump_csr("Wtmp", Wtmp);
+    dump_dev("lam_out", lam, (size_t)rnf * 8);
+    dcsr *AfW = amgd_spgemm(Af, W0);
+    dcsr *Arhat0 = amgd_mpm(1., AfW, 1., Ar);
+    dcsr_free(&AfW);
+    AfW = amgd_spgemm(Af, Wtmp);
+    dcsr *Arhat = amgd_mpm(1., AfW, 1., Ar);
+    dcsr_free(&AfW);
+    dcsr *Arr = amgd_mpm(1.0, Arhat, 1.0, Ar);
+    dcsr *ArW = amgd_mxmpoint(Wtmp, Arr);
+    dcsr_free(&Arr);
+    dcsr *ArWt = amgd_transpose(ArW, NULL);
+    amgd_colsum(ArWt, Dcs);                          /* sum(W.*(Arhat+Ar), 1) */
+    dcsr_free(&ArW); dcsr_free(&ArWt);
+    amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+    amgd_vunary(Dcs, cnc, AMGD_V_INV);
+    amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+    dcsr *R = scale_abs_scale(Arhat, Dfsqrti, Dcs);  /* |Dfsqrti*Arhat|*Dcsqrti */
+    dcsr *R0 = scale_abs_scale(Arhat0, Dfsqrti, Dcs);
+    dcsr *Rt = amgd_transpose(R, NULL);
+    amgd_spmv(R, onesc, tmp, 0., NULL, 1., NULL);
+    amgd_spmvt(Rt, tmp, w1);                         /* w1 = ((R*1)'*R)' */
+    amgd_spmv(R, w1, tmp, 0., NULL, 1., NULL);
+    amgd_spmvt(Rt, tmp, w2);                         /* w2 = ((R*w1)'*R)' */
+    dcsr_free(&Rt);
+    amgd_vdiv_guard(r, w2, w1, cnc);
+    double maxr = 0;
+    uint64_t n = amgd_count_gt(r, cnc, gamma2, &maxr);
+    double w1m = amgd_max_first(w1, cnc, NULL);
+    if (verbose())
+      printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)W_skel->nnz,
+             (unsigned long)n, sqrt(gamma2), sqrt(maxr));
+    int stalled = prev_nnz == W_skel->nnz;   /* reference would loop forever */
+    if (stalled) g_ub++;
+    prev_nnz = W_skel->nnz;
+    if (n == 0 || w1m <= gamma2 || stalled) {
+      dcsr_free(&W0);
+      solve_weights(&W, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
+      double *wuc = dalloc(rnf);
+      amgd_spmv(W, uc, wuc, 0., NULL, 1., NULL);
+      amgd_scale_diag_match(W, v, wuc);
+      amgd_free(wuc);
+      dcsr_free(&Wtmp); dcsr_free(&W0); dcsr_free(&Arhat0); dcsr_free(&Arhat);
+      dcsr_free(&R0); dcsr_free(&R);
+      factor_free(&fac);
+      break;
+    }
+    amgd_alpha_update(alpha, Dc, w2, cnc);
+    dcsr *nsk = expand_support(W_skel, R, R0, gamma2);
+    dcsr_free(&W_skel);
+    W_skel = nsk;
+    dcsr_free(&Wtmp); dcsr_free(&W0); dcsr_free(&Arhat0); dcsr_free(&Arhat);
+    dcsr_free(&R0); dcsr_free(&R);
+    factor_free(&fac);
+  }
+  dcsr_free(&W_skel); dcsr_free(&Amt);
+  amgd_free(Df); amgd_free(Dfinv); amgd_free(uc); amgd_free(tmp); amgd_free(v); amgd_free(b);
+  amgd_free(Dc); amgd_free(Dcinv); amgd_free(lam); amgd_free(alpha); amgd_free(Dcs);
+  amgd_free(w1); amgd_free(w2); amgd_free(onesc); amgd_free(r);
+  return W;
+}
+
+/* ------------------------------------------------------------------------ */
+/* hierarchy                                                                 */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  dcsr *A, *Af, *W, *AfP;
+  uint8_t *vc;
+  double *D;
+  unsigned long *idc, *idf;
+  double m, rho;
+} level_t;
+
+struct amgd_hier {
+  uint32_t nlevels, cap, n0;
+  level_t *lv;
+  unsigned long *id;      /* device, level-0 ids 1..n */
+  int nullspace;
+  double tolc, gamma;
+};
+
+static void add_time(double *acc, double *t0) {
+  amgd_sync();
+  double t = amgd_wtime();
+  *acc += (t - *t0) * 1e3;
+  *t0 = t;
+}
+
+API int amgd_init(int device) { return amgd_rt_init(device); }
+API void amgd_set_exact_dots(int on) { amgd_set_exact(on); }
+API const char *amgd_error(void) { return amgd_last_error(); }
+API void amgd_get_stats(amgd_stats *st) { *st = g_st; }
+API void *amgd_dev_alloc(size_t bytes) { return amgd_alloc(bytes); }
+API void amgd_dev_free(void *p) { amgd_free(p); }
+API void amgd_dev_upload(void *d, const void *h, size_t n) { amgd_h2d(d, h, n); }
+API void amgd_dev_download(void *h, const void *d, size_t n) { amgd_d2h(h, d, n); }
+
+extern void amgd_spgemm_set_timer(int slot);
+extern void amgd_spgemm_bytes_reset(void);
+extern uint64_t amgd_spgemm_bytes(void);
+
+API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj, const double *dAv,
+                          amgd_hier **out, int flags) {
+  (void)flags;
+  if (amgd_rt_init(0) != 0) {
+    fprintf(stderr, "omp_amg_amd: %s\n", amgd_last_error());
+    return -1;
+  }
+  memset(&g_st, 0, sizeof g_st);
+  g_ub = 0;
+  amgd_timer_reset();
+  amgd_sync();
+  double t_start = amgd_wtime(), t0 = t_start;
+  dcsr *A = amgd_build_csr(nz, dAi, dAj, dAv);
+  add_time(&g_st.t_build_ms, &t0);
+
+  const double tol = 0.5, ctol = 0.7, itol = 1e-4;
+  const double gamma2 = 1. - sqrt(1. - tol), gamma = sqrt(gamma2);
+  amgd_hier *h = (amgd_hier *)calloc(1, sizeof(amgd_hier));
+  h->cap = 64;
+  h->lv = (level_t *)calloc(h->cap, sizeof(level_t));
+  h->tolc = ctol;
+  h->gamma = gamma;
+  h->n0 = A->rn;
+  h->id = (unsigned long *)amgd_alloc((size_t)A->rn * 8 + 8);
+  amgd_ids_iota(h->id, A->rn);
+  g_st.rows0 = A->rn;
+  g_st.nnz0 = A->nnz;
+  uint32_t level = 0;
+  for (;;) {
+    if (level + 1 >= h->cap) {
+      h->cap *= 2;
+      h->lv = (level_t *)realloc(h->lv, h->cap * sizeof(level_t));
+      memset(h->lv + h->cap / 2, 0, (h->cap / 2) * sizeof(level_t));
+    }
+    level_t *L = &h->lv[level];
+    uint32_t rn = A->rn, cn = A->cn;
+    g_lvl = (int)level;
+    L->A = A;
+    if (verbose()) printf("Level %u, dim(A) = %u, nnz(A)/dim(A) = %f\n", level + 1, cn,
+                          cn ? (double)A->nnz / cn : 0.0);
+    if (cn <= 1) {
+      double a0 = 0;
+      if (A->nnz) amgd_d2h(&a0, A->a, 8);
+      h->nullspace = a0 < 1e-9 ? 1 : 0;
+      break;
+    }
+    /* --- coarsen --- */
+    uint8_t *vc = (uint8_t *)amgd_alloc(rn + 1), *vf = (uint8_t *)amgd_alloc(rn + 1);
+    coarsen(A, vc, ctol);
+    amgd_u8_not(vc, vf, rn);
+    L->vc = vc;
+    add_time(&g_st.t_coarsen_ms, &t0);
+    /* --- smoother --- */
+    dcsr *Af = amgd_sub_mat(A, vf, vf);
+    uint32_t rnf = Af->rn;
+    double *s = dalloc(rnf), *D = dalloc(rnf);
+    amgd_rowsum_sq_inv(Af, s);                      /* s = 1./sum(Af.*Af) */
+    amgd_diag(Af, D);
+    amgd_vop(D, D, s, rnf, AMGD_V_MUL);
+    amgd_free(s);
+    if (rnf >= 2) {
+      double *Dh = dalloc(rnf);
+      amgd_d2d(Dh, D, (size_t)rnf * 8);
+      amgd_vunary(Dh, rnf, AMGD_V_SQRT);
+      dcsr *DAD = dcsr_copy(Af);
+      amgd_diag_op(DAD, Dh, AMGD_DMULT);
+      amgd_diag_op(DAD, Dh, AMGD_MULTD);
+      double lambda[KMAX + 2];
+      uint32_t k = lanczos(DAD, lambda);
+      double a = lambda[0], b = lambda[k - 1];
+      amgd_vscale(D, rnf, 2. / (a + b));
+      L->rho = (b - a) / (b + a);
+      double c;
+      chebsim(&L->m, &c, L->rho, gamma2);
+      amgd_free(Dh);
+      dcsr_free(&DAD);
+    } else {
+      L->rho = 0;
+      L->m = 1;
+    }
+    L->D = D;
+    L->Af = Af;
+    add_time(&g_st.t_smoother_ms, &t0);
+    /* --- interpolation --- */
+    dcsr *Afc = amgd_sub_mat(A, vf, vc), *Ac = amgd_sub_mat(A, vc, vc);
+    uint32_t rnc = Ac->rn;
+    L->idc = (unsigned long *)amgd_alloc((size_t)rnc * 8 + 8);
+    L->idf = (unsigned long *)amgd_alloc((size_t)rnf * 8 + 8);
+    amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, rn, L->idc, L->idf);
+    dcsr *W = interpolation(Af, Ac, Afc, gamma2, itol);
+    L->W = W;
+    add_time(&g_st.t_interp_ms, &t0);
+    /* --- Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) --- */
+    amgd_spgemm_set_timer(0);
+    dcsr *AfW = amgd_spgemm(Af, W);
+    dcsr *AfP = amgd_mpm(1., AfW, 1., Afc);
+    dcsr_free(&AfW);
+    L->AfP = AfP;
+    dcsr *Wt = amgd_transpose(W, NULL);
+    dcsr *WtAfP = amgd_spgemm(Wt, AfP);
+    dcsr *Acf = amgd_transpose(Afc, NULL);
+    dcsr *AcfW = amgd_spgemm(Acf, W);
+    amgd_spgemm_set_timer(-1);
+    dcsr *Atmp = amgd_mpm(1., WtAfP, 1., AcfW);
+    A = amgd_mpm(1., Atmp, 1, Ac);
+    g_st.rap_out_nnz += A->nnz;
+    dcsr_free(&Wt); dcsr_free(&WtAfP); dcsr_free(&Acf); dcsr_free(&AcfW); dcsr_free(&Atmp);
+    dcsr_free(&Afc); dcsr_free(&Ac);
+    amgd_free(vf);
+    add_time(&g_st.t_rap_ms, &t0);
+    level++;
+  }
+  h->nlevels = level + 1;
+  amgd_sync();
+  g_st.t_total_ms = (amgd_wtime() - t_start) * 1e3;
+  g_st.rap_kernel_ms = amgd_timer_ms(0);
+  g_st.rap_bytes = amgd_spgemm_bytes();
+  amgd_spgemm_bytes_reset();
+  g_st.nlevels = h->nlevels;
+  g_st.ub_events = (uint32_t)g_ub;
+  g_st.peak_bytes = amgd_pool_peak_bytes();
+  *out = h;
+  return 0;
+}
+
+static struct csr_mat *csr_to_host(const dcsr *A) {
+  struct csr_mat *M = (struct csr_mat *)malloc(sizeof *M);
+  M->rn = A->rn;
+  M->cn = A->cn;
+  M->row_off = (amg_uint *)malloc(((size_t)A->rn + 1) * sizeof(amg_uint));
+  M->col = (amg_uint *)malloc((A->nnz ? A->nnz : 1) * sizeof(amg_uint));
+  M->a = (double *)malloc((A->nnz ? A->nnz : 1) * sizeof(double));
+  amgd_to_host_cols(A, M->row_off, M->col, M->a);
+  return M;
+}
+
+API int amgd_hier_export(const amgd_hier *h, struct amg_setup_data *data) {
+  amgd_sync();
+  double t0 = amgd_wtime();
+  uint32_t nl = h->nlevels, cap = nl + 1;
+  data->tolc = h->tolc;
+  data->gamma = h->gamma;
+  data->n = (double *)malloc(cap * 8); data->nnz = (double *)malloc(cap * 8);
+  data->nnzf = (double *)malloc(cap * 8); data->nnzfp = (double *)malloc(cap * 8);
+  data->m = (double *)malloc(cap * 8); data->rho = (double *)malloc(cap * 8);
+  data->A = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->Af = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->W = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->AfP = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->idc = (amg_uint **)malloc(cap * sizeof(void *));
+  data->idf = (amg_uint **)malloc(cap * sizeof(void *));
+  data->C = (double **)malloc(cap * sizeof(void *));
+  data->F = (double **)malloc(cap * sizeof(void *));
+  data->D = (double **)malloc(cap * sizeof(void *));
+  data->id = (amg_uint *)malloc((size_t)h->n0 * sizeof(amg_uint) + 8);
+  amgd_d2h(data->id, h->id, (size_t)h->n0 * 8);
+  for (uint32_t l = 0; l < nl; l++) {
+    const level_t *L = &h->lv[l];
+    data->n[l] = L->A->cn;
+    data->nnz[l] = (double)L->A->nnz;
+    data->A[l] = csr_to_host(L->A);
+    if (l + 1 == nl) break;
+    uint32_t rn = L->A->rn, rnf = L->Af->rn, rnc = rn - rnf;
+    uint8_t *vc = (uint8_t *)malloc(rn + 1);
+    amgd_d2h(vc, L->vc, rn);
+    data->C[l] = (double *)malloc((size_t)rn * 8 + 8);
+    data->F[l] = (double *)malloc((size_t)rn * 8 + 8);
+    for (uint32_t i = 0; i < rn; i++) { data->C[l][i] = vc[i] ? 1. : 0.; data->F[l][i] = vc[i] ? 0. : 1.; }
+    free(vc);
+    data->D[l] = (double *)malloc((size_t)rnf * 8 + 8);
+    amgd_d2h(data->D[l], L->D, (size_t)rnf * 8);
+    data->m[l] = L->m;
+    data->rho[l] = L->rho;
+    data->nnzf[l] = (double)L->Af->nnz;
+    data->nnzfp[l] = (double)L->AfP->nnz;
+    data->Af[l] = csr_to_host(L->Af);
+    data->W[l] = csr_to_host(L->W);
+    data->AfP[l] = csr_to_host(L->AfP);
+    data->idc[l] = (amg_uint *)malloc((size_t)rnc * 8 + 8);
+    data->idf[l] = (amg_uint *)malloc((size_t)rnf * 8 + 8);
+    amgd_d2h(data->idc[l], L->idc, (size_t)rnc * 8);
+    amgd_d2h(data->idf[l], L->idf, (size_t)rnf * 8);
+  }
+  data->nlevels = nl;
+  data->nullspace = (amg_uint)h->nullspace;
+  g_st.t_copy_ms = (amgd_wtime() - t0) * 1e3;
+  return 0;
+}
+
+API void amgd_hier_free(amgd_hier **hp) {
+  amgd_hier *h = *hp;
+  if (!h) return;
+  for (uint32_t l = 0; l < h->nlevels; l++) {
+    level_t *L = &h->lv[l];
+    dcsr_free(&L->A); dcsr_free(&L->Af); dcsr_free(&L->W); dcsr_free(&L->AfP);
+    if (L->vc) amgd_free(L->vc);
+    if (L->D) amgd_free(L->D);
+    if (L->idc) amgd_free(L->idc);
+    if (L->idf) amgd_free(L->idf);
+  }
+  amgd_free(h->id);
+  free(h->lv);
+  free(h);
+  *hp = NULL;
+}
+
+/* ------------------------------------------------------------------------ */
+/* drop-in host ABI (amg_setup.h)                                            */
+/* ------------------------------------------------------------------------ */
+API void amg_setup(amg_uint n, const amg_uint *Ai, const amg_uint *Aj, const double *Av,
+                   struct amg_setup_data *data) {
+  if (amgd_rt_init(0) != 0) {
+    fprintf(stderr, "omp_amg_amd: amg_setup needs a HIP device: %s\n", amgd_last_error());
+    abort();
+  }
+  uint32_t *hi = (uint32_t *)malloc((size_t)n * 4 + 4), *hj = (uint32_t *)malloc((size_t)n * 4 + 4);
+  for (amg_uint k = 0; k < n; k++) {
+    if (Ai[k] > 0xfffffffeul || Aj[k] > 0xfffffffeul) {
+      fprintf(stderr, "omp_amg_amd: index %lu exceeds 32-bit range\n", (unsigned long)k);
+      abort();
+    }
+    hi[k] = (uint32_t)Ai[k];
+    hj[k] = (uint32_t)Aj[k];
+  }
+  uint32_t *di = (uint32_t *)amgd_alloc((size_t)n * 4 + 4), *dj = (uint32_t *)amgd_alloc((size_t)n * 4 + 4);
+  double *dv = dalloc(n);
+  amgd_h2d(di, hi, (size_t)n * 4);
+  amgd_h2d(dj, hj, (size_t)n * 4);
+  amgd_h2d(dv, Av, (size_t)n * 8);
+  free(hi); free(hj);
+  amgd_hier *h = NULL;
+  if (amgd_setup_device(n, di, dj, dv, &h, 0) != 0) abort();
+  amgd_free(di); amgd_free(dj); amgd_free(dv);
+  amgd_hier_export(h, data);
+  amgd_hier_free(&h);
+}
+
+static void free_csr_host(struct csr_mat **M) {
+  if (*M) { free((*M)->row_off); free((*M)->col); free((*M)->a); free(*M); *M = NULL; }
+}
+
+API void free_data(struct amg_setup_data **data) {
+  struct amg_setup_data *d = *data;
+  if (!d) return;
+  free(d->n); free(d->nnz); free(d->nnzf); free(d->nnzfp); free(d->m); free(d->rho);
+  for (amg_uint i = 0; i < d->nlevels; i++) free_csr_host(&d->A[i]);
+  for (amg_uint i = 0; i + 1 < d->nlevels; i++) {
+    free(d->C[i]); free(d->F[i]); free(d->D[i]); free(d->idc[i]); free(d->idf[i]);
+    free_csr_host(&d->Af[i]); free_csr_host(&d->W[i]); free_csr_host(&d->AfP[i]);
+  }
+  free(d->id); free(d->idc); free(d->idf); free(d->C); free(d->F); free(d->D);
+  free(d->A); free(d->Af); free(d->W); free(d->AfP);
+  free(d);
+  *data = NULL;
+}
+
+/* amg_export (amg_setup.c:405-595): the Nek5000 AMG file set */
+static uint64_t max_row(const struct csr_mat *m) {
+  uint64_t mx = 0;
+  for (amg_uint i = 0; i < m->rn; i++) if (m->row_off[i + 1] - m->row_off[i] > mx) mx = m->row_off[i + 1] - m->row_off[i];
+  return mx;
+}
+static void save_mats(amg_uint *len, amg_uint n, amg_uint nl, const amg_uint *lvl, amg_uint **id,
+                      struct csr_mat **mat, const char *fn) {
+  const double magic = 3.14159;
+  FILE *f = fopen(fn, "w");
+  if (!f) { perror(fn); return; }
+  fwrite(&magic, sizeof(double), 1, f);
+  uint64_t mx = 0;
+  for (amg_uint i = 0; i < nl; i++) { uint64_t l = max_row(mat[i]); if (l > mx) mx = l; }
+  double *buf = (double *)malloc((2 * mx + 1) * sizeof(double));
+  amg_uint *row = (amg_uint *)calloc(nl + 1, sizeof(amg_uint));
+  for (amg_uint i = 0; i < n; i++) {
+    amg_uint l = lvl[i] - 1;
+    if (l > nl) { printf("level out of bounds\n"); continue; }
+    if (l == nl) { len[i] = 0; continue; }
+    struct csr_mat *M = mat[l];
+    amg_uint j = row[l]++;
+    if (j >= M->rn) { printf("row out of bounds\n"); continue; }
+    amg_uint kb = M->row_off[j], ke = M->row_off[j + 1];
+    double *p = buf;
+    for (amg_uint k = kb; k != ke; ++k) *p++ = (double)id[l][M->col[k]], *p++ = M->a[k];
+    len[i] = ke - kb;
+    fwrite(buf, sizeof(double), 2 * (ke - kb), f);
+  }
+  for (amg_uint i = 0; i < nl; i++) if (row[i] != mat[i]->rn) printf("matrices not exhausted\n");
+  free(row); free(buf);
+  fclose(f);
+  printf("%d matrices written to %s\n", (int)nl, fn);
+}
+API void amg_export(struct amg_setup_data *data) {
+  amg_uint nl = data->nlevels, n = (amg_uint)data->n[0];
+  amg_uint *lvl = (amg_uint *)malloc(n * sizeof(amg_uint) + 8);
+  for (amg_uint i = 0; i < n; i++) lvl[i] = 1;
+  for (amg_uint i = 0; i + 1 < nl; i++)
+    for (amg_uint j = 0; j < (amg_uint)data->n[i + 1]; j++) lvl[data->idc[i][j] - 1] += 1;
+  double *dvec = (double *)malloc(n * sizeof(double) + 8);
+  for (amg_uint i = 0; i + 1 < nl; i++) {
+    amg_uint m = (amg_uint)(data->n[i] - data->n[i + 1]);
+    for (amg_uint j = 0; j < m; j++) dvec[data->idf[i][j] - 1] = data->D[i][j];
+  }
+  amg_uint k = data->idc[nl - 2][0] - 1;
+  dvec[k] = data->nullspace != 0 ? 0. : 1. / data->A[nl - 1]->a[0];
+  amg_uint *Wl = (amg_uint *)malloc(n * sizeof(amg_uint) + 8);
+  amg_uint *Pl = (amg_uint *)malloc(n * sizeof(amg_uint) + 8);
+  amg_uint *Fl = (amg_uint *)malloc(n * sizeof(amg_uint) + 8);
+  save_mats(Wl, n, nl - 1, lvl, data->idc, data->W, "amg_W.dat");
+  save_mats(Pl, n, nl - 1, lvl, data->idc, data->AfP, "amg_AfP.dat");
+  save_mats(Fl, n, nl - 1, lvl, data->idf, data->Af, "amg_Aff.dat");
+  FILE *f = fopen("amg.dat", "w");
+  if (f) {
+    const double magic = 3.14159, stamp = 2.01;
+    double t;
+    fwrite(&magic, sizeof(double), 1, f);
+    fwrite(&stamp, sizeof(double), 1, f);
+    t = (double)nl; fwrite(&t, sizeof(double), 1, f);
+    fwrite(data->m, sizeof(double), nl - 1, f);
+    fwrite(data->rho, sizeof(double), nl - 1, f);
+    t = (double)n; fwrite(&t, sizeof(double), 1, f);
+    for (amg_uint i = 0; i < n; i++) {
+      double rec[6] = {(double)data->id[i], (double)lvl[i], (double)Wl[i], (double)Pl[i], (double)Fl[i], dvec[i]};
+      fwrite(rec, sizeof(double), 6, f);
+    }
+    fclose(f);
+    printf("Vectors written to %s\n", "amg.dat");
+  }
+  free(Wl); free(Pl); free(Fl); free(dvec); free(lvl);
+}
+
+/* ------------------------------------------------------------------------ */
+/* gslib crs.h (reference crs.h:8-21, amg.c:475)                             */
+/* ------------------------------------------------------------------------ */
+struct crs_data { amgd_hier *h; amg_uint un; amg_uint null_space; };
+
+API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz, const amg_uint *Ai,
+                               const amg_uint *Aj, const double *A, amg_uint null_space,
+                               const struct comm *comm) {
+  if (comm && comm->np != 1) {
+    fprintf(stderr, "omp_amg_amd: crs_setup supports np == 1 (got %lu)\n", (unsigned long)comm->np);
+    abort();
+  }
+  /* local dof k is global id[k]; entries touching id 0 are dropped (amg.c:1065) */
+  amg_uint *I = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8), *J = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8);
+  double *V = (double *)malloc(nz * sizeof(double) + 8);
+  amg_uint m = 0;
+  for (amg_uint k = 0; k < nz; k++) {
+    amg_uint i = Ai[k], j = Aj[k];
+    if (i >= n || j >= n || id[i] == 0 || id[j] == 0 || A[k] == 0) continue;
+    I[m] = id[i] - 1; J[m] = id[j] - 1; V[m] = A[k]; m++;
+  }
+  struct crs_data *d = (struct crs_data *)calloc(1, sizeof *d);
+  uint32_t *di = (uint32_t *)amgd_alloc(m * 4 + 4), *dj = (uint32_t *)amgd_alloc(m * 4 + 4);
+  double *dv = dalloc(m);
+  uint32_t *hi = (uint32_t *)malloc(m * 4 + 4), *hj = (uint32_t *)malloc(m * 4 + 4);
+  for (amg_uint k = 0; k < m; k++) { hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k]; }
+  amgd_h2d(di, hi, m * 4); amgd_h2d(dj, hj, m * 4); amgd_h2d(dv, V, m * 8);
+  free(hi); free(hj); free(I); free(J); free(V);
+  if (amgd_setup_device(m, di, dj, dv, &d->h, 0) != 0) abort();
+  amgd_free(di); amgd_free(dj); amgd_free(dv);
+  d->un = n;
+  d->null_space = null_space;
+  return d;
+}
+API void crs_solve(double *x, struct crs_data *data, double *b) {
+  (void)x; (void)data; (void)b;
+  fprintf(stderr, "omp_amg_amd: crs_solve (AMG V-cycle) is not implemented; setup only\n");
+  abort();
+}
+API void crs_stats(struct crs_data *data) {
+  printf("AMG stats: %u levels (setup %.3f ms)\n", data && data->h ? data->h->nlevels : 0, g_st.t_total_ms);
+}
+API void crs_free(struct crs_data *data) {
+  if (!data) return;
+  amgd_hier_free(&data->h);
+  free(data);
+}

@@ -1,0 +1,97 @@
+/*
+ * amgd_testapi.c -- kernel-level test hooks of libomp_amg_amd.so.
+ *
+ * Exposes single device primitives on host CSR inputs so tests/test_gpu_*.py
+ * can check each HIP kernel against a host restatement of the reference
+ * operation it replaces (mxm, transpose, mpm, mxmpoint, apply_M, min_skel,
+ * coarsen).  Not used by the setup path itself.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "amgd.h"
+
+#define API __attribute__((visibility("default")))
+
+typedef struct { uint32_t rn, cn; uint64_t nnz; uint64_t *ro; uint32_t *col; double *a; } hcsr;
+
+static dcsr *up(const hcsr *H) {
+  dcsr *A = dcsr_new(H->rn, H->cn, H->nnz);
+  amgd_h2d(A->ro, H->ro, ((size_t)H->rn + 1) * 8);
+  amgd_h2d(A->col, H->col, H->nnz * 4);
+  amgd_h2d(A->a, H->a, H->nnz * 8);
+  return A;
+}
+static void down(const dcsr *A, hcsr *H) {
+  H->rn = A->rn; H->cn = A->cn; H->nnz = A->nnz;
+  H->ro = (uint64_t *)malloc(((size_t)A->rn + 1) * 8);
+  H->col = (uint32_t *)malloc(A->nnz * 4 + 4);
+  H->a = (double *)malloc(A->nnz * 8 + 8);
+  amgd_d2h(H->ro, A->ro, ((size_t)A->rn + 1) * 8);
+  amgd_d2h(H->col, A->col, A->nnz * 4);
+  amgd_d2h(H->a, A->a, A->nnz * 8);
+}
+
+/* op: 0 spgemm(A,B)  1 transpose(A)  2 mpm(alpha,A,beta,B)  3 mxmpoint(A,B)  4 min_skel(A) */
+API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, double beta, hcsr *HX) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA), *B = HB ? up(HB) : NULL, *X = NULL;
+  switch (op) {
+    case 0: X = amgd_spgemm(A, B); break;
+    case 1: X = amgd_transpose(A, NULL); break;
+    case 2: X = amgd_mpm(alpha, A, beta, B); break;
+    case 3: X = amgd_mxmpoint(A, B); break;
+    case 4: X = amgd_min_skel(A); break;
+    default: return -2;
+  }
+  down(X, HX);
+  dcsr_free(&A); dcsr_free(&B); dcsr_free(&X);
+  return 0;
+}
+
+/* z = alpha*y + beta*(A x) (y may be NULL) */
+API int amgd_test_spmv(const hcsr *HA, const double *x, double alpha, const double *y, double beta, double *z) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA);
+  double *dx = (double *)amgd_alloc((size_t)HA->cn * 8 + 8), *dz = (double *)amgd_alloc((size_t)HA->rn * 8 + 8);
+  double *dy = NULL;
+  amgd_h2d(dx, x, (size_t)HA->cn * 8);
+  if (y) { dy = (double *)amgd_alloc((size_t)HA->rn * 8 + 8); amgd_h2d(dy, y, (size_t)HA->rn * 8); }
+  amgd_spmv(A, dx, dz, alpha, dy, beta, NULL);
+  amgd_d2h(z, dz, (size_t)HA->rn * 8);
+  amgd_free(dx); amgd_free(dz); if (dy) amgd_free(dy);
+  dcsr_free(&A);
+  return 0;
+}
+
+/* build_csr on host COO (u32 indices) */
+API int amgd_test_build(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V, hcsr *HX) {
+  if (amgd_rt_init(0) != 0) return -1;
+  uint32_t *di = (uint32_t *)amgd_alloc(nz * 4 + 4), *dj = (uint32_t *)amgd_alloc(nz * 4 + 4);
+  double *dv = (double *)amgd_alloc(nz * 8 + 8);
+  amgd_h2d(di, I, nz * 4); amgd_h2d(dj, J, nz * 4); amgd_h2d(dv, V, nz * 8);
+  dcsr *X = amgd_build_csr(nz, di, dj, dv);
+  down(X, HX);
+  dcsr_free(&X);
+  amgd_free(di); amgd_free(dj); amgd_free(dv);
+  return 0;
+}
+
+/* sqrt / div / 1/x on a host vector, to check IEEE rounding of the device math */
+API int amgd_test_math(int op, uint64_t n, const double *a, const double *b, double *out) {
+  if (amgd_rt_init(0) != 0) return -1;
+  double *da = (double *)amgd_alloc(n * 8 + 8), *db = (double *)amgd_alloc(n * 8 + 8);
+  amgd_h2d(da, a, n * 8);
+  amgd_h2d(db, b, n * 8);
+  if (op == 0) amgd_vunary(da, n, AMGD_V_SQRT);
+  else if (op == 1) amgd_vunary(da, n, AMGD_V_INV);
+  else amgd_vop(da, da, db, n, AMGD_V_DIV);
+  amgd_d2h(out, da, n * 8);
+  amgd_free(da); amgd_free(db);
+  return 0;
+}
+
+API void amgd_test_free(hcsr *H) {
+  free(H->ro); free(H->col); free(H->a);
+  H->ro = NULL; H->col = NULL; H->a = NULL;
+}

@@ -76,6 +76,22 @@ static void csr_shrink(ocsr *A) {
   A->a = realloc(A->a, (z ? z : 1) * sizeof(double));
 }
 
+static int o_lvl = 0, o_it = 0;
+static void dump_raw(const char *name, const void *p, size_t bytes) {
+  const char *dir = getenv("ORACLE_DUMP");
+  if (!dir || !*dir) return;
+  char fn[512];
+  snprintf(fn, sizeof fn, "%s/L%d_it%d_%s.bin", dir, o_lvl, o_it, name);
+  FILE *f = fopen(fn, "wb");
+  if (f) { fwrite(p, 1, bytes, f); fclose(f); }
+}
+static void dump_ocsr(const char *name, const ocsr *A) {
+  char n2[256];
+  snprintf(n2, sizeof n2, "%s_ro", name); dump_raw(n2, A->ro, ((size_t)A->rn + 1) * 8);
+  snprintf(n2, sizeof n2, "%s_col", name); dump_raw(n2, A->col, A->ro[A->rn] * 4);
+  snprintf(n2, sizeof n2, "%s_a", name); dump_raw(n2, A->a, A->ro[A->rn] * 8);
+}
+
 /* ------------------------------------------------------------------------
  * COO -> CSR, stable by (i, j): coo2csr (amg_setup.c:3684) sorts with
  * sarray_sort_2(i, j), a stable radix sort; duplicates are kept in input order.
@@ -720,6 +736,7 @@ static void solve_constraint(double *lam, const ocsr *W_skel, const ocsr *W_skel
   ocsr *S = spgemm(W_skel, Wsk_t);
   csr_free(&Wsk_t);
   interp_lmop(S, Af, au2, W_skelt);
+  dump_ocsr("S", S);
   double *resid = NEW(double, nf), *d = NEW(double, nf), *dl = NEW(double, nf);
   apply_M(resid, 1.0, v, -1.0, W0, u);
   diag(d, S);
@@ -907,6 +924,8 @@ static ocsr *interpolation(const ocsr *Af, const ocsr *Ac, const ocsr *Ar, doubl
   apply_M(tmp, 0, NULL, -1, Ar, uc);
   for (u32 i = 0; i < rnf; i++) b[i] = 1.0;
   pcg(v, Af, tmp, Df, 1e-16, b);
+  o_it = 0;
+  dump_raw("v", v, rnf * 8);
   double *Dc = NEW(double, cnc), *Dcinv = NEW(double, cnc);
   diag(Dc, Ac); diag(Dcinv, Ac);
   for (u32 i = 0; i < rnc; i++) Dcinv[i] = 1. / Dcinv[i];
@@ -930,9 +949,17 @@ static ocsr *interpolation(const ocsr *Af, const ocsr *Ac, const ocsr *Ar, doubl
   for (u32 i = 0; i < cnc; i++) ones[i] = 1.0;
   ocsr *W = NULL;
   u64 prev_nnz = (u64)-1;
+  int it = 0;
   for (;;) {
     ocsr *Wtmp, *W0;
+    o_it = ++it;
+    dump_ocsr("Wskel", W_skel);
+    dump_raw("alpha", alpha, cnc * 8);
+    dump_raw("lam_in", lam, rnf * 8);
     solve_weights(&Wtmp, &W0, lam, W_skel, Af, Ar, rnc, alpha, uc, v, tol);
+    dump_ocsr("W0", W0);
+    dump_ocsr("Wtmp", Wtmp);
+    dump_raw("lam_out", lam, rnf * 8);
     ocsr *AfW = spgemm(Af, W0);
     ocsr *Arhat0 = mpm(1., AfW, 1., Ar);
     csr_free(&AfW);
@@ -1047,6 +1074,7 @@ API void amg_setup(amg_uint n, const amg_uint *Ai, const amg_uint *Aj, const dou
     data->n[level] = cn;
     data->nnz[level] = (double)nnz(A);
     data->A[level] = to_abi(A);
+    o_lvl = (int)level;
     if (getenv("ORACLE_VERBOSE")) printf("Level %u, dim(A) = %u, nnz = %lu\n", level + 1, cn, (unsigned long)nnz(A)), fflush(stdout);
     if (cn <= 1) {
       data->nullspace = 0;

@@ -1,0 +1,109 @@
+"""Kernel-level parity of the HIP primitives against host restatements of the
+reference operations (tests/refops.py), bit for bit, through the library's
+test hooks (amgd_testapi.c)."""
+import numpy as np
+import pytest
+
+import refops
+import omp_amg_amd as oa
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_spgemm_short_rows(seed):
+    rng = np.random.default_rng(seed)
+    A = refops.rand_csr(rng, 300, 200, 0.03, ints=(seed == 2))
+    B = refops.rand_csr(rng, 200, 250, 0.03, ints=(seed == 2))
+    X = oa.test_csr_op(0, A, B)
+    assert refops.same(X, refops.spgemm(A, B))
+
+
+def test_spgemm_long_rows_and_cancellation():
+    rng = np.random.default_rng(7)
+    A = refops.rand_csr(rng, 40, 600, 0.5, ints=True)          # > 1024 products per row
+    B = refops.rand_csr(rng, 600, 900, 0.05, ints=True)
+    X = oa.test_csr_op(0, A, B)
+    R = refops.spgemm(A, B)
+    assert refops.same(X, R)
+
+
+def test_spgemm_empty_rows():
+    rng = np.random.default_rng(3)
+    A = refops.rand_csr(rng, 50, 40, 0.02)
+    B = refops.rand_csr(rng, 40, 30, 0.0)                        # B all empty
+    X = oa.test_csr_op(0, A, B)
+    assert X.nnz == 0 and X.rn == 50
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_transpose(seed):
+    rng = np.random.default_rng(seed)
+    A = refops.rand_csr(rng, 500, 300, 0.02)
+    assert refops.same(oa.test_csr_op(1, A), refops.transpose(A))
+
+
+def test_mpm_and_mxmpoint():
+    rng = np.random.default_rng(5)
+    A = refops.rand_csr(rng, 200, 150, 0.05, ints=True)
+    B = refops.rand_csr(rng, 200, 150, 0.05, ints=True)
+    assert refops.same(oa.test_csr_op(2, A, B, 1.0, -1.0), refops.mpm(1.0, A, -1.0, B))
+    assert refops.same(oa.test_csr_op(2, A, B, 1.0, 1.0), refops.mpm(1.0, A, 1.0, B))
+    assert refops.same(oa.test_csr_op(3, A, B), refops.mxmpoint(A, B))
+
+
+def test_spmv_ordered():
+    rng = np.random.default_rng(11)
+    A = refops.rand_csr(rng, 1000, 800, 0.01)
+    L = refops.rand_csr(rng, 300, 5000, 0.6)                     # long rows: direct path
+    x = rng.standard_normal(800)
+    y = rng.standard_normal(1000)
+    assert np.array_equal(oa.test_spmv(A, x), refops.spmv(A, x))
+    assert np.array_equal(oa.test_spmv(A, x, 1.0, y, -1.0), refops.spmv(A, x, 1.0, y, -1.0))
+    xl = rng.standard_normal(5000)
+    assert np.array_equal(oa.test_spmv(L, xl), refops.spmv(L, xl))
+
+
+def test_min_skel():
+    rng = np.random.default_rng(4)
+    R = refops.rand_csr(rng, 300, 100, 0.03)
+    R.a = np.abs(R.a)
+    R.a[::7] = 0.0
+    assert refops.same(oa.test_csr_op(4, R), refops.min_skel(R))
+
+
+def test_build_csr_drops_zeros_and_empty_rows():
+    rng = np.random.default_rng(9)
+    n = 60
+    I = rng.integers(0, n, 400).astype(np.uint32)
+    J = rng.integers(0, n, 400).astype(np.uint32)
+    key = np.unique(I.astype(np.int64) * n + J)
+    I, J = (key // n).astype(np.uint32), (key % n).astype(np.uint32)
+    V = rng.standard_normal(len(I))
+    V[::9] = 0.0
+    perm = rng.permutation(len(I))
+    X = oa.test_build(I[perm], J[perm], V[perm])
+    # host restatement of build_csr (amg_setup.c:3612)
+    keep = V != 0
+    rn = int(I.max()) + 1
+    rows = np.zeros(rn, bool)
+    rows[I[keep]] = True
+    newid = np.cumsum(rows) - 1
+    m = keep & rows[J] if J.max() < rn else keep
+    order = np.lexsort((J[m], I[m]))
+    ii, jj, vv = I[m][order], J[m][order], V[m][order]
+    ro = np.zeros(rows.sum() + 1, dtype=np.int64)
+    np.add.at(ro, newid[ii] + 1, 1)
+    assert np.array_equal(X.row_off, np.cumsum(ro))
+    assert np.array_equal(X.col, newid[jj])
+    assert np.array_equal(X.a, vv)
+
+
+def test_device_math_is_ieee():
+    """sqrt, 1/x and x/y must round like the host (the reference's sqrt/div)."""
+    rng = np.random.default_rng(0)
+    a = np.abs(rng.standard_normal(100000)) * 10.0 ** rng.integers(-30, 30, 100000)
+    b = rng.standard_normal(100000) * 10.0 ** rng.integers(-30, 30, 100000)
+    assert np.array_equal(oa.test_math(0, a), np.sqrt(a))
+    assert np.array_equal(oa.test_math(1, a), 1.0 / a)
+    assert np.array_equal(oa.test_math(2, a, b), a / b)

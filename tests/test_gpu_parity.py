@@ -1,0 +1,82 @@
+"""Parity of the HIP AMG setup, through the drop-in C ABI (amg_setup.h), against
+  * the reference's own outputs (tests/golden/*.npz, made from the compiled
+    reference by tests/golden/make_golden.py), and
+  * the CPU oracle (oracle/, pinned bit-exactly to the reference) on larger
+    grids the reference's O(n^2) mxm cannot reach in test time.
+
+Bar (DESIGN.md "Parity"): level sizes, C/F masks, idc/idf and every CSR
+pattern identical; W/AfP/Af/A values within 1e-12 relative to each matrix's
+largest entry; Chebyshev D / rho within 1e-9 (Lanczos dots are tree-ordered).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLD, golden_cases
+import omp_amg_amd as oa
+from omp_amg_amd import abi, parity, problems
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_gpu_matches_reference_fixture(case):
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    bad = parity.compare(ref, h, exact=False, rtol=RTOL)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("gen", [
+    ("p7_20", lambda: problems.poisson3d(20)),
+    ("p7_24x20x16", lambda: problems.poisson3d(16, mx=24, my=20)),
+    ("aniso_16", lambda: problems.poisson3d(16, eps=1e-3)),
+    ("p27_12", lambda: problems.poisson3d(12, 27)),
+    ("sem_e3_N4", lambda: problems.sem_laplacian(3, 3, 3, 4, seed=2, jitter=0.3)),
+], ids=lambda g: g[0])
+def test_gpu_matches_oracle_larger(oracle_lib, gen):
+    Ai, Aj, Av = gen[1]()
+    ref = abi.run_setup(oracle_lib, Ai, Aj, Av)
+    h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    bad = parity.compare(ref, h, exact=False, rtol=RTOL)
+    assert not bad, bad
+
+
+def test_export_files_match_oracle(oracle_lib, tmp_path):
+    """amg_export writes the Nek5000 AMG files (amg_setup.c:405): same bytes for
+    ids / levels / row lengths; values within tolerance."""
+    import ctypes as C
+    Ai, Aj, Av = problems.load_amgdmp(GOLD)
+    outs = {}
+    for name, L in (("gpu", oa.lib()), ("oracle", oracle_lib)):
+        d = tmp_path / name
+        d.mkdir()
+        cwd = os.getcwd()
+        os.chdir(d)
+        try:
+            libc = C.CDLL(None)
+            libc.malloc.restype = C.c_void_p
+            raw = libc.malloc(C.sizeof(abi.AmgSetupData))
+            C.memset(raw, 0, C.sizeof(abi.AmgSetupData))
+            dp = C.cast(raw, C.POINTER(abi.AmgSetupData))
+            abi.srand(1)
+            u64 = C.POINTER(abi.amg_uint)
+            ai = np.ascontiguousarray(Ai, dtype=np.uint64)
+            aj = np.ascontiguousarray(Aj, dtype=np.uint64)
+            av = np.ascontiguousarray(Av)
+            with abi.quiet_stdout():
+                L.amg_setup(len(av), ai.ctypes.data_as(u64), aj.ctypes.data_as(u64),
+                            av.ctypes.data_as(C.POINTER(C.c_double)), dp)
+                L.amg_export.argtypes = [C.POINTER(abi.AmgSetupData)]
+                L.amg_export(dp)
+            L.free_data(C.pointer(dp))
+        finally:
+            os.chdir(cwd)
+        outs[name] = {f: np.fromfile(d / f) for f in ("amg.dat", "amg_W.dat", "amg_AfP.dat", "amg_Aff.dat")}
+    for f in outs["gpu"]:
+        g, o = outs["gpu"][f], outs["oracle"][f]
+        assert g.shape == o.shape, f
+        np.testing.assert_allclose(g, o, rtol=1e-9, atol=1e-12, err_msg=f)
