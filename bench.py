@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Benchmark: AMG setup throughput of the MI355X-native setup path.
+
+metric  : "AMG setup rows/sec + RAP SpGEMM nnz/sec at 1/2/4/8 MI355X" (BASELINE.json)
+workload: BASELINE.json configs[1] -- 3D 7-point Poisson 256^3 CSR (16.7M rows,
+          116M nnz) on one MI355X.  One "step" = one full AMG setup (build_csr,
+          coarsening, Chebyshev/Lanczos smoother, energy-minimising interpolation,
+          Galerkin RAP for every level) from a device-resident COO matrix to a
+          hierarchy resident in HBM.  Inputs are uploaded before the timed region.
+value   : whole-job rows/s = (ranks x rows) / max-over-ranks seconds per step.
+          Round 1 runs one independent replica per GPU (DESIGN.md "Multi-GPU:
+          replicas only"), so scaling is "weak".
+roofline: the Galerkin RAP SpGEMM kernels (A_{l+1} = W'AfP + A_cf W + A_cc and
+          AfP = Af W), event-timed live on the library stream; algorithmic bytes
+          = 12 B per nnz of each operand and result + 8 B per row.
+cpu_baseline: the reference's own serial setup (oracle/_ref/libref_amg.so,
+          compiled from /root/reference sources) on a bounded sample, rank 0 only.
+
+Run: python bench.py [--gpus N --steps K --warmup W] [--m 256] [--stencil 7]
+     N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1)
+    p.add_argument("--warmup", type=int, default=0)
+    p.add_argument("--m", type=int, default=256, help="grid edge (configs[1]: 256)")
+    p.add_argument("--stencil", type=int, default=7)
+    p.add_argument("--fast-dots", action="store_true",
+                   help="tree-ordered global dots instead of reference order (not parity-certified)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-m", type=int, default=24, help="reference CPU sample grid edge")
+    p.add_argument("--traffic", type=float, default=None,
+                   help="RAP HBM bytes per launch from a rocprofv3 PMC pass (profiles/)")
+    return p.parse_args()
+
+
+def cpu_baseline(m):
+    """Reference serial setup (compiled from /root/reference by oracle/Makefile)
+    on a bounded sample; falls back to our CPU restatement if _ref is absent."""
+    from omp_amg_amd import abi, problems
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_amg.so")
+    kind = "reference"
+    if not os.path.exists(ref):
+        ref = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+        kind = "port"
+    if not os.path.exists(ref):
+        return None
+    lib = abi.bind_setup(ctypes.CDLL(ref))
+    Ai, Aj, Av = problems.poisson3d(m, 7)
+    t0 = time.perf_counter()
+    h = abi.run_setup(lib, Ai, Aj, Av)
+    dt = time.perf_counter() - t0
+    rows = m ** 3
+    return {"value": rows / dt, "unit": "rows/s", "cores": 1, "kind": kind,
+            "sample": f"3D 7-point Poisson {m}^3 ({rows} rows, {h.nlevels} levels), "
+                      f"full serial amg_setup, {dt:.2f} s on one host core"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import omp_amg_amd as oa
+    from omp_amg_amd import problems
+
+    oa.lib().amgd_init(local)
+    Ai, Aj, Av = problems.poisson3d(args.m, args.stencil)
+    rows = args.m ** 3
+    ds = oa.DeviceSetup(Ai, Aj, Av)
+    del Ai, Aj, Av
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ds.run(exact_dots=not args.fast_dots)
+    barrier()
+    rap_ms, rap_bytes, rap_nnz, st = 0.0, 0, 0, None
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = ds.run(exact_dots=not args.fast_dots)
+        rap_ms += st["rap_kernel_ms"]
+        rap_bytes += st["rap_bytes"]
+        rap_nnz += st["rap_out_nnz"]
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt * 1e3 / args.steps
+    value = world * rows * args.steps / dt
+
+    if rank == 0:
+        achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
+        out = {
+            "metric": "AMG setup rows/sec + RAP SpGEMM nnz/sec at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"3D {args.stencil}-point Poisson {args.m}^3 CSR, full AMG setup "
+                                   f"(BASELINE configs[1])",
+                       "rows": rows, "nnz": int(st["nnz0"]), "levels": int(st["nlevels"]),
+                       "parallelism": f"replicas x{world}",
+                       "global_dots": "tree" if args.fast_dots else "reference-order"},
+            "rap_spgemm_nnz_per_s": world * rap_nnz / (rap_ms * 1e-3) if rap_ms > 0 else None,
+            "phases_ms": {k: round(st[k], 2) for k in ("t_build_ms", "t_coarsen_ms", "t_smoother_ms",
+                                                          "t_interp_ms", "t_rap_ms")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": args.traffic,
+                         "kernel": "k_spgemm_short<1>/k_spgemm_long<1> (RAP + AfP products)",
+                         "algorithmic_bytes_per_setup": rap_bytes / args.steps,
+                         "kernel_ms_per_setup": rap_ms / args.steps},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_m)
+        print(json.dumps(out), flush=True)
+    ds.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -275,11 +275,58 @@ extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qof
 // (c, k, m) order, stably radix-sorted by landing position and added to S in
 // that order: bit-identical to the reference's sequential accumulation.
 // ---------------------------------------------------------------------------
-__global__ void k_lmop_contrib(const uint32_t *erow, uint64_t e0, uint64_t e1,
-                               const uint64_t *wro, const uint32_t *wcol, const double *Q,
-                               const uint64_t *qoff, const double *u, const uint64_t *sro,
-                               const uint32_t *scol, uint64_t snnz, const uint64_t *coff,
-                               uint64_t cbase, uint64_t *key, double *val) {
+// (1) landing positions: one thread per (c, k) replays sp_add's forward walk
+// over S starting at row Qj[k].  The reference steps one stored entry at a
+// time (and keeps going into the following rows when a column is absent);
+// here each step is a lower_bound inside the current row plus, when the row
+// is exhausted, a skip over whole rows using per-row / per-64-row /
+// per-4096-row column maxima -- the same landing, O(log) instead of O(nnz).
+__device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t lo, uint64_t hi,
+                                                    uint32_t x) {
+  while (lo < hi) {
+    uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// first row r2 > r with rowmax[r2] >= x, or nrows
+__device__ uint32_t next_row_ge(const int64_t *rmax, const int64_t *b64, const int64_t *b4k,
+                                uint32_t nrows, uint32_t r, int64_t x) {
+  uint32_t r2 = r + 1;
+  while (r2 < nrows && (r2 & 63)) { if (rmax[r2] >= x) return r2; r2++; }
+  while (r2 < nrows && (r2 & 4095)) {
+    if (b64[r2 >> 6] >= x) {
+      for (uint32_t q = r2; q < r2 + 64 && q < nrows; q++) if (rmax[q] >= x) return q;
+    }
+    r2 += 64;
+  }
+  while (r2 < nrows) {
+    if (b4k[r2 >> 12] >= x) {
+      for (uint32_t q = r2; q < r2 + 4096 && q < nrows; q += 64)
+        if (b64[q >> 6] >= x)
+          for (uint32_t p = q; p < q + 64 && p < nrows; p++) if (rmax[p] >= x) return p;
+    }
+    r2 += 4096;
+  }
+  return nrows;
+}
+__global__ void k_rowmax(const uint64_t *ro, const uint32_t *col, uint32_t n, int64_t *rmax) {
+  GRID_STRIDE(r, n) rmax[r] = ro[r + 1] > ro[r] ? (int64_t)col[ro[r + 1] - 1] : -1;
+}
+__global__ void k_blockmax(const int64_t *in, uint64_t n, int shift, int64_t *out, uint64_t nout) {
+  GRID_STRIDE(b, nout) {
+    int64_t m = -1;
+    uint64_t s0 = b << shift, s1 = min(n, (b + 1) << shift);
+    for (uint64_t q = s0; q < s1; q++) m = in[q] > m ? in[q] : m;
+    out[b] = m;
+  }
+}
+__global__ void k_lmop_land(const uint32_t *erow, uint64_t e0, uint64_t e1, const uint64_t *wro,
+                            const uint32_t *wcol, const uint64_t *sro, const uint32_t *scol,
+                            uint32_t srn, uint64_t snnz, const int64_t *rmax, const int64_t *b64,
+                            const int64_t *b4k, const uint64_t *coff, uint64_t cbase,
+                            uint64_t *key) {
   for (uint64_t e = e0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e1;
        e += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t c = erow[e];
@@ -287,29 +334,55 @@ __global__ void k_lmop_contrib(const uint32_t *erow, uint64_t e0, uint64_t e1,
     uint32_t nz = (uint32_t)(wro[c + 1] - w0);
     uint32_t k = (uint32_t)(e - w0);
     const uint32_t *Qj = wcol + w0;
-    const double *Qc = Q + qoff[c];
-    double uc = u[c];
     uint64_t o = coff[c] - cbase + (uint64_t)k * nz;
-    uint32_t j = Qj[k];
-    uint64_t t = sro[j];
-    bool live = sro[j + 1] != t;   // sp_add returns at once on an empty row
+    uint32_t r = Qj[k];                      // walk starts in row Qj[k]
+    uint64_t t = sro[r];
+    bool live = sro[r + 1] != t;             // sp_add returns at once on an empty row
     for (uint32_t m = 0; m < nz; m++) {
-      uint64_t land = snnz;          // "no landing" sorts after every real position
+      uint64_t land = snnz;                  // "no landing" sorts after every real position
       if (live) {
         uint32_t xm = Qj[m];
-        while (t < snnz && scol[t] < xm) t++;
-        if (t >= snnz) live = false;   // reference runs off the end of St (UB)
-        else land = t++;
-      }
-      double q = 0.0;
-      uint32_t t0 = k > m ? k : m;
-      for (uint32_t tt = t0; tt < nz; tt++) {
-        const double *qt = Qc + tri(tt);
-        q += qt[k] * qt[m];
+        uint64_t end = sro[r + 1];
+        if (t < end && rmax[r] >= (int64_t)xm) {
+          land = lower_bound_u32(scol, t, end, xm);
+        } else {
+          uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xm);
+          if (r2 >= srn) live = false;       // reference runs off the end of St (UB)
+          else { r = r2; land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xm); }
+        }
+        // next step starts after the landing; if that is the end of row r, the
+        // "current row" test fails and the skip starts at row r+1 = position t
+        if (live) t = land + 1;
       }
       key[o + m] = land;
-      val[o + m] = uc * q;
     }
+  }
+}
+// (2) values: one thread per contribution (c, k, m):
+//     u_c * sum_{t >= max(k,m)} q_t[k] * q_t[m], t ascending (QQt, amg_setup.c:1638-1642)
+__global__ void k_lmop_val(uint64_t n, uint32_t c0, uint32_t c1, const uint64_t *coff,
+                           uint64_t cbase, const uint64_t *wro, const double *Q,
+                           const uint64_t *qoff, const double *u, const uint64_t *key,
+                           uint64_t snnz, double *val) {
+  GRID_STRIDE(o, n) {
+    if (key[o] >= snnz) { val[o] = 0.0; continue; }
+    uint64_t g = o + cbase;
+    uint32_t lo = c0, hi = c1;            // last c with coff[c] <= g
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (coff[mid] <= g) lo = mid; else hi = mid;
+    }
+    uint32_t c = lo;
+    uint32_t nz = (uint32_t)(wro[c + 1] - wro[c]);
+    uint64_t r = g - coff[c];
+    uint32_t k = (uint32_t)(r / nz), m = (uint32_t)(r % nz);
+    const double *Qc = Q + qoff[c];
+    double q = 0.0;
+    for (uint32_t tt = k > m ? k : m; tt < nz; tt++) {
+      const double *qt = Qc + tri(tt);
+      q += qt[k] * qt[m];
+    }
+    val[o] = u[c] * q;
   }
 }
 __global__ void k_seg_accum(const uint64_t *key, const double *val, uint64_t n, uint64_t snnz,
@@ -345,6 +418,15 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64
   amgd_d2h(hro.data(), Wt->ro, (rn + 1) * 8);
   uint32_t *erow = (uint32_t *)amgd_alloc(Wt->nnz * 4 + 4);
   amgd_row_of_entry_launch(Wt->ro, rn, erow);
+  uint32_t srn = S->rn;
+  uint64_t n64 = ((uint64_t)srn + 63) >> 6, n4k = ((uint64_t)srn + 4095) >> 12;
+  int64_t *rmax = (int64_t *)amgd_alloc(((size_t)srn + 1) * 8);
+  int64_t *b64 = (int64_t *)amgd_alloc((n64 + 1) * 8), *b4k = (int64_t *)amgd_alloc((n4k + 1) * 8);
+  if (srn) {
+    k_rowmax<<<grid_for(srn), 256, 0, s>>>(S->ro, S->col, srn, rmax);
+    k_blockmax<<<grid_for(n64), 256, 0, s>>>(rmax, srn, 6, b64, n64);
+    k_blockmax<<<grid_for(n4k), 256, 0, s>>>(rmax, srn, 12, b4k, n4k);
+  }
   const uint64_t CH = std::min<uint64_t>(total, 1ull << 26);   // contributions per chunk
   uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);
   double *val = (double *)amgd_alloc(CH * 8 + 8), *val2 = (double *)amgd_alloc(CH * 8 + 8);
@@ -369,9 +451,11 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64
     }
     uint64_t e0 = hro[c0], e1 = hro[c1];
     if (n && e1 > e0) {
-      k_lmop_contrib<<<grid_for(e1 - e0, 256, 65536), 256, 0, s>>>(
-          erow, e0, e1, Wt->ro, Wt->col, Q, qoff, u, S->ro, S->col, S->nnz, coff, hcoff[c0], key,
-          val);
+      k_lmop_land<<<grid_for(e1 - e0, 256, 65536), 256, 0, s>>>(
+          erow, e0, e1, Wt->ro, Wt->col, S->ro, S->col, srn, S->nnz, rmax, b64, b4k, coff,
+          hcoff[c0], key);
+      k_lmop_val<<<grid_for(n, 256, 65536), 256, 0, s>>>(n, c0, c1, coff, hcoff[c0], Wt->ro, Q,
+                                                          qoff, u, key, S->nnz, val);
       KCHECK();
       size_t tb2 = 0;
       HIPCK(rocprim::radix_sort_pairs(nullptr, tb2, key, key2, val, val2, (size_t)n, 0, eb, s));
@@ -383,7 +467,7 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64
     c0 = c1;
   }
   amgd_free(tmp); amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2);
-  amgd_free(erow); amgd_free(coff);
+  amgd_free(erow); amgd_free(coff); amgd_free(rmax); amgd_free(b64); amgd_free(b4k);
 }
 
 // ---------------------------------------------------------------------------
@@ -407,9 +491,12 @@ extern "C" void amgd_csc_gemv(const dcsr *Rt, const uint64_t *perm, const double
     k_csc_gemv<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, a, x, Rt->rn, z);
   KCHECK();
 }
+// Per bad column c (w_c > (1+theta)*goal && sumR_c != 0): first row of the max of
+// R(i,c)*rs_i (amg_setup.c:1343-1364), removed from R (both CSR and CSC copies).
 __global__ void k_fs_select(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
-                            double *a, const double *rs, const double *w, const double *sumR,
-                            double thr, uint32_t n, uint32_t *si, uint32_t *sj, unsigned *cnt) {
+                            double *ta, double *a, const double *rs, const double *w,
+                            const double *sumR, double thr, uint32_t n, uint32_t *si, uint32_t *sj,
+                            unsigned *cnt) {
   GRID_STRIDE(c, n) {
     if (!(w[c] > thr && sumR[c] != 0.)) continue;
     double mx = -DBL_MAX;
@@ -417,13 +504,13 @@ __global__ void k_fs_select(const uint64_t *tro, const uint32_t *trow, const uin
     uint64_t best = ~0ull;
     for (uint64_t q = tro[c]; q < tro[c + 1]; q++) {
       uint32_t i = trow[q];
-      double x = a[perm[q]] * rs[i];
+      double x = ta[q] * rs[i];
       if (x > mx) { mx = x; mi = i; best = q; }
     }
     unsigned p = atomicAdd(&cnt[0], 1u);
     si[p] = mi;
     sj[p] = (uint32_t)c;
-    if (best != ~0ull) { a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
+    if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
   }
 }
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
@@ -433,8 +520,8 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   unsigned *cnt = (unsigned *)amgd_alloc(8);
   amgd_memset(cnt, 0, 8);
   if (Rt->rn)
-    k_fs_select<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, Rl->a, rs, w, sumR,
-                                                         thr, Rt->rn, sel_i, sel_j, cnt);
+    k_fs_select<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, w,
+                                                         sumR, thr, Rt->rn, sel_i, sel_j, cnt);
   KCHECK();
   unsigned h[2];
   amgd_d2h(h, cnt, 8);

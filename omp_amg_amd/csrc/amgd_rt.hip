@@ -355,7 +355,16 @@ __global__ __launch_bounds__(256) void k_dot_seq(const double *a, const double *
       if (tid == 0) {
         uint64_t m = n - base < SEQ_TILE ? n - base : SEQ_TILE;
         const double *p = buf[cur];
-        for (uint64_t j = 0; j < m; j++) s += p[j];
+        uint64_t j = 0;
+        // independent LDS loads first, then the dependent add chain in order
+        for (; j + 16 <= m; j += 16) {
+          double v[16];
+#pragma unroll
+          for (int q = 0; q < 16; q++) v[q] = p[j + q];
+#pragma unroll
+          for (int q = 0; q < 16; q++) s += v[q];
+        }
+        for (; j < m; j++) s += p[j];
       }
     } else if (t + 1 < ntile) {
       uint64_t nb = base + SEQ_TILE;

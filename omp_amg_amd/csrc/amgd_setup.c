@@ -380,16 +380,16 @@ static dcsr *find_support(const dcsr *R, double goal) {
   for (;;) {
     it++;
     amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);          /* rs = R*1 */
-    amgd_csc_gemv(Rt, perm, Rl->a, rs, w);                /* w = R'*rs (row order) */
+    amgd_spmvt(Rt, rs, w);                                /* w = R'*rs (row order) */
     amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
-    amgd_csc_gemv(Rt, perm, Rl->a, tmp, w2);              /* w2 = R'*(R*w) */
+    amgd_spmvt(Rt, tmp, w2);                              /* w2 = R'*(R*w) */
     amgd_vdiv_guard(vv, w2, w, nc);
     double mv = amgd_max_first(vv, nc, NULL), mw = mv;   /* max(v) twice, amg_setup.c:1316-1317 */
     if (mv < goal || mw < goal) break;
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
-    amgd_csc_gemv(Rt, perm, Rl->a, NULL, sumR);
+    amgd_colsum(Rt, sumR);
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     ns += nsel;

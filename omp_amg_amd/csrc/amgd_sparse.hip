@@ -268,11 +268,46 @@ __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t
     }
   }
 }
+// long rows: one wavefront per row; the 64 lanes load and multiply a chunk
+// (coalesced) into LDS, lane 0 adds the chunk in order -- same sum, same order.
+__global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, uint32_t rn, const double *x,
+                                                   double *z, double alpha, const double *y,
+                                                   double beta, const uint8_t *f) {
+  __shared__ double buf[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < rn; i += (uint64_t)gridDim.x * 4) {
+    uint64_t k0 = ro[i], k1 = ro[i + 1];
+    double t = 0;
+    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
+      uint64_t k = c0 + lane;
+      if (k < k1) buf[w][lane] = a[k] * x[col[k]];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (lane == 0) {
+        int m = (int)min((uint64_t)64, k1 - c0);
+        for (int q = 0; q < m; q++) t += buf[w][q];
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (lane == 0) {
+      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) v = v * (f[i] ? 1.0 : 0.0);
+      z[i] = v;
+    }
+  }
+}
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
   if (M->rn == 0) return;
-  int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
-  k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+  if (M->nnz >= 32ull * M->rn) {
+    int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
+    k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+  } else {
+    int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
+    k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+  }
   KCHECK();
 }
 // z = M^T x: rows of Mt are columns of M with rows ascending -> ordered gather
