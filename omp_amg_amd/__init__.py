@@ -83,6 +83,8 @@ def lib() -> C.CDLL:
                                       C.POINTER(HCsr)]
         L.amgd_test_math.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.amgd_test_free.argtypes = [C.POINTER(HCsr)]
+        L.amgd_test_dot.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        L.amgd_test_dot.restype = C.c_double
         _lib = L
     return _lib
 
@@ -217,3 +219,11 @@ def test_math(op: int, a, b=None):
     out = np.zeros_like(a)
     lib().amgd_test_math(op, len(a), a.ctypes.data, b.ctypes.data, out.ctypes.data)
     return out
+
+
+def test_dot(mode: int, a, b=None, plain: bool = False, exact: bool = True) -> float:
+    """exact (reference-order) dot through the library: mode 0 a.b, 1 a.a, 2 (a.*b).*b"""
+    init()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
+    return lib().amgd_test_dot(mode, len(a), a.ctypes.data, b.ctypes.data, int(plain), int(exact))

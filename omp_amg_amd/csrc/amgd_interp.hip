@@ -132,11 +132,17 @@ __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
 }
 __global__ void k_split_by_nz(const uint64_t *wro, uint32_t rn, uint32_t cap, uint32_t *sl,
                               uint32_t *bl, unsigned *cnt) {
-  GRID_STRIDE(c, rn) {
-    uint64_t nz = wro[c + 1] - wro[c];
-    if (nz == 0) continue;
-    if (nz <= cap) sl[atomicAdd(&cnt[0], 1u)] = (uint32_t)c;
-    else bl[atomicAdd(&cnt[1], 1u)] = (uint32_t)c;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t iters = (rn + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {
+    uint64_t c = c0 + it * stride;
+    uint64_t nz = c < rn ? wro[c + 1] - wro[c] : 0;
+    bool sm = nz != 0 && nz <= cap, bg = nz > cap;
+    unsigned ps = wave_append(&cnt[0], sm);
+    unsigned pb = wave_append(&cnt[1], bg);
+    if (sm) sl[ps] = (uint32_t)c;
+    if (bg) bl[pb] = (uint32_t)c;
   }
 }
 __global__ void k_max_nz(const uint64_t *wro, uint32_t rn, unsigned long long *mx) {
@@ -493,24 +499,33 @@ extern "C" void amgd_csc_gemv(const dcsr *Rt, const uint64_t *perm, const double
 }
 // Per bad column c (w_c > (1+theta)*goal && sumR_c != 0): first row of the max of
 // R(i,c)*rs_i (amg_setup.c:1343-1364), removed from R (both CSR and CSC copies).
-__global__ void k_fs_select(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
-                            double *ta, double *a, const double *rs, const double *w,
-                            const double *sumR, double thr, uint32_t n, uint32_t *si, uint32_t *sj,
-                            unsigned *cnt) {
-  GRID_STRIDE(c, n) {
+__global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const uint32_t *trow,
+                                                   const uint64_t *perm, double *ta, double *a,
+                                                   const double *rs, const double *w,
+                                                   const double *sumR, double thr, uint32_t n,
+                                                   uint32_t *si, uint32_t *sj, unsigned *cnt) {
+  // one wavefront per column; (value, position) max with the first position on ties
+  const int lane = threadIdx.x & 63;
+  for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n;
+       c += (uint64_t)gridDim.x * 4) {
     if (!(w[c] > thr && sumR[c] != 0.)) continue;
     double mx = -DBL_MAX;
-    uint32_t mi = 0;
     uint64_t best = ~0ull;
-    for (uint64_t q = tro[c]; q < tro[c + 1]; q++) {
-      uint32_t i = trow[q];
-      double x = ta[q] * rs[i];
-      if (x > mx) { mx = x; mi = i; best = q; }
+    for (uint64_t q = tro[c] + lane; q < tro[c + 1]; q += 64) {
+      double x = ta[q] * rs[trow[q]];
+      if (x > mx) { mx = x; best = q; }
     }
-    unsigned p = atomicAdd(&cnt[0], 1u);
-    si[p] = mi;
-    sj[p] = (uint32_t)c;
-    if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
+    for (int o = 32; o > 0; o >>= 1) {
+      double om = __shfl_down(mx, o, 64);
+      unsigned long long ob = __shfl_down((unsigned long long)best, o, 64);
+      if (om > mx || (om == mx && ob < best)) { mx = om; best = ob; }
+    }
+    if (lane == 0) {
+      unsigned p = atomicAdd(&cnt[0], 1u);
+      si[p] = best != ~0ull ? trow[best] : 0u;
+      sj[p] = (uint32_t)c;
+      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
+    }
   }
 }
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
@@ -520,8 +535,8 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   unsigned *cnt = (unsigned *)amgd_alloc(8);
   amgd_memset(cnt, 0, 8);
   if (Rt->rn)
-    k_fs_select<<<grid_for(Rt->rn), 256, 0, amgd_s()>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, w,
-                                                         sumR, thr, Rt->rn, sel_i, sel_j, cnt);
+    k_fs_select<<<(int)std::min<uint64_t>((Rt->rn + 3) / 4, 65536), 256, 0, amgd_s()>>>(
+        Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, w, sumR, thr, Rt->rn, sel_i, sel_j, cnt);
   KCHECK();
   unsigned h[2];
   amgd_d2h(h, cnt, 8);

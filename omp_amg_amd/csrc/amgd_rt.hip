@@ -380,7 +380,167 @@ __global__ __launch_bounds__(256) void k_dot_seq(const double *a, const double *
   }
   if (tid == 0) *out = s;
 }
+// ---------------------------------------------------------------------------
+// Parallel bit-exact emulation of the sequential sum s = ((0 + p0) + p1) + ...
+//
+// While the running sum s stays strictly inside one binade [2^e, 2^(e+1)) (or
+// its negative), every step rounds on the fixed grid u = 2^(e-52) and s is a
+// multiple of u, so fl(s + p) = s + RN_u(p): the step is an integer addition
+// of m = rint(p/u) in units of u.  One 1024-thread block streams tiles of
+// products through LDS, computes the m's, block-scans them, and finds the first
+// index where the candidate running value leaves the binade interior, where
+// p/u is an exact tie (ties-to-even would depend on s), or where |p/u| is
+// huge.  Everything before that index is committed at once; that element is
+// added the ordinary way; the scan resumes after it.  The result is identical,
+// bit for bit, to the left-to-right loop (tests/test_gpu_kernels.py checks it
+// against k_dot_seq on adversarial inputs).
+// ---------------------------------------------------------------------------
+#define BN_THREADS 1024
+#define BN_PER 4
+#define BN_TILE (BN_THREADS * BN_PER)
+
+__device__ __forceinline__ long long bn_block_excl_scan(long long v, long long *sh, long long *total) {
+  // exclusive scan of one value per thread across the block (wrapping arithmetic)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long x = (unsigned long long)v;
+  for (int o = 1; o < 64; o <<= 1) {
+    unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[w] = (long long)x;
+  __syncthreads();
+  if (w == 0) {
+    unsigned long long t = lane < BN_THREADS / 64 ? (unsigned long long)sh[lane] : 0ull;
+    for (int o = 1; o < 64; o <<= 1) {
+      unsigned long long y = __shfl_up(t, o, 64);
+      if (lane >= o) t += y;
+    }
+    if (lane < BN_THREADS / 64) sh[lane] = (long long)t;   // inclusive per-wave totals
+  }
+  __syncthreads();
+  unsigned long long before = w > 0 ? (unsigned long long)sh[w - 1] : 0ull;
+  unsigned long long incl = before + x;
+  *total = sh[BN_THREADS / 64 - 1];
+  __syncthreads();
+  return (long long)(incl - (unsigned long long)v);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, const double *b,
+                                                           uint64_t n, double *out) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  __shared__ double s_sh;
+  __shared__ int viol_sh;
+  const int tid = threadIdx.x;
+  double s = 0.0;                      // uniform running sum
+  for (uint64_t base = 0; base < n; base += BN_TILE) {
+    int tlen = (int)min((uint64_t)BN_TILE, n - base);
+    for (int q = tid; q < tlen; q += BN_THREADS) {
+      uint64_t i = base + q;
+      double x = a[i];
+      tile[q] = MODE == 0 ? x * b[i] : MODE == 1 ? x * x : (x * b[i]) * b[i];
+    }
+    __syncthreads();
+    int j = 0, rounds = 0;
+    while (j < tlen) {
+      // sequential steps where the grid argument does not apply (s == 0,
+      // subnormal s), or once a tile has needed too many re-scans
+      if (s == 0.0 && rounds <= 48) {
+        // 0 + p == p exactly (and +0 for a zero p): jump to the first nonzero product
+        if (tid == 0) viol_sh = 0x7fffffff;
+        __syncthreads();
+        for (int q = j + tid; q < tlen; q += BN_THREADS)
+          if (tile[q] != 0.0) { atomicMin(&viol_sh, q); break; }
+        __syncthreads();
+        int f = viol_sh;
+        if (f == 0x7fffffff) { j = tlen; }
+        else { s = s + tile[f]; j = f + 1; }
+        __syncthreads();
+        continue;
+      }
+      if (fabs(s) < 2.2250738585072014e-308 || rounds > 48) {
+        if (tid == 0) {
+          double t = s;
+          int stop = rounds > 48 ? tlen : j + 1;
+          for (int q = j; q < stop; q++) t += tile[q];
+          s_sh = t;
+        }
+        __syncthreads();
+        s = s_sh;
+        j = rounds > 48 ? tlen : j + 1;
+        __syncthreads();
+        continue;
+      }
+      rounds++;
+      int e = ilogb(s);
+      double u = ldexp(1.0, e - 52);
+      long long S0 = (long long)ldexp(s, 52 - e);       // |S0| in [2^52, 2^53)
+      const long long LO = (1ll << 52), HI = (1ll << 53);
+      // each thread owns BN_PER consecutive elements of [j, tlen)
+      int first = j + tid * BN_PER;
+      long long m[BN_PER];
+      bool bad[BN_PER];
+      long long loc = 0;
+#pragma unroll
+      for (int q = 0; q < BN_PER; q++) {
+        int idx = first + q;
+        m[q] = 0;
+        bad[q] = false;
+        if (idx < tlen) {
+          double x = tile[idx] / u;                       // exact: power-of-two scaling
+          double r = rint(x);
+          if (!(fabs(x) < 4.6e18) || fabs(r - x) == 0.5) bad[q] = true;   // huge or tie
+          else m[q] = (long long)r;
+        }
+        loc = (long long)((unsigned long long)loc + (unsigned long long)m[q]);
+      }
+      long long total;
+      long long pre = bn_block_excl_scan(loc, sh, &total);
+      // first violating index in my elements
+      int myv = 0x7fffffff;
+      long long run = (long long)((unsigned long long)S0 + (unsigned long long)pre);
+#pragma unroll
+      for (int q = 0; q < BN_PER; q++) {
+        int idx = first + q;
+        if (idx >= tlen || myv != 0x7fffffff) continue;
+        if (bad[q]) { myv = idx; continue; }
+        run = (long long)((unsigned long long)run + (unsigned long long)m[q]);
+        bool inside = S0 > 0 ? (run > LO && run < HI) : (run < -LO && run > -HI);
+        if (!inside) myv = idx;
+      }
+      if (tid == 0) viol_sh = 0x7fffffff;
+      __syncthreads();
+      if (myv != 0x7fffffff) atomicMin(&viol_sh, myv);
+      __syncthreads();
+      int v = viol_sh;
+      if (v == 0x7fffffff) {
+        // whole remainder stays inside the binade
+        long long fin = (long long)((unsigned long long)S0 + (unsigned long long)total);
+        s = ldexp((double)fin, e - 52);
+        j = tlen;
+      } else {
+        // commit [j, v) exactly, then add element v the ordinary way
+        if (first <= v - 1 && v - 1 < first + BN_PER) {
+          long long r2 = (long long)((unsigned long long)S0 + (unsigned long long)pre);
+          for (int q = 0; first + q < v; q++) r2 = (long long)((unsigned long long)r2 + (unsigned long long)m[q]);
+          s_sh = ldexp((double)r2, e - 52) + tile[v];
+        }
+        if (v == j && tid == 0) s_sh = s + tile[v];
+        __syncthreads();
+        s = s_sh;
+        j = v + 1;
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *out = s;
+}
+
 static int g_exact = -1;
+static int g_seq_plain = 0;      // 1: plain one-lane sequential loop (test reference)
+extern "C" void amgd_set_seq_plain(int on) { g_seq_plain = on; }
 extern "C" void amgd_set_exact(int on) { g_exact = on ? 1 : 0; }
 extern "C" int amgd_get_exact(void) {
   if (g_exact < 0) {
@@ -398,8 +558,14 @@ static double seq_finish() {
 extern "C" double amgd_dot(const double *a, const double *b, uint64_t n) {
   if (n == 0) return 0.0;
   if (amgd_get_exact()) {
-    if (b) k_dot_seq<0><<<1, 256, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
-    else k_dot_seq<1><<<1, 256, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
+    if (g_seq_plain) {
+      if (b) k_dot_seq<0><<<1, 256, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
+      else k_dot_seq<1><<<1, 256, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
+    } else if (b) {
+      k_dot_binade<0><<<1, BN_THREADS, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
+    } else {
+      k_dot_binade<1><<<1, BN_THREADS, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
+    }
     return seq_finish();
   }
   int nb = red_grid(n);
@@ -410,7 +576,8 @@ extern "C" double amgd_norm2(const double *a, uint64_t n) { return sqrt(amgd_dot
 extern "C" double amgd_dot3(const double *M, const double *b, uint64_t n) {
   if (n == 0) return 0.0;
   if (amgd_get_exact()) {
-    k_dot_seq<2><<<1, 256, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
+    if (g_seq_plain) k_dot_seq<2><<<1, 256, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
+    else k_dot_binade<2><<<1, BN_THREADS, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
     return seq_finish();
   }
   int nb = red_grid(n);

@@ -256,10 +256,10 @@ __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t
       }
       __syncthreads();
       if (i < r1)
-        for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += sa[k - b0] * x[sc[k - b0]];
+        for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += x ? sa[k - b0] * x[sc[k - b0]] : sa[k - b0];
       __syncthreads();
     } else if (i < r1) {
-      for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += a[k] * x[col[k]];
+      for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += x ? a[k] * x[col[k]] : a[k];
     }
     if (i < r1) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
@@ -281,12 +281,18 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
     double t = 0;
     for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
       uint64_t k = c0 + lane;
-      if (k < k1) buf[w][lane] = a[k] * x[col[k]];
+      if (k < k1) buf[w][lane] = x ? a[k] * x[col[k]] : a[k];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       if (lane == 0) {
         int m = (int)min((uint64_t)64, k1 - c0);
-        for (int q = 0; q < m; q++) t += buf[w][q];
+        int q = 0;
+        for (; q + 8 <= m; q += 8) {
+          double v0 = buf[w][q], v1 = buf[w][q + 1], v2 = buf[w][q + 2], v3 = buf[w][q + 3];
+          double v4 = buf[w][q + 4], v5 = buf[w][q + 5], v6 = buf[w][q + 6], v7 = buf[w][q + 7];
+          t += v0; t += v1; t += v2; t += v3; t += v4; t += v5; t += v6; t += v7;
+        }
+        for (; q < m; q++) t += buf[w][q];
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -322,8 +328,7 @@ __global__ void k_rowsum(const uint64_t *ro, const double *a, uint32_t rn, doubl
   }
 }
 extern "C" void amgd_colsum(const dcsr *Mt, double *z) {
-  if (Mt->rn) k_rowsum<<<grid_for(Mt->rn), 256, 0, amgd_s()>>>(Mt->ro, Mt->a, Mt->rn, z);
-  KCHECK();
+  amgd_spmv(Mt, nullptr, z, 0.0, nullptr, 1.0, nullptr);   // t = sum of a, row order
 }
 
 // ---------------------------------------------------------------------------
@@ -527,9 +532,18 @@ __global__ void k_spgemm_ub(const uint64_t *aro, const uint32_t *acol, uint32_t 
 }
 __global__ void k_split_rows(const uint64_t *ub, uint32_t rn, uint32_t *shortl, uint32_t *longl,
                              unsigned *counts) {
-  GRID_STRIDE(i, rn) {
-    if (ub[i] <= SHORT_UB) shortl[atomicAdd(&counts[0], 1u)] = (uint32_t)i;
-    else longl[atomicAdd(&counts[1], 1u)] = (uint32_t)i;
+  // every lane of a wave iterates the same number of times (wave_append needs the whole wave)
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t iters = (rn + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {
+    uint64_t i = i0 + it * stride;
+    bool v = i < rn;
+    bool sh = v && ub[i] <= SHORT_UB;
+    unsigned ps = wave_append(&counts[0], sh);
+    unsigned pl = wave_append(&counts[1], v && !sh);
+    if (sh) shortl[ps] = (uint32_t)i;
+    else if (v) longl[pl] = (uint32_t)i;
   }
 }
 
@@ -670,6 +684,122 @@ __global__ __launch_bounds__(256) void k_spgemm_long(
   }
 }
 
+// mid rows (more than SHORT_UB products): one 256-thread block per row, an
+// 8192-slot open-addressing hash in LDS, a block barrier per k step (so every
+// slot sees its additions in ascending k), and a bitonic sort of the (column,
+// value) pairs for the ordered write.  Rows with more than MID_CAP distinct
+// columns overflow to the dense-slab kernel above.
+#define MID_SLOTS 8192
+#define MID_CAP 4096
+#define OVERFLOW_MARK 0xffffffffffffffffull
+__device__ inline uint32_t hslot13(uint32_t j) { return (j * 2654435761u) >> (32 - 13); }
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_spgemm_mid(const uint32_t *rows, uint32_t nrows,
+                                                    const uint64_t *aro, const uint32_t *acol,
+                                                    const double *aa, const uint64_t *bro,
+                                                    const uint32_t *bcol, const double *ba,
+                                                    uint64_t *cnt, const uint64_t *xro,
+                                                    uint32_t *xcol, double *xa) {
+  __shared__ uint32_t hk[MID_SLOTS];
+  __shared__ double hv[MID_SLOTS];
+  __shared__ uint32_t sk[MODE == 1 ? MID_CAP : 1];
+  __shared__ double sv[MODE == 1 ? MID_CAP : 1];
+  __shared__ unsigned nfill, nout;
+  __shared__ int ovf;
+  const int tid = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    uint32_t i = rows[r];
+    for (int q = tid; q < MID_SLOTS; q += 256) { hk[q] = EMPTY_KEY; hv[q] = 0.0; }
+    if (tid == 0) { nfill = 0; nout = 0; ovf = 0; }
+    __syncthreads();
+    uint64_t a0 = aro[i], a1 = aro[i + 1];
+    for (uint64_t ka = a0; ka < a1 && !ovf; ka++) {
+      uint32_t k = acol[ka];
+      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
+      double av = aa[ka];
+      uint64_t b0 = bro[k], b1 = bro[k + 1];
+      for (uint64_t c0 = b0; c0 < b1; c0 += 256) {
+        uint64_t kb = c0 + tid;
+        if (kb < b1 && !ovf) {
+          uint32_t j = bcol[kb];
+          uint32_t sl = hslot13(j);
+          bool ok = true;
+          while (true) {
+            uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
+            if (old == EMPTY_KEY) {
+              if (atomicAdd(&nfill, 1u) >= MID_CAP) { ovf = 1; ok = false; }
+              break;
+            }
+            if (old == j) break;
+            sl = (sl + 1) & (MID_SLOTS - 1);
+          }
+          if (MODE == 1 && ok) hv[sl] = hv[sl] + ba[kb] * av;
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    if (ovf) {                    // symbolic only (numeric rows were routed by count)
+      if (tid == 0) cnt[i] = OVERFLOW_MARK;
+      __syncthreads();
+      continue;
+    }
+    if (MODE == 0) {
+      if (tid == 0) cnt[i] = nfill;
+      __syncthreads();
+      continue;
+    }
+    for (int q = tid; q < MID_SLOTS; q += 256) {
+      uint32_t key = hk[q];
+      if (key != EMPTY_KEY && hv[q] != 0.0) {
+        unsigned p = atomicAdd(&nout, 1u);
+        sk[p] = key;
+        sv[p] = hv[q];
+      }
+    }
+    __syncthreads();
+    unsigned n = nout, P = 1;
+    while (P < n) P <<= 1;
+    for (unsigned q = n + tid; q < P; q += 256) { sk[q] = EMPTY_KEY; sv[q] = 0.0; }
+    __syncthreads();
+    for (unsigned size = 2; size <= P; size <<= 1)
+      for (unsigned stride = size >> 1; stride > 0; stride >>= 1) {
+        for (unsigned t = tid; t < P / 2; t += 256) {
+          unsigned lo = 2 * t - (t & (stride - 1));
+          unsigned hi = lo + stride;
+          bool up = ((lo & size) == 0);
+          uint32_t kl = sk[lo], kh = sk[hi];
+          if ((kl > kh) == up) {
+            sk[lo] = kh; sk[hi] = kl;
+            double v = sv[lo]; sv[lo] = sv[hi]; sv[hi] = v;
+          }
+        }
+        __syncthreads();
+      }
+    uint64_t base = xro[i];
+    for (unsigned q = tid; q < n; q += 256) { xcol[base + q] = sk[q]; xa[base + q] = sv[q]; }
+    if (tid == 0) cnt[i] = n;
+    __syncthreads();
+  }
+}
+__global__ void k_route_overflow(const uint32_t *midl, uint32_t nmid, const uint64_t *cnt,
+                                 uint32_t *midok, uint32_t *dense, unsigned *counts) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t iters = (nmid + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {
+    uint64_t r = r0 + it * stride;
+    bool v = r < nmid;
+    uint32_t i = v ? midl[r] : 0;
+    bool o = v && cnt[i] == OVERFLOW_MARK;
+    unsigned p0 = wave_append(&counts[0], v && !o);
+    unsigned p1 = wave_append(&counts[1], o);
+    if (v && !o) midok[p0] = i;
+    if (o) dense[p1] = i;
+  }
+}
+
 void amgd_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *sa,
                        const uint64_t *dro, uint32_t rn, uint32_t *dcol, double *da);
 
@@ -706,35 +836,54 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   HIPCK(hipMemsetAsync(cnt, 0, ((size_t)rn + 1) * 8, s));
   double *slab_v = nullptr;
   uint32_t *slab_s = nullptr;
-  int nlb = (int)std::min<unsigned>(hc[1], LONG_BLOCKS);
-  if (hc[1]) {
-    slab_v = (double *)amgd_alloc((size_t)nlb * B->cn * 8 + 8);
-    slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
-    HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
-  }
   int gs = (int)std::min<unsigned>(std::max(hc[0], 1u), 65536u);
+  // symbolic: short rows (wave hash), mid rows (block hash, may overflow)
   if (hc[0])
     k_spgemm_short<0><<<gs, 64, 0, s>>>(shortl, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a,
                                         cnt, nullptr, nullptr, nullptr);
   if (hc[1])
-    k_spgemm_long<0><<<nlb, 256, 0, s>>>(longl, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
-                                          B->cn, slab_v, slab_s, cnt, nullptr, nullptr, nullptr);
+    k_spgemm_mid<0><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
+        longl, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, cnt, nullptr, nullptr, nullptr);
   KCHECK();
+  uint32_t *midok = nullptr, *densel = nullptr;
+  unsigned hr[2] = {0, 0};
+  if (hc[1]) {
+    midok = (uint32_t *)amgd_alloc((size_t)hc[1] * 4 + 4);
+    densel = (uint32_t *)amgd_alloc((size_t)hc[1] * 4 + 4);
+    unsigned *rc = (unsigned *)amgd_alloc(8);
+    HIPCK(hipMemsetAsync(rc, 0, 8, s));
+    k_route_overflow<<<grid_for(hc[1]), 256, 0, s>>>(longl, hc[1], cnt, midok, densel, rc);
+    amgd_d2h(hr, rc, 8);
+    amgd_free(rc);
+  }
+  int nlb = (int)std::min<unsigned>(hr[1], LONG_BLOCKS);
+  if (hr[1]) {
+    slab_v = (double *)amgd_alloc((size_t)nlb * B->cn * 8 + 8);
+    slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
+    HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
+    k_spgemm_long<0><<<nlb, 256, 0, s>>>(densel, hr[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
+                                          B->cn, slab_v, slab_s, cnt, nullptr, nullptr, nullptr);
+    KCHECK();
+  }
   uint64_t dist = amgd_scan_u64(cnt, rn);   // cnt := offsets of the distinct layout
   uint32_t *tcol = (uint32_t *)amgd_alloc(dist * 4 + 4);
   double *ta = (double *)amgd_alloc(dist * 8 + 8);
   uint64_t *cnt2 = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
   HIPCK(hipMemsetAsync(cnt2, 0, ((size_t)rn + 1) * 8, s));
-  if (hc[1]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
+  if (hr[1]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
   if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
   if (hc[0])
     k_spgemm_short<1><<<gs, 64, 0, s>>>(shortl, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a,
                                         cnt2, cnt, tcol, ta);
-  if (hc[1])
-    k_spgemm_long<1><<<nlb, 256, 0, s>>>(longl, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
+  if (hr[0])
+    k_spgemm_mid<1><<<(int)std::min<unsigned>(hr[0], 16384u), 256, 0, s>>>(
+        midok, hr[0], A->ro, A->col, A->a, B->ro, B->col, B->a, cnt2, cnt, tcol, ta);
+  if (hr[1])
+    k_spgemm_long<1><<<nlb, 256, 0, s>>>(densel, hr[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
                                           B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
+  if (midok) { amgd_free(midok); amgd_free(densel); }
   uint64_t nz = amgd_scan_u64(cnt2, rn);
   if (g_sg_slot >= 0)
     g_sg_bytes += 12 * (A->nnz + B->nnz + nz) + 8 * ((uint64_t)A->rn + B->rn + rn + 3);

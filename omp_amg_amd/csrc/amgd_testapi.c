@@ -91,6 +91,23 @@ API int amgd_test_math(int op, uint64_t n, const double *a, const double *b, dou
   return 0;
 }
 
+/* exact dot: mode 0 a.b, 1 a.a, 2 (a.*b).*b; plain=1 uses the one-lane loop */
+extern void amgd_set_seq_plain(int on);
+API double amgd_test_dot(int mode, uint64_t n, const double *a, const double *b, int plain, int exact) {
+  if (amgd_rt_init(0) != 0) return 0.0 / 0.0;
+  double *da = (double *)amgd_alloc(n * 8 + 8), *db = (double *)amgd_alloc(n * 8 + 8);
+  amgd_h2d(da, a, n * 8);
+  amgd_h2d(db, b, n * 8);
+  int old = amgd_get_exact();
+  amgd_set_exact(exact);
+  amgd_set_seq_plain(plain);
+  double r = mode == 0 ? amgd_dot(da, db, n) : mode == 1 ? amgd_dot(da, NULL, n) : amgd_dot3(da, db, n);
+  amgd_set_seq_plain(0);
+  amgd_set_exact(old);
+  amgd_free(da); amgd_free(db);
+  return r;
+}
+
 API void amgd_test_free(hcsr *H) {
   free(H->ro); free(H->col); free(H->a);
   H->ro = NULL; H->col = NULL; H->a = NULL;

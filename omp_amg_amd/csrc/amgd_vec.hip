@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cfloat>
 #include <cstdio>
+#include <algorithm>
 
 #include "amgd.h"
 #include "amgd_dev.h"
@@ -173,9 +174,46 @@ __global__ void k_matmax_gather(const uint64_t *tro, const uint32_t *tcol, const
     y[k] = m;
   }
 }
+__global__ __launch_bounds__(256) void k_amax_wave(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, uint32_t rn, const uint8_t *f,
+                                                   double tol, double *amax) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < rn; i += (uint64_t)gridDim.x * 4) {
+    double m = 0;
+    for (uint64_t k = ro[i] + lane; k < ro[i + 1]; k += 64)
+      if (f[col[k]] != 0 && fabs(a[k]) > m) m = fabs(a[k]);
+    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_down(m, o, 64); m = u > m ? u : m; }
+    if (lane == 0) amax[i] = m * tol;
+  }
+}
+__global__ __launch_bounds__(256) void k_matmax_gather_wave(const uint64_t *tro, const uint32_t *tcol,
+                                                            const double *ta, uint32_t n,
+                                                            const uint8_t *f, const double *x,
+                                                            const double *amax, double *y) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += (uint64_t)gridDim.x * 4) {
+    double m = -DBL_MAX;
+    if (f[k] != 0)
+      for (uint64_t t = tro[k] + lane; t < tro[k + 1]; t += 64) {
+        uint32_t i = tcol[t];
+        if (fabs(ta[t]) < amax[i]) continue;
+        double xi = x[i];
+        if (xi > m) m = xi;
+      }
+    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_down(m, o, 64); m = u > m ? u : m; }
+    if (lane == 0) y[k] = m;
+  }
+}
 extern "C" void amgd_mat_max(const dcsr *S, const dcsr *St, const uint8_t *f, const double *x,
                              double tol, double *amax, double *y) {
   if (!S->rn) return;
+  if (S->nnz >= 24ull * S->rn) {   // long rows: one wavefront per row (max is order-free)
+    int g = (int)std::min<uint64_t>((S->rn + 3) / 4, 65536);
+    k_amax_wave<<<g, 256, 0, amgd_s()>>>(S->ro, S->col, S->a, S->rn, f, tol, amax);
+    k_matmax_gather_wave<<<g, 256, 0, amgd_s()>>>(St->ro, St->col, St->a, St->rn, f, x, amax, y);
+    KCHECK();
+    return;
+  }
   k_amax<<<grid_for(S->rn), 256, 0, amgd_s()>>>(S->ro, S->col, S->a, S->rn, f, tol, amax);
   k_matmax_gather<<<grid_for(St->rn), 256, 0, amgd_s()>>>(St->ro, St->col, St->a, St->rn, f, x,
                                                            amax, y);

@@ -28,6 +28,14 @@ def test_spgemm_long_rows_and_cancellation():
     assert refops.same(X, R)
 
 
+def test_spgemm_dense_overflow_rows():
+    """rows with more than 4096 distinct columns take the dense-slab path"""
+    rng = np.random.default_rng(8)
+    A = refops.rand_csr(rng, 12, 1500, 0.5)
+    B = refops.rand_csr(rng, 1500, 7000, 0.02)
+    assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
+
+
 def test_spgemm_empty_rows():
     rng = np.random.default_rng(3)
     A = refops.rand_csr(rng, 50, 40, 0.02)
@@ -107,3 +115,42 @@ def test_device_math_is_ieee():
     assert np.array_equal(oa.test_math(0, a), np.sqrt(a))
     assert np.array_equal(oa.test_math(1, a), 1.0 / a)
     assert np.array_equal(oa.test_math(2, a, b), a / b)
+
+
+def _seq(p):
+    s = 0.0
+    for x in p.tolist():
+        s += x
+    return s
+
+
+@pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel"])
+def test_exact_dot_matches_sequential(kind):
+    """The binade-parallel exact sum equals the left-to-right loop bit for bit."""
+    rng = np.random.default_rng(hash(kind) % 2**32)
+    n = 300000
+    if kind == "normal":
+        a, b = rng.standard_normal(n), rng.standard_normal(n)
+    elif kind == "positive":
+        a = np.abs(rng.standard_normal(n)); b = a.copy()
+    elif kind == "ints":
+        a, b = rng.integers(-5, 6, n).astype(float), rng.integers(-5, 6, n).astype(float)
+    elif kind == "ties":
+        a = np.ones(n); a[0] = 2.0 ** 53; b = np.ones(n)
+    elif kind == "zeros":
+        a = rng.standard_normal(n); a[: n // 2] = 0.0; a[n // 2 + 5: n // 2 + 9000] = 0.0; b = rng.standard_normal(n)
+    elif kind == "range":
+        a = rng.standard_normal(n) * 10.0 ** rng.integers(-40, 40, n); b = rng.standard_normal(n)
+    else:
+        a = rng.standard_normal(n); a[1::2] = -a[::2][: len(a[1::2])]; b = np.ones(n)
+    for mode in (0, 1, 2):
+        if mode == 0:
+            ref = _seq(a * b)
+        elif mode == 1:
+            ref = _seq(a * a)
+        else:
+            ref = _seq((a * b) * b)
+        got = oa.test_dot(mode, a, b)
+        plain = oa.test_dot(mode, a, b, plain=True)
+        assert np.float64(got).view(np.uint64) == np.float64(ref).view(np.uint64), (mode, got, ref)
+        assert np.float64(plain).view(np.uint64) == np.float64(ref).view(np.uint64), (mode, plain, ref)
