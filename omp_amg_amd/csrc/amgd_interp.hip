@@ -62,65 +62,228 @@ extern "C" dcsr *amgd_min_skel(const dcsr *R) {
 }
 
 // ---------------------------------------------------------------------------
-// Q factor: one block per support, NT threads; scratch (3*nz doubles) in LDS
-// for small supports, in a global slab for large ones.
+// Q factor (interp, amg_setup.c:2053-2099).  Per support of nz points, for
+// k = 0..nz-1:
+//   s1[m] = A(Qj[k], Qj[m])  (m <= k)
+//   s2[i] = sum_{j<=i} U[i][j] s1[j]          (mv_utt, i < k)
+//   qk[i] = sum_{j=i}^{k-1} U[j][i] s2[j]     (mv_ut)
+//   al = -1/sqrt(s1[k] - sum_m s1[m] qk[m]);  U[k][i] = qk[i] al, U[k][k] = -al
+// U is the packed row-major triangle (row i at tri(i)).  Every sum keeps the
+// reference's order, one lane per output.  Three tiers by nz:
+//   nz <=  64 / <= 128 : the whole triangle in LDS, one wavefront per support
+//   nz <= 1024         : 256 threads, U in HBM; loads are issued QB at a time
+//                        ahead of the ordered adds (the sums are latency-bound
+//                        chains), mv_ut walks j in lock-step so every load
+//                        instruction of a wave is one coalesced row segment
+//   nz  > 1024         : (the orphan support gathered at coarse point 0) all
+//                        lanes of a cooperative grid, three grid barriers per k
 // ---------------------------------------------------------------------------
 #define QF_LDS_NZ 512
-template <int NT, bool GSCR>
-__global__ __launch_bounds__(NT) void k_qfactor(const uint32_t *rows, uint32_t nrows,
-                                                const uint64_t *wro, const uint32_t *wcol,
-                                                const uint64_t *aro, const uint32_t *acol,
-                                                const double *aa, const uint64_t *qoff, double *Q,
-                                                double *gscr, uint64_t gstride) {
-  __shared__ double lds[GSCR ? 1 : 3 * QF_LDS_NZ];
-  __shared__ double sh_alpha;
-  const int tid = threadIdx.x;
+
+template <int NZMAX>
+__global__ __launch_bounds__(64) void k_qfactor_lds(const uint32_t *rows, uint32_t nrows,
+                                                    const uint64_t *wro, const uint32_t *wcol,
+                                                    const uint64_t *aro, const uint32_t *acol,
+                                                    const double *aa, const uint64_t *qoff,
+                                                    double *Q) {
+  __shared__ double U[NZMAX * (NZMAX + 1) / 2];
+  __shared__ double s1[NZMAX], s2[NZMAX], qk[NZMAX];
+  __shared__ double sh_al;
+  const int t = threadIdx.x;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    uint32_t c = rows[r];
-    uint64_t w0 = wro[c];
-    uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t c = rows[r];
+    const uint64_t w0 = wro[c];
+    const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
     const uint32_t *Qj = wcol + w0;
-    double *Qc = Q + qoff[c];
-    double *sqv1, *sqv2, *qk;
-    if (GSCR) {
-      sqv1 = gscr + (uint64_t)blockIdx.x * gstride;
-      sqv2 = sqv1 + nz;
-      qk = sqv2 + nz;
-    } else {
-      sqv1 = lds;
-      sqv2 = lds + QF_LDS_NZ;
-      qk = lds + 2 * QF_LDS_NZ;
-    }
     for (uint32_t k = 0; k < nz; k++) {
-      uint32_t s = Qj[k];
-      uint64_t a0 = aro[s], a1 = aro[s + 1];
-      for (uint32_t m = tid; m <= k; m += NT) sqv1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+      const uint32_t sk = Qj[k];
+      const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
+      for (uint32_t m = t; m <= k; m += 64) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
       __syncthreads();
-      for (uint32_t i = tid; i < k; i += NT) {        // sqv2 = Q^t sqv1  (mv_utt)
-        const double *U = Qc + tri(i);
+      for (uint32_t i = t; i < k; i += 64) {
+        const double *Ui = U + tri(i);
         double v = 0;
-        for (uint32_t j = 0; j <= i; j++) v += U[j] * sqv1[j];
-        sqv2[i] = v;
+        for (uint32_t j = 0; j <= i; j++) v += Ui[j] * s1[j];
+        s2[i] = v;
       }
       __syncthreads();
-      for (uint32_t i = tid; i < k; i += NT) {        // qk = Q sqv2  (mv_ut)
+      for (uint32_t i = t; i < k; i += 64) {
         double y = 0;
-        for (uint32_t j = i; j < k; j++) y += Qc[tri(j) + i] * sqv2[j];
+        for (uint32_t j = i; j < k; j++) y += U[tri(j) + i] * s2[j];
         qk[i] = y;
       }
       __syncthreads();
-      if (tid == 0) {
-        double al = sqv1[k];
-        for (uint32_t m = 0; m < k; m++) al -= sqv1[m] * qk[m];
-        sh_alpha = -1.0 / sqrt(al);
+      if (t == 0) {
+        double al = s1[k];
+        for (uint32_t m = 0; m < k; m++) al -= s1[m] * qk[m];
+        sh_al = -1.0 / sqrt(al);
       }
       __syncthreads();
-      double al = sh_alpha;
-      double *out = Qc + tri(k);
-      for (uint32_t i = tid; i < k; i += NT) out[i] = qk[i] * al;
-      if (tid == 0) out[k] = -al;
+      const double al = sh_al;
+      double *out = U + tri(k);
+      for (uint32_t i = t; i < k; i += 64) out[i] = qk[i] * al;
+      if (t == 0) out[k] = -al;
       __syncthreads();
     }
+    double *Qc = Q + qoff[c];
+    const uint32_t tn = nz * (nz + 1) / 2;
+    for (uint32_t e = t; e < tn; e += 64) Qc[e] = U[e];
+    __syncthreads();
+  }
+}
+
+// sum_{j<n} u[j]*x[j] in order, loads issued QB at a time (latency hiding)
+#define QB 32
+__device__ __forceinline__ double seq_dot_batched(const double *u, const double *x, uint32_t n) {
+  double v = 0;
+  for (uint32_t j0 = 0; j0 < n; j0 += QB) {
+    double r[QB];
+#pragma unroll
+    for (int q = 0; q < QB; q++) r[q] = (j0 + q < n) ? u[j0 + q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < QB; q++)
+      if (j0 + q < n) v += r[q] * x[j0 + q];
+  }
+  return v;
+}
+// qk[i] = sum_{j=i}^{k-1} U[tri(j)+i] s2[j]; the lanes of a wave (i = ib+lane) walk j in
+// lock-step from ib so each load instruction reads 64 consecutive doubles of row j
+__device__ __forceinline__ double mv_ut_lane(const double *U, const double *s2, uint32_t ib,
+                                            uint32_t i, uint32_t k) {
+  double y = 0;
+  for (uint32_t j0 = ib; j0 < k; j0 += QB) {
+    double r[QB];
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+      uint32_t j = j0 + q;
+      r[q] = (j < k && j >= i) ? U[tri(j) + i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < QB; q++) {
+      uint32_t j = j0 + q;
+      if (j < k && j >= i) y += r[q] * s2[j];
+    }
+  }
+  return y;
+}
+
+// mid supports: one 256-thread block each, U in HBM (the output), s1/s2/qk in LDS
+__global__ __launch_bounds__(256) void k_qfactor_mid(const uint32_t *rows, uint32_t nrows,
+                                                     const uint64_t *wro, const uint32_t *wcol,
+                                                     const uint64_t *aro, const uint32_t *acol,
+                                                     const double *aa, const uint64_t *qoff,
+                                                     double *Q) {
+  __shared__ double s1[1024], s2[1024], qk[1024];
+  __shared__ double sh_al;
+  const int t = threadIdx.x, lane = t & 63;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t c = rows[r];
+    const uint64_t w0 = wro[c];
+    const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t *Qj = wcol + w0;
+    double *U = Q + qoff[c];
+    for (uint32_t k = 0; k < nz; k++) {
+      const uint32_t sk = Qj[k];
+      const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
+      for (uint32_t m = t; m <= k; m += 256) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+      __syncthreads();
+      for (uint32_t i = t; i < k; i += 256) s2[i] = seq_dot_batched(U + tri(i), s1, i + 1);
+      __syncthreads();
+      for (uint32_t ib = t - lane; ib < k; ib += 256) {
+        const uint32_t i = ib + lane;
+        double y = mv_ut_lane(U, s2, ib, i, k);
+        if (i < k) qk[i] = y;
+      }
+      __syncthreads();
+      if (t == 0) {
+        double al = s1[k];
+        for (uint32_t m = 0; m < k; m++) al -= s1[m] * qk[m];
+        sh_al = -1.0 / sqrt(al);
+      }
+      __syncthreads();
+      const double al = sh_al;
+      double *out = U + tri(k);
+      for (uint32_t i = t; i < k; i += 256) out[i] = qk[i] * al;
+      if (t == 0) out[k] = -al;
+      __syncthreads();
+    }
+  }
+}
+
+// grid barrier for the cooperative kernel (all blocks resident)
+__device__ __forceinline__ void grid_sync(unsigned *bar, unsigned nblocks, unsigned &gen) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned a = atomicAdd(&bar[0], 1u);
+    if (a == nblocks - 1) {
+      atomicExch(&bar[0], 0u);
+      __threadfence();
+      atomicAdd(&bar[1], 1u);
+    } else {
+      while (__hip_atomic_load(&bar[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen)
+        __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __threadfence();
+  gen++;
+}
+
+// huge supports (nz <= QF_COOP_MAX): one support at a time over a cooperative
+// grid of 64-lane blocks; s1/s2/qk are global (shared by the blocks) and staged
+// through LDS where a block reads them serially
+#define QF_COOP_MAX 8192
+__global__ __launch_bounds__(64) void k_qfactor_coop(uint32_t c, const uint64_t *wro,
+                                                     const uint32_t *wcol, const uint64_t *aro,
+                                                     const uint32_t *acol, const double *aa,
+                                                     const uint64_t *qoff, double *Q,
+                                                     double *s1b, double *s2, double *qk,
+                                                     unsigned *bar) {
+  extern __shared__ double xs[];      // 2 * nz doubles
+  __shared__ double sh_al;
+  const uint32_t lane = threadIdx.x, G = gridDim.x;
+  const uint32_t gt = blockIdx.x * 64 + lane, GT = G * 64;
+  const uint64_t w0 = wro[c];
+  const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+  const uint32_t *Qj = wcol + w0;
+  double *U = Q + qoff[c];
+  double *xa = xs, *xb = xs + nz;
+  unsigned gen = 0;
+  for (uint32_t k = 0; k <= nz; k++) {
+    if (k > 0) {                                   // finish row k-1 (every block computes al)
+      const uint32_t kp = k - 1;
+      const double *s1p = s1b + (uint64_t)(kp & 1) * nz;
+      for (uint32_t m = lane; m <= kp; m += 64) { xa[m] = s1p[m]; xb[m] = qk[m]; }
+      __syncthreads();
+      if (lane == 0) {
+        double al = xa[kp];
+        for (uint32_t m = 0; m < kp; m++) al -= xa[m] * xb[m];
+        sh_al = -1.0 / sqrt(al);
+      }
+      __syncthreads();
+      const double al = sh_al;
+      for (uint32_t i = gt; i < kp; i += GT) U[tri(kp) + i] = xb[i] * al;
+      if (gt == 0) U[tri(kp) + kp] = -al;
+    }
+    if (k == nz) break;
+    double *s1 = s1b + (uint64_t)(k & 1) * nz;
+    const uint32_t sk = Qj[k];
+    const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
+    for (uint32_t m = gt; m <= k; m += GT) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+    grid_sync(bar, G, gen);
+    for (uint32_t m = lane; m <= k; m += 64) xa[m] = s1[m];
+    __syncthreads();
+    for (uint32_t i = gt; i < k; i += GT) s2[i] = seq_dot_batched(U + tri(i), xa, i + 1);
+    grid_sync(bar, G, gen);
+    for (uint32_t m = lane; m < k; m += 64) xa[m] = s2[m];
+    __syncthreads();
+    for (uint32_t ib = gt - lane; ib < k; ib += GT) {
+      const uint32_t i = ib + lane;
+      double y = mv_ut_lane(U, xa, ib, i, k);
+      if (i < k) qk[i] = y;
+    }
+    grid_sync(bar, G, gen);
   }
 }
 
@@ -130,19 +293,24 @@ __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
     sz[c] = nz * (nz + 1) / 2;
   }
 }
-__global__ void k_split_by_nz(const uint64_t *wro, uint32_t rn, uint32_t cap, uint32_t *sl,
-                              uint32_t *bl, unsigned *cnt) {
+// columns binned by support size nz (empty supports skipped) against lim[0..nb-2]
+__global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, uint32_t l0, uint32_t l1, uint32_t l2,
+                         int nb, uint32_t *lists, unsigned *cnt) {
+  const uint32_t lim[3] = {l0, l1, l2};
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (rn + stride - 1) / stride;
-  for (uint64_t it = 0; it < iters; it++) {
+  for (uint64_t it = 0; it < iters; it++) {   // uniform trip count (wave_append)
     uint64_t c = c0 + it * stride;
     uint64_t nz = c < rn ? wro[c + 1] - wro[c] : 0;
-    bool sm = nz != 0 && nz <= cap, bg = nz > cap;
-    unsigned ps = wave_append(&cnt[0], sm);
-    unsigned pb = wave_append(&cnt[1], bg);
-    if (sm) sl[ps] = (uint32_t)c;
-    if (bg) bl[pb] = (uint32_t)c;
+    int bin = nb - 1;
+    for (int q = nb - 2; q >= 0; q--)
+      if (nz <= lim[q]) bin = q;
+    for (int q = 0; q < nb; q++) {
+      bool take = nz != 0 && bin == q;
+      unsigned p = wave_append(&cnt[q], take);
+      if (take) lists[(uint64_t)q * ((uint64_t)rn + 1) + p] = (uint32_t)c;
+    }
   }
 }
 __global__ void k_max_nz(const uint64_t *wro, uint32_t rn, unsigned long long *mx) {
@@ -158,54 +326,106 @@ struct RowSplit {
 };
 static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
   RowSplit rs;
-  rs.sl = (uint32_t *)amgd_alloc(((size_t)Wt->rn + 1) * 4);
-  rs.bl = (uint32_t *)amgd_alloc(((size_t)Wt->rn + 1) * 4);
-  unsigned *cnt = (unsigned *)amgd_alloc(16);
-  amgd_memset(cnt, 0, 16);
+  const uint64_t L = (uint64_t)Wt->rn + 1;
+  rs.sl = (uint32_t *)amgd_alloc(2 * L * 4);
+  rs.bl = rs.sl + L;
+  unsigned *cnt = (unsigned *)amgd_alloc(32);
+  amgd_memset(cnt, 0, 32);
   if (Wt->rn) {
-    k_split_by_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, rs.sl, rs.bl, cnt);
-    k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 2));
+    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, 0, 0, 2, rs.sl, cnt);
+    k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 4));
   }
-  unsigned h[4];
-  amgd_d2h(h, cnt, 16);
+  unsigned h[8];
+  amgd_d2h(h, cnt, 32);
   amgd_free(cnt);
   rs.ns = h[0];
   rs.nb = h[1];
   uint64_t mx;
-  memcpy(&mx, &h[2], 8);
+  memcpy(&mx, &h[4], 8);
   rs.maxnz = mx;
   return rs;
 }
-static void free_split(RowSplit &rs) { amgd_free(rs.sl); amgd_free(rs.bl); }
+static void free_split(RowSplit &rs) { amgd_free(rs.sl); }
 
+#define QF_T1 64
+#define QF_T2 128
+#define QF_T3 1024
 extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
                                 uint64_t *qtotal) {
   hipStream_t s = amgd_s();
-  uint64_t *qoff = (uint64_t *)amgd_alloc(((size_t)Wt->rn + 1) * 8);
-  if (Wt->rn) k_qsize<<<grid_for(Wt->rn), 256, 0, s>>>(Wt->ro, Wt->rn, qoff);
-  uint64_t tot = amgd_scan_u64(qoff, Wt->rn);
+  static int sglog = -1;
+  if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
+  double t_start = 0;
+  if (sglog) { amgd_sync(); t_start = amgd_wtime(); }
+  const uint32_t rn = Wt->rn;
+  const uint64_t L = (uint64_t)rn + 1;
+  uint64_t *qoff = (uint64_t *)amgd_alloc(L * 8);
+  if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
+  uint64_t tot = amgd_scan_u64(qoff, rn);
   double *Q = (double *)amgd_alloc(tot * 8 + 8);
-  RowSplit rs = split_rows(Wt, QF_LDS_NZ);
-  if (rs.ns) {
-    int g = (int)std::min<unsigned>(rs.ns, 65536u);
-    k_qfactor<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, A->ro, A->col, A->a, qoff,
-                                          Q, nullptr, 0);
+  uint32_t *lists = (uint32_t *)amgd_alloc(4 * L * 4);
+  unsigned *cnt = (unsigned *)amgd_alloc(32);
+  amgd_memset(cnt, 0, 32);
+  unsigned hn[4] = {0, 0, 0, 0};
+  if (rn) {
+    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, QF_T1, QF_T2, QF_T3, 4, lists, cnt);
     KCHECK();
+    amgd_d2h(hn, cnt, 16);
   }
-  if (rs.nb) {
-    int g = (int)std::min<unsigned>(rs.nb, 1024u);
-    uint64_t stride = 3 * rs.maxnz + 8;
-    double *scr = (double *)amgd_alloc((size_t)g * stride * 8);
-    k_qfactor<256, true><<<g, 256, 0, s>>>(rs.bl, rs.nb, Wt->ro, Wt->col, A->ro, A->col, A->a, qoff,
-                                           Q, scr, stride);
-    KCHECK();
-    amgd_free(scr);
+  if (hn[0])
+    k_qfactor_lds<QF_T1><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
+        lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (hn[1])
+    k_qfactor_lds<QF_T2><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
+        lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (hn[2])
+    k_qfactor_mid<<<(int)std::min<unsigned>(hn[2], 8192u), 256, 0, s>>>(
+        lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  KCHECK();
+  if (hn[3]) {                    // huge supports, one cooperative launch each
+    std::vector<uint32_t> big(hn[3]);
+    amgd_d2h(big.data(), lists + 3 * L, (size_t)hn[3] * 4);
+    std::vector<uint64_t> ro(rn + 1);
+    amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
+    for (uint32_t c : big) {
+      uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
+      if (nz > QF_COOP_MAX) {
+        fprintf(stderr, "omp_amg_amd: support of %u points exceeds QF_COOP_MAX\n", nz);
+        abort();
+      }
+      double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
+      double *s2 = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
+      unsigned *bar = (unsigned *)amgd_alloc(16);
+      amgd_memset(bar, 0, 16);
+      int G = (int)std::min<uint32_t>((nz + 63) / 64, 256u);
+      const uint64_t *pwro = Wt->ro, *paro = A->ro, *pqoff = qoff;
+      const uint32_t *pwcol = Wt->col, *pacol = A->col;
+      const double *paa = A->a;
+      void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2, &qk, &bar};
+      static bool attr = false;
+      if (!attr) {
+        HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
+        attr = true;
+      }
+      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
+                                       (unsigned)(2 * (size_t)nz * 8), s));
+      KCHECK();
+      amgd_free(s1b); amgd_free(bar);
+    }
   }
-  free_split(rs);
+  if (sglog) {
+    amgd_sync();
+    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u Q %lu  %.2f ms\n", rn,
+            (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], (unsigned long)tot,
+            (amgd_wtime() - t_start) * 1e3);
+  }
+  amgd_free(lists); amgd_free(cnt);
   *qoff_out = qoff;
   if (qtotal) *qtotal = tot;
   return Q;
 }
+
 
 // ---------------------------------------------------------------------------
 // Q application (the tail of interp, amg_setup.c:2100-2108):

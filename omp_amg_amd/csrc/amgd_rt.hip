@@ -425,17 +425,17 @@ __device__ __forceinline__ long long bn_block_excl_scan(long long v, long long *
   return (long long)(incl - (unsigned long long)v);
 }
 
+__device__ __forceinline__ double bn_product(const double *a, const double *b, uint64_t i, int MODE_) {
+  double x = a[i];
+  return MODE_ == 0 ? x * b[i] : MODE_ == 1 ? x * x : (x * b[i]) * b[i];
+}
+// the whole block adds products [lo, hi) to the running sum s (uniform), in order
 template <int MODE>
-__global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, const double *b,
-                                                           uint64_t n, double *out) {
-  __shared__ double tile[BN_TILE];
-  __shared__ long long sh[BN_THREADS / 64 + 1];
-  __shared__ double s_sh;
-  __shared__ int viol_sh;
+__device__ double binade_range(const double *a, const double *b, uint64_t lo, uint64_t hi, double s,
+                               double *tile, long long *sh, double *s_sh, int *viol_sh) {
   const int tid = threadIdx.x;
-  double s = 0.0;                      // uniform running sum
-  for (uint64_t base = 0; base < n; base += BN_TILE) {
-    int tlen = (int)min((uint64_t)BN_TILE, n - base);
+  for (uint64_t base = lo; base < hi; base += BN_TILE) {
+    int tlen = (int)min((uint64_t)BN_TILE, hi - base);
     for (int q = tid; q < tlen; q += BN_THREADS) {
       uint64_t i = base + q;
       double x = a[i];
@@ -448,12 +448,12 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, cons
       // subnormal s), or once a tile has needed too many re-scans
       if (s == 0.0 && rounds <= 48) {
         // 0 + p == p exactly (and +0 for a zero p): jump to the first nonzero product
-        if (tid == 0) viol_sh = 0x7fffffff;
+        if (tid == 0) (*viol_sh) = 0x7fffffff;
         __syncthreads();
         for (int q = j + tid; q < tlen; q += BN_THREADS)
-          if (tile[q] != 0.0) { atomicMin(&viol_sh, q); break; }
+          if (tile[q] != 0.0) { atomicMin(&(*viol_sh), q); break; }
         __syncthreads();
-        int f = viol_sh;
+        int f = (*viol_sh);
         if (f == 0x7fffffff) { j = tlen; }
         else { s = s + tile[f]; j = f + 1; }
         __syncthreads();
@@ -464,10 +464,10 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, cons
           double t = s;
           int stop = rounds > 48 ? tlen : j + 1;
           for (int q = j; q < stop; q++) t += tile[q];
-          s_sh = t;
+          (*s_sh) = t;
         }
         __syncthreads();
-        s = s_sh;
+        s = (*s_sh);
         j = rounds > 48 ? tlen : j + 1;
         __syncthreads();
         continue;
@@ -509,11 +509,11 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, cons
         bool inside = S0 > 0 ? (run > LO && run < HI) : (run < -LO && run > -HI);
         if (!inside) myv = idx;
       }
-      if (tid == 0) viol_sh = 0x7fffffff;
+      if (tid == 0) (*viol_sh) = 0x7fffffff;
       __syncthreads();
-      if (myv != 0x7fffffff) atomicMin(&viol_sh, myv);
+      if (myv != 0x7fffffff) atomicMin(&(*viol_sh), myv);
       __syncthreads();
-      int v = viol_sh;
+      int v = (*viol_sh);
       if (v == 0x7fffffff) {
         // whole remainder stays inside the binade
         long long fin = (long long)((unsigned long long)S0 + (unsigned long long)total);
@@ -524,18 +524,213 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, cons
         if (first <= v - 1 && v - 1 < first + BN_PER) {
           long long r2 = (long long)((unsigned long long)S0 + (unsigned long long)pre);
           for (int q = 0; first + q < v; q++) r2 = (long long)((unsigned long long)r2 + (unsigned long long)m[q]);
-          s_sh = ldexp((double)r2, e - 52) + tile[v];
+          (*s_sh) = ldexp((double)r2, e - 52) + tile[v];
         }
-        if (v == j && tid == 0) s_sh = s + tile[v];
+        if (v == j && tid == 0) (*s_sh) = s + tile[v];
         __syncthreads();
-        s = s_sh;
+        s = (*s_sh);
         j = v + 1;
       }
       __syncthreads();
     }
     __syncthreads();
   }
+  return s;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, const double *b,
+                                                           uint64_t n, double *out) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  __shared__ double s_sh;
+  __shared__ int viol_sh;
+  double s = binade_range<MODE>(a, b, 0, n, 0.0, tile, sh, &s_sh, &viol_sh);
+  if (threadIdx.x == 0) *out = s;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-CU speculation for long vectors.  The vector is cut into chunks of
+// BN_TILE products.  (1) every chunk's plain sum, (2) an approximate prefix
+// -> a guessed binade e_c of the running sum entering chunk c, (3) for that
+// guess, in parallel over chunks: M_c = sum of rint(p/u_e) and the min / max
+// of its prefixes (or a flag: tie, huge, no usable guess).  (4) one block walks
+// the chunks in order with the exact running sum s: if s lies in binade e_c and
+// s/u + every prefix stays strictly inside the binade, the chunk is exactly
+// s + u*M_c (the same integer argument as above); otherwise that chunk is
+// added by binade_range.  The result is the sequential sum, bit for bit.
+// ---------------------------------------------------------------------------
+#define SP_T 256
+#define SP_PER (BN_TILE / SP_T)
+template <int MODE>
+__global__ __launch_bounds__(SP_T) void k_dot_csum(const double *a, const double *b, uint64_t n,
+                                                   double *csum) {
+  __shared__ double red[SP_T];
+  uint64_t G = (n + BN_TILE - 1) / BN_TILE;
+  for (uint64_t c = blockIdx.x; c < G; c += gridDim.x) {
+    uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
+    double t = 0;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += SP_T) t += bn_product(a, b, i, MODE);
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = SP_T / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) csum[c] = red[0];
+    __syncthreads();
+  }
+}
+// exclusive prefix of the chunk sums (any order: it is only a guess)
+__global__ __launch_bounds__(1024) void k_dot_approx_prefix(double *csum, uint64_t G) {
+  __shared__ double part[1024];
+  uint64_t per = (G + 1023) / 1024;
+  uint64_t lo = threadIdx.x * per, hi = min(G, lo + per);
+  double t = 0;
+  for (uint64_t c = lo; c < hi; c++) t += csum[c];
+  part[threadIdx.x] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = 0;
+    for (int q = 0; q < 1024; q++) { double v = part[q]; part[q] = r; r += v; }
+  }
+  __syncthreads();
+  double r = part[threadIdx.x];
+  for (uint64_t c = lo; c < hi; c++) { double v = csum[c]; csum[c] = r; r += v; }
+}
+struct SpecRec { long long M, mn, mx; int e, flag; };
+template <int MODE>
+__global__ __launch_bounds__(SP_T) void k_dot_spec(const double *a, const double *b, uint64_t n,
+                                                   const double *approx, SpecRec *rec) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long ssum[SP_T / 64], smin[SP_T / 64], smax[SP_T / 64];
+  __shared__ int sflag;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint64_t G = (n + BN_TILE - 1) / BN_TILE;
+  for (uint64_t c = blockIdx.x; c < G; c += gridDim.x) {
+    uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
+    int tlen = (int)(hi - lo);
+    for (int q = tid; q < tlen; q += SP_T) tile[q] = bn_product(a, b, lo + q, MODE);
+    if (tid == 0) sflag = 0;
+    __syncthreads();
+    double g = approx[c];
+    int flag = !(fabs(g) >= 1e-290) || !(fabs(g) < 1e300);
+    int e = flag ? 0 : ilogb(g);
+    double u = ldexp(1.0, e - 52);
+    long long loc = 0, lmin = 0x7fffffffffffffffll, lmax = -0x7fffffffffffffffll;
+    int first = tid * SP_PER;
+    for (int q = 0; q < SP_PER; q++) {
+      int idx = first + q;
+      if (idx >= tlen) break;
+      double x = tile[idx] / u;
+      double r = rint(x);
+      if (!(fabs(x) < 4.6e18) || fabs(r - x) == 0.5) { flag = 1; break; }
+      loc += (long long)r;
+      lmin = loc < lmin ? loc : lmin;
+      lmax = loc > lmax ? loc : lmax;
+    }
+    if (flag) atomicOr(&sflag, 1);
+    // exclusive scan of loc over the block; prefix extremes = pre + local extremes
+    long long x = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+      long long y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    long long pre_w = x - loc;                // exclusive within the wave
+    long long mn = first < tlen ? pre_w + lmin : 0x7fffffffffffffffll;
+    long long mx = first < tlen ? pre_w + lmax : -0x7fffffffffffffffll;
+    for (int o = 32; o > 0; o >>= 1) {
+      long long m1 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mx, o, 64);
+      mn = m1 < mn ? m1 : mn;
+      mx = m2 > mx ? m2 : mx;
+    }
+    if (lane == 63) ssum[w] = x;
+    if (lane == 0) { smin[w] = mn; smax[w] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      long long run = 0, gmn = 0x7fffffffffffffffll, gmx = -0x7fffffffffffffffll;
+      for (int q = 0; q < SP_T / 64; q++) {
+        if (smin[q] != 0x7fffffffffffffffll) {
+          gmn = run + smin[q] < gmn ? run + smin[q] : gmn;
+          gmx = run + smax[q] > gmx ? run + smax[q] : gmx;
+        }
+        run += ssum[q];
+      }
+      SpecRec r;
+      r.M = run; r.mn = gmn; r.mx = gmx; r.e = e; r.flag = sflag;
+      rec[c] = r;
+    }
+    __syncthreads();
+  }
+}
+#define SP_BATCH 512
+template <int MODE>
+__global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, const double *b,
+                                                            uint64_t n, const SpecRec *rec,
+                                                            double *out) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  __shared__ double s_sh;
+  __shared__ int viol_sh;
+  __shared__ SpecRec rb[SP_BATCH];
+  __shared__ unsigned long long cnext;
+  const int tid = threadIdx.x;
+  const uint64_t G = (n + BN_TILE - 1) / BN_TILE;
+  const long long LO = (1ll << 52), HI = (1ll << 53);
+  double s = 0.0;
+  for (uint64_t cb = 0; cb < G; cb += SP_BATCH) {
+    uint64_t ce = min(G, cb + SP_BATCH);
+    for (uint64_t c = cb + tid; c < ce; c += BN_THREADS) rb[c - cb] = rec[c];
+    __syncthreads();
+    uint64_t c = cb;
+    while (c < ce) {
+      if (tid == 0) {
+        double t = s;
+        uint64_t q = c;
+        for (; q < ce; q++) {
+          const SpecRec r = rb[q - cb];
+          if (r.flag || !(fabs(t) >= 2.2250738585072014e-308) || ilogb(t) != r.e) break;
+          long long S0 = (long long)ldexp(t, 52 - r.e);
+          bool ok = S0 > 0 ? (S0 + r.mn > LO && S0 + r.mx < HI)
+                           : (S0 + r.mx < -LO && S0 + r.mn > -HI);
+          if (!ok) break;
+          t = ldexp((double)(S0 + r.M), r.e - 52);
+        }
+        s_sh = t;
+        cnext = q;
+      }
+      __syncthreads();
+      s = s_sh;
+      c = cnext;
+      __syncthreads();
+      if (c < ce) {                         // speculation failed: add this chunk exactly
+        uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
+        s = binade_range<MODE>(a, b, lo, hi, s, tile, sh, &s_sh, &viol_sh);
+        c++;
+      }
+    }
+    __syncthreads();
+  }
   if (tid == 0) *out = s;
+}
+#define SP_MIN_N (16ull * BN_TILE)
+template <int MODE>
+static void dot_exact_launch(const double *a, const double *b, uint64_t n, double *out) {
+  hipStream_t st = amgd_s();
+  if (n < SP_MIN_N) {
+    k_dot_binade<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, out);
+    return;
+  }
+  uint64_t G = (n + BN_TILE - 1) / BN_TILE;
+  double *csum = (double *)amgd_alloc(G * 8 + 8);
+  SpecRec *rec = (SpecRec *)amgd_alloc(G * sizeof(SpecRec) + 64);
+  int g = (int)std::min<uint64_t>(G, 8192);
+  k_dot_csum<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum);
+  k_dot_approx_prefix<<<1, 1024, 0, st>>>(csum, G);
+  k_dot_spec<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum, rec);
+  k_dot_resolve<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, rec, out);
+  amgd_free(csum);
+  amgd_free(rec);
 }
 
 static int g_exact = -1;
@@ -562,9 +757,9 @@ extern "C" double amgd_dot(const double *a, const double *b, uint64_t n) {
       if (b) k_dot_seq<0><<<1, 256, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
       else k_dot_seq<1><<<1, 256, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
     } else if (b) {
-      k_dot_binade<0><<<1, BN_THREADS, 0, amgd_s()>>>(a, b, n, red_buf() + 2 * RED_BLOCKS);
+      dot_exact_launch<0>(a, b, n, red_buf() + 2 * RED_BLOCKS);
     } else {
-      k_dot_binade<1><<<1, BN_THREADS, 0, amgd_s()>>>(a, a, n, red_buf() + 2 * RED_BLOCKS);
+      dot_exact_launch<1>(a, a, n, red_buf() + 2 * RED_BLOCKS);
     }
     return seq_finish();
   }
@@ -577,7 +772,7 @@ extern "C" double amgd_dot3(const double *M, const double *b, uint64_t n) {
   if (n == 0) return 0.0;
   if (amgd_get_exact()) {
     if (g_seq_plain) k_dot_seq<2><<<1, 256, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
-    else k_dot_binade<2><<<1, BN_THREADS, 0, amgd_s()>>>(M, b, n, red_buf() + 2 * RED_BLOCKS);
+    else dot_exact_launch<2>(M, b, n, red_buf() + 2 * RED_BLOCKS);
     return seq_finish();
   }
   int nb = red_grid(n);

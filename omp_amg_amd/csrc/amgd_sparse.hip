@@ -231,37 +231,38 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
 
 // ---------------------------------------------------------------------------
 // SpMV: t_i = sum_j a_ij x_col(j), left to right from +0.0 (apply_M).
-// CSR-stream: a 256-thread block owns 256 consecutive rows, stages their
-// (col, a) range through LDS with coalesced loads when it fits, then each
-// thread sums its own row in order.  Long-row blocks read rows directly.
+// CSR-stream: a 256-thread block owns 256 consecutive rows and walks their
+// nnz range in LDS-sized chunks: all threads compute the products of a chunk
+// with coalesced loads of (col, a), then each thread adds the part of its own
+// row inside the chunk, in order.  Chunks are visited in order, so every row
+// sum is the reference's left-to-right sum whatever the row lengths.
 // ---------------------------------------------------------------------------
 #define SPMV_ROWS 256
-#define SPMV_LDS 2048
+#define SPMV_CH 4096
 __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t *col,
                                               const double *a, uint32_t rn, const double *x,
                                               double *z, double alpha, const double *y,
                                               double beta, const uint8_t *f) {
-  __shared__ uint32_t sc[SPMV_LDS];
-  __shared__ double sa[SPMV_LDS];
+  __shared__ double pv[SPMV_CH];
+  const int tid = threadIdx.x;
   for (uint64_t r0 = (uint64_t)blockIdx.x * SPMV_ROWS; r0 < rn;
        r0 += (uint64_t)gridDim.x * SPMV_ROWS) {
-    uint64_t r1 = min((uint64_t)rn, r0 + SPMV_ROWS);
-    uint64_t b0 = ro[r0], b1 = ro[r1];
-    uint64_t i = r0 + threadIdx.x;
+    const uint64_t r1 = min((uint64_t)rn, r0 + SPMV_ROWS);
+    const uint64_t b0 = ro[r0], b1 = ro[r1];
+    const uint64_t i = r0 + tid;
+    const bool own = i < r1;
+    const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
     double t = 0;
-    if (b1 - b0 <= SPMV_LDS) {
-      for (uint64_t k = b0 + threadIdx.x; k < b1; k += blockDim.x) {
-        sc[k - b0] = col[k];
-        sa[k - b0] = a[k];
-      }
+    for (uint64_t c0 = b0; c0 < b1; c0 += SPMV_CH) {
+      const uint64_t c1 = min(b1, c0 + SPMV_CH);
+      for (uint64_t k = c0 + tid; k < c1; k += 256) pv[k - c0] = x ? a[k] * x[col[k]] : a[k];
       __syncthreads();
-      if (i < r1)
-        for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += x ? sa[k - b0] * x[sc[k - b0]] : sa[k - b0];
+      const uint64_t lo = max(k0, c0), hi = min(k1, c1);
+#pragma unroll 8
+      for (uint64_t k = lo; k < hi; k++) t += pv[k - c0];
       __syncthreads();
-    } else if (i < r1) {
-      for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += x ? a[k] * x[col[k]] : a[k];
     }
-    if (i < r1) {
+    if (own) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
@@ -503,20 +504,21 @@ extern "C" dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B) {
 //   exact zeros dropped, columns ascending; duplicate columns in a row of A:
 //   the last one wins (the reference scatters A's row into a dense x).
 //
-// Symbolic pass counts distinct columns, numeric pass accumulates.  Rows are
-// binned by their product upper bound:
-//   short rows : one wavefront per row, open-addressing hash in LDS.  Steps
-//                over k are sequential; within a step the 64 lanes take
-//                distinct columns of B's row k, so every slot sees its
-//                additions in ascending k -- bit-exact Gustavson.
-//   long rows  : one 256-thread block per row, dense accumulator in a global
-//                scratch slab (one per resident block), block barrier per k,
-//                emitted in column order by a sweep over the touched range.
+// One row per work-group (a single wavefront, or 256 threads for big rows).
+// The products of a row are enumerated flat: a window of NT consecutive A
+// entries is loaded, their B-row lengths prefix-summed, and every lane takes
+// one product (so a lane never idles on short B rows).  Keys go into an
+// open-addressing hash in LDS; the numeric pass then applies the values layer
+// by layer in ascending k (a B row has distinct columns, so the lanes of one
+// layer never collide) -- every slot sees its additions in the reference's
+// order.  Occupied slots are compacted in place, bitonic-sorted by column
+// and written out.  Rows are binned: symbolic by product upper bound,
+// numeric by the distinct count the symbolic pass found; rows with more than
+// 4096 distinct columns use the dense-slab kernel.
 // ---------------------------------------------------------------------------
-#define HS_SLOTS 2048           // LDS hash slots per wavefront row
-#define SHORT_UB 1024           // products upper bound for the LDS path
 #define EMPTY_KEY 0xffffffffu
 #define LONG_BLOCKS 512         // resident long-row blocks (dense slabs)
+#define OVERFLOW_MARK 0xffffffffffffffffull
 
 __global__ void k_spgemm_ub(const uint64_t *aro, const uint32_t *acol, uint32_t rn,
                             const uint64_t *bro, uint64_t *ub) {
@@ -530,90 +532,204 @@ __global__ void k_spgemm_ub(const uint64_t *aro, const uint32_t *acol, uint32_t 
     ub[i] = s;
   }
 }
-__global__ void k_split_rows(const uint64_t *ub, uint32_t rn, uint32_t *shortl, uint32_t *longl,
-                             unsigned *counts) {
-  // every lane of a wave iterates the same number of times (wave_append needs the whole wave)
+
+// bin rows by v[i] (u64) against ascending thresholds lim[0..nb-2]; the last
+// bin takes the rest.  skip0: rows with v == 0 go nowhere.
+#define SG_MAXBIN 6
+struct SgBins { uint64_t lim[SG_MAXBIN]; };
+__global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int skip0,
+                           uint32_t *lists, unsigned *counts) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (rn + stride - 1) / stride;
-  for (uint64_t it = 0; it < iters; it++) {
+  for (uint64_t it = 0; it < iters; it++) {   // every lane iterates alike (wave_append)
     uint64_t i = i0 + it * stride;
-    bool v = i < rn;
-    bool sh = v && ub[i] <= SHORT_UB;
-    unsigned ps = wave_append(&counts[0], sh);
-    unsigned pl = wave_append(&counts[1], v && !sh);
-    if (sh) shortl[ps] = (uint32_t)i;
-    else if (v) longl[pl] = (uint32_t)i;
+    bool ok = i < rn;
+    uint64_t x = ok ? v[i] : 0;
+    if (skip0 && x == 0) ok = false;
+    int bin = nb - 1;
+    for (int q = nb - 2; q >= 0; q--)
+      if (x <= b.lim[q]) bin = q;
+    for (int q = 0; q < nb; q++) {
+      unsigned p = wave_append(&counts[q], ok && bin == q);
+      if (ok && bin == q) lists[(uint64_t)q * ((uint64_t)rn + 1) + p] = (uint32_t)i;
+    }
   }
 }
 
-__device__ inline uint32_t hslot(uint32_t j) { return (j * 2654435761u) >> (32 - 11); }
+__device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) { return (j * 2654435761u) >> (32 - lg); }
 
-// MODE 0: count distinct; MODE 1: numeric -> write sorted nonzeros at xro[i], count in cnt[i]
-template <int MODE>
-__global__ __launch_bounds__(64) void k_spgemm_short(
-    const uint32_t *rows, uint32_t nrows, const uint64_t *aro, const uint32_t *acol,
-    const double *aa, const uint64_t *bro, const uint32_t *bcol, const double *ba, uint64_t *cnt,
-    const uint64_t *xro, uint32_t *xcol, double *xa) {
-  __shared__ uint32_t hk[HS_SLOTS];
-  __shared__ double hv[HS_SLOTS];
-  __shared__ uint32_t ok[SHORT_UB];
-  __shared__ double ov[SHORT_UB];
-  const int lane = threadIdx.x;
+// inclusive block scan of one u32 per thread (NT = 64 or 256)
+template <int NT>
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t *wtot) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (NT == 64) return v;
+  const int w = threadIdx.x >> 6;
+  if (lane == 63) wtot[w] = v;
+  __syncthreads();
+  uint32_t add = 0;
+  for (int q = 0; q < w; q++) add += wtot[q];
+  __syncthreads();
+  return v + add;
+}
+
+// MODE 0: count distinct columns (cap: overflow -> OVERFLOW_MARK)
+// MODE 1: numeric, write nonzeros sorted at xro[i], count to cnt[i]
+template <int NT, int LG, int MODE>
+__global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nrows,
+                                               const uint64_t *aro, const uint32_t *acol,
+                                               const double *aa, const uint64_t *bro,
+                                               const uint32_t *bcol, const double *ba, uint32_t cap,
+                                               uint64_t *cnt, const uint64_t *xro, uint32_t *xcol,
+                                               double *xa) {
+  constexpr uint32_t S = 1u << LG;
+  __shared__ uint32_t hk[S];
+  __shared__ double hv[MODE ? S : 1];
+  __shared__ uint32_t wend[NT];
+  __shared__ uint64_t wbst[NT];
+  __shared__ double wav[NT];
+  __shared__ uint32_t wtot[NT / 64];
+  __shared__ unsigned nfill;
+  __shared__ int ovf;
+  const int t = threadIdx.x;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    uint32_t i = rows[r];
-    for (int s = lane; s < HS_SLOTS; s += 64) { hk[s] = EMPTY_KEY; hv[s] = 0.0; }
+    const uint32_t i = rows[r];
+    for (uint32_t s = t; s < S; s += NT) {
+      hk[s] = EMPTY_KEY;
+      if (MODE) hv[s] = 0.0;
+    }
+    if (t == 0) { nfill = 0; ovf = 0; }
     __syncthreads();
-    uint64_t a0 = aro[i], a1 = aro[i + 1];
-    for (uint64_t ka = a0; ka < a1; ka++) {
-      uint32_t k = acol[ka];
-      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
-      double av = aa[ka];
-      uint64_t b0 = bro[k], b1 = bro[k + 1];
-      uint64_t nch = (b1 - b0 + 63) / 64;
-      for (uint64_t ch = 0; ch < nch; ch++) {
-        uint64_t kb = b0 + ch * 64 + lane;
-        if (kb < b1) {
+    const uint64_t a0 = aro[i], a1 = aro[i + 1];
+    for (uint64_t wb = a0; wb < a1; wb += NT) {
+      uint64_t ka = wb + t;
+      uint32_t len = 0;
+      uint64_t bs = 0;
+      double av = 0.0;
+      if (ka < a1) {
+        uint32_t k = acol[ka];
+        if (!(ka + 1 < a1 && acol[ka + 1] == k)) {
+          bs = bro[k];
+          len = (uint32_t)(bro[k + 1] - bs);
+          av = aa[ka];
+        }
+      }
+      uint32_t inc = block_incl_scan<NT>(len, wtot);
+      wend[t] = inc;
+      wbst[t] = bs;
+      wav[t] = av;
+      __syncthreads();
+      const uint32_t T = wend[NT - 1];
+      for (uint32_t q0 = 0; q0 < T; q0 += NT) {
+        const uint32_t q = q0 + t;
+        const bool v = q < T;
+        int l = 0;
+        uint32_t sl = 0;
+        double p = 0.0;
+        if (v) {
+          int lo = 0, hi = NT - 1;
+          while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (wend[mid] > q) hi = mid;
+            else lo = mid + 1;
+          }
+          l = lo;
+          uint32_t st = l ? wend[l - 1] : 0u;
+          uint64_t kb = wbst[l] + (q - st);
           uint32_t j = bcol[kb];
-          uint32_t sl = hslot(j);
+          if (MODE) p = ba[kb] * wav[l];
+          sl = sg_hash(j, LG);
           while (true) {
             uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
-            if (old == EMPTY_KEY || old == j) break;
-            sl = (sl + 1) & (HS_SLOTS - 1);
+            if (old == EMPTY_KEY) {
+              if (MODE == 0 && atomicAdd(&nfill, 1u) >= cap) ovf = 1;
+              break;
+            }
+            if (old == j) break;
+            sl = (sl + 1) & (S - 1);
           }
-          if (MODE == 1) hv[sl] = hv[sl] + ba[kb] * av;
         }
-        __syncthreads();   // slot updates of chunk/step t land before step t+1
+        if (MODE == 1) {
+          // layers of this chunk: A-entries [lf, ll] (uniform bounds)
+          uint32_t qa = q0, qb = min(q0 + NT, T) - 1;
+          int lf = 0, ll = 0;
+          {
+            int lo = 0, hi = NT - 1;
+            while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qa) hi = mid; else lo = mid + 1; }
+            lf = lo;
+            lo = lf; hi = NT - 1;
+            while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qb) hi = mid; else lo = mid + 1; }
+            ll = lo;
+          }
+          if (lf == ll) {                  // one B row: distinct columns, no collision
+            if (v) hv[sl] = hv[sl] + p;
+          } else {
+            for (int lay = lf; lay <= ll; lay++) {
+              if (v && l == lay) hv[sl] = hv[sl] + p;
+              __syncthreads();
+            }
+          }
+        }
+        __syncthreads();
+        if (MODE == 0 && ovf) break;
       }
+      __syncthreads();
+      if (MODE == 0 && ovf) break;
     }
-    // gather occupied slots (numeric: nonzero only) into ok/ov, then rank-sort
-    __shared__ unsigned nout;
-    if (lane == 0) nout = 0;
-    __syncthreads();
-    for (int s = lane; s < HS_SLOTS; s += 64) {
-      uint32_t key = hk[s];
-      bool take = key != EMPTY_KEY && (MODE == 0 || hv[s] != 0.0);
-      if (take) {
-        unsigned p = atomicAdd(&nout, 1u);
-        ok[p] = key;
-        if (MODE == 1) ov[p] = hv[s];
-      }
-    }
-    __syncthreads();
-    unsigned n = nout;
     if (MODE == 0) {
-      if (lane == 0) cnt[i] = n;
-    } else {
-      uint64_t base = xro[i];
-      for (unsigned e = lane; e < n; e += 64) {
-        uint32_t key = ok[e];
-        unsigned rank = 0;
-        for (unsigned f = 0; f < n; f++) rank += ok[f] < key;
-        xcol[base + rank] = key;
-        xa[base + rank] = ov[e];
-      }
-      if (lane == 0) cnt[i] = n;
+      if (t == 0) cnt[i] = ovf ? OVERFLOW_MARK : (uint64_t)nfill;
+      __syncthreads();
+      continue;
     }
+    // compact occupied nonzero slots to the front (in place, order kept)
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < S; c0 += NT) {
+      uint32_t s = c0 + t;
+      uint32_t key = hk[s];
+      double val = hv[s];
+      bool take = key != EMPTY_KEY && val != 0.0;
+      uint32_t inc = block_incl_scan<NT>(take ? 1u : 0u, wtot);
+      uint32_t tot = __shfl(inc, 63, 64);
+      if (NT > 64) {
+        if (t == NT - 1) wend[0] = inc;
+        __syncthreads();
+        tot = wend[0];
+      }
+      __syncthreads();
+      if (take) {
+        hk[base + inc - 1] = key;
+        hv[base + inc - 1] = val;
+      }
+      base += tot;
+      __syncthreads();
+    }
+    const uint32_t n = base;
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t s = n + t; s < P; s += NT) hk[s] = EMPTY_KEY;
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1)
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t tt = t; tt < P / 2; tt += NT) {
+          uint32_t lo = 2 * tt - (tt & (stride - 1));
+          uint32_t hi = lo + stride;
+          bool up = (lo & size) == 0;
+          uint32_t kl = hk[lo], kh = hk[hi];
+          if ((kl > kh) == up) {
+            hk[lo] = kh; hk[hi] = kl;
+            double x = hv[lo]; hv[lo] = hv[hi]; hv[hi] = x;
+          }
+        }
+        __syncthreads();
+      }
+    const uint64_t ob = xro[i];
+    for (uint32_t s = t; s < n; s += NT) { xcol[ob + s] = hk[s]; xa[ob + s] = hv[s]; }
+    if (t == 0) cnt[i] = n;
     __syncthreads();
   }
 }
@@ -684,122 +800,6 @@ __global__ __launch_bounds__(256) void k_spgemm_long(
   }
 }
 
-// mid rows (more than SHORT_UB products): one 256-thread block per row, an
-// 8192-slot open-addressing hash in LDS, a block barrier per k step (so every
-// slot sees its additions in ascending k), and a bitonic sort of the (column,
-// value) pairs for the ordered write.  Rows with more than MID_CAP distinct
-// columns overflow to the dense-slab kernel above.
-#define MID_SLOTS 8192
-#define MID_CAP 4096
-#define OVERFLOW_MARK 0xffffffffffffffffull
-__device__ inline uint32_t hslot13(uint32_t j) { return (j * 2654435761u) >> (32 - 13); }
-
-template <int MODE>
-__global__ __launch_bounds__(256) void k_spgemm_mid(const uint32_t *rows, uint32_t nrows,
-                                                    const uint64_t *aro, const uint32_t *acol,
-                                                    const double *aa, const uint64_t *bro,
-                                                    const uint32_t *bcol, const double *ba,
-                                                    uint64_t *cnt, const uint64_t *xro,
-                                                    uint32_t *xcol, double *xa) {
-  __shared__ uint32_t hk[MID_SLOTS];
-  __shared__ double hv[MID_SLOTS];
-  __shared__ uint32_t sk[MODE == 1 ? MID_CAP : 1];
-  __shared__ double sv[MODE == 1 ? MID_CAP : 1];
-  __shared__ unsigned nfill, nout;
-  __shared__ int ovf;
-  const int tid = threadIdx.x;
-  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    uint32_t i = rows[r];
-    for (int q = tid; q < MID_SLOTS; q += 256) { hk[q] = EMPTY_KEY; hv[q] = 0.0; }
-    if (tid == 0) { nfill = 0; nout = 0; ovf = 0; }
-    __syncthreads();
-    uint64_t a0 = aro[i], a1 = aro[i + 1];
-    for (uint64_t ka = a0; ka < a1 && !ovf; ka++) {
-      uint32_t k = acol[ka];
-      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
-      double av = aa[ka];
-      uint64_t b0 = bro[k], b1 = bro[k + 1];
-      for (uint64_t c0 = b0; c0 < b1; c0 += 256) {
-        uint64_t kb = c0 + tid;
-        if (kb < b1 && !ovf) {
-          uint32_t j = bcol[kb];
-          uint32_t sl = hslot13(j);
-          bool ok = true;
-          while (true) {
-            uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
-            if (old == EMPTY_KEY) {
-              if (atomicAdd(&nfill, 1u) >= MID_CAP) { ovf = 1; ok = false; }
-              break;
-            }
-            if (old == j) break;
-            sl = (sl + 1) & (MID_SLOTS - 1);
-          }
-          if (MODE == 1 && ok) hv[sl] = hv[sl] + ba[kb] * av;
-        }
-        __syncthreads();
-      }
-    }
-    __syncthreads();
-    if (ovf) {                    // symbolic only (numeric rows were routed by count)
-      if (tid == 0) cnt[i] = OVERFLOW_MARK;
-      __syncthreads();
-      continue;
-    }
-    if (MODE == 0) {
-      if (tid == 0) cnt[i] = nfill;
-      __syncthreads();
-      continue;
-    }
-    for (int q = tid; q < MID_SLOTS; q += 256) {
-      uint32_t key = hk[q];
-      if (key != EMPTY_KEY && hv[q] != 0.0) {
-        unsigned p = atomicAdd(&nout, 1u);
-        sk[p] = key;
-        sv[p] = hv[q];
-      }
-    }
-    __syncthreads();
-    unsigned n = nout, P = 1;
-    while (P < n) P <<= 1;
-    for (unsigned q = n + tid; q < P; q += 256) { sk[q] = EMPTY_KEY; sv[q] = 0.0; }
-    __syncthreads();
-    for (unsigned size = 2; size <= P; size <<= 1)
-      for (unsigned stride = size >> 1; stride > 0; stride >>= 1) {
-        for (unsigned t = tid; t < P / 2; t += 256) {
-          unsigned lo = 2 * t - (t & (stride - 1));
-          unsigned hi = lo + stride;
-          bool up = ((lo & size) == 0);
-          uint32_t kl = sk[lo], kh = sk[hi];
-          if ((kl > kh) == up) {
-            sk[lo] = kh; sk[hi] = kl;
-            double v = sv[lo]; sv[lo] = sv[hi]; sv[hi] = v;
-          }
-        }
-        __syncthreads();
-      }
-    uint64_t base = xro[i];
-    for (unsigned q = tid; q < n; q += 256) { xcol[base + q] = sk[q]; xa[base + q] = sv[q]; }
-    if (tid == 0) cnt[i] = n;
-    __syncthreads();
-  }
-}
-__global__ void k_route_overflow(const uint32_t *midl, uint32_t nmid, const uint64_t *cnt,
-                                 uint32_t *midok, uint32_t *dense, unsigned *counts) {
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t iters = (nmid + stride - 1) / stride;
-  for (uint64_t it = 0; it < iters; it++) {
-    uint64_t r = r0 + it * stride;
-    bool v = r < nmid;
-    uint32_t i = v ? midl[r] : 0;
-    bool o = v && cnt[i] == OVERFLOW_MARK;
-    unsigned p0 = wave_append(&counts[0], v && !o);
-    unsigned p1 = wave_append(&counts[1], o);
-    if (v && !o) midok[p0] = i;
-    if (o) dense[p1] = i;
-  }
-}
-
 void amgd_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *sa,
                        const uint64_t *dro, uint32_t rn, uint32_t *dcol, double *da);
 
@@ -817,73 +817,79 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     abort();
   }
   hipStream_t s = amgd_s();
-  uint32_t rn = A->rn;
-  uint64_t *ub = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
-  uint32_t *shortl = (uint32_t *)amgd_alloc(((size_t)rn + 1) * 4);
-  uint32_t *longl = (uint32_t *)amgd_alloc(((size_t)rn + 1) * 4);
-  unsigned *counts = (unsigned *)amgd_alloc(8);
-  HIPCK(hipMemsetAsync(counts, 0, 8, s));
+  static int sglog = -1;
+  if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
+  double t_start = 0;
+  if (sglog) { amgd_sync(); t_start = amgd_wtime(); }
+  const uint32_t rn = A->rn;
+  const uint64_t L = (uint64_t)rn + 1;
+  uint64_t *ub = (uint64_t *)amgd_alloc(L * 8);
+  uint32_t *lists = (uint32_t *)amgd_alloc((size_t)SG_MAXBIN * L * 4);
+  unsigned *counts = (unsigned *)amgd_alloc(64);
+  uint64_t *cnt = (uint64_t *)amgd_alloc(L * 8);
+  HIPCK(hipMemsetAsync(counts, 0, 64, s));
+  HIPCK(hipMemsetAsync(cnt, 0, L * 8, s));
+  unsigned hc[SG_MAXBIN] = {0};
   if (rn) {
     k_spgemm_ub<<<grid_for(rn), 256, 0, s>>>(A->ro, A->col, rn, B->ro, ub);
-    k_split_rows<<<grid_for(rn), 256, 0, s>>>(ub, rn, shortl, longl, counts);
+    SgBins b;
+    b.lim[0] = 2048;
+    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(ub, rn, b, 2, 0, lists, counts);
     KCHECK();
+    amgd_d2h(hc, counts, 8);
   }
-  unsigned hc[2];
-  amgd_d2h(hc, counts, 8);
-  // the row lists come out of atomics in arbitrary order; rows are independent
-  // so order does not affect results
-  uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
-  HIPCK(hipMemsetAsync(cnt, 0, ((size_t)rn + 1) * 8, s));
+  // symbolic: distinct count per row (row order in the lists is arbitrary; rows are independent)
+  if (hc[0])
+    k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
+        lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
+  if (hc[1])
+    k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
+        lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
+        nullptr);
+  KCHECK();
+  // numeric bins by distinct count: wave/512, wave/2048, wave/4096, block/8192 slots, dense slab
+  unsigned hn[SG_MAXBIN] = {0};
+  if (rn) {
+    HIPCK(hipMemsetAsync(counts, 0, 64, s));
+    SgBins b;
+    b.lim[0] = 256; b.lim[1] = 1024; b.lim[2] = 2048; b.lim[3] = 4096;
+    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(cnt, rn, b, 5, 1, lists, counts);
+    KCHECK();
+    amgd_d2h(hn, counts, 20);
+  }
   double *slab_v = nullptr;
   uint32_t *slab_s = nullptr;
-  int gs = (int)std::min<unsigned>(std::max(hc[0], 1u), 65536u);
-  // symbolic: short rows (wave hash), mid rows (block hash, may overflow)
-  if (hc[0])
-    k_spgemm_short<0><<<gs, 64, 0, s>>>(shortl, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a,
-                                        cnt, nullptr, nullptr, nullptr);
-  if (hc[1])
-    k_spgemm_mid<0><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
-        longl, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, cnt, nullptr, nullptr, nullptr);
-  KCHECK();
-  uint32_t *midok = nullptr, *densel = nullptr;
-  unsigned hr[2] = {0, 0};
-  if (hc[1]) {
-    midok = (uint32_t *)amgd_alloc((size_t)hc[1] * 4 + 4);
-    densel = (uint32_t *)amgd_alloc((size_t)hc[1] * 4 + 4);
-    unsigned *rc = (unsigned *)amgd_alloc(8);
-    HIPCK(hipMemsetAsync(rc, 0, 8, s));
-    k_route_overflow<<<grid_for(hc[1]), 256, 0, s>>>(longl, hc[1], cnt, midok, densel, rc);
-    amgd_d2h(hr, rc, 8);
-    amgd_free(rc);
-  }
-  int nlb = (int)std::min<unsigned>(hr[1], LONG_BLOCKS);
-  if (hr[1]) {
+  const uint32_t *densel = lists + 4 * L;
+  int nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
+  if (hn[4]) {                    // recount (rows past the hash capacity carry OVERFLOW_MARK)
     slab_v = (double *)amgd_alloc((size_t)nlb * B->cn * 8 + 8);
     slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
     HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
-    k_spgemm_long<0><<<nlb, 256, 0, s>>>(densel, hr[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
+    k_spgemm_long<0><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col, B->a,
                                           B->cn, slab_v, slab_s, cnt, nullptr, nullptr, nullptr);
     KCHECK();
   }
   uint64_t dist = amgd_scan_u64(cnt, rn);   // cnt := offsets of the distinct layout
   uint32_t *tcol = (uint32_t *)amgd_alloc(dist * 4 + 4);
   double *ta = (double *)amgd_alloc(dist * 8 + 8);
-  uint64_t *cnt2 = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
-  HIPCK(hipMemsetAsync(cnt2, 0, ((size_t)rn + 1) * 8, s));
-  if (hr[1]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
+  uint64_t *cnt2 = (uint64_t *)amgd_alloc(L * 8);
+  HIPCK(hipMemsetAsync(cnt2, 0, L * 8, s));
+  if (hn[4]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
   if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
-  if (hc[0])
-    k_spgemm_short<1><<<gs, 64, 0, s>>>(shortl, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a,
-                                        cnt2, cnt, tcol, ta);
-  if (hr[0])
-    k_spgemm_mid<1><<<(int)std::min<unsigned>(hr[0], 16384u), 256, 0, s>>>(
-        midok, hr[0], A->ro, A->col, A->a, B->ro, B->col, B->a, cnt2, cnt, tcol, ta);
-  if (hr[1])
-    k_spgemm_long<1><<<nlb, 256, 0, s>>>(densel, hr[1], A->ro, A->col, A->a, B->ro, B->col, B->a,
+#define SG_NUM(NT, LG, bin, gmax)                                                               \
+  if (hn[bin])                                                                                  \
+    k_sg_row<NT, LG, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
+        lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta);
+  SG_NUM(64, 9, 0, 65536u)
+  SG_NUM(64, 11, 1, 65536u)
+  SG_NUM(64, 12, 2, 65536u)
+  SG_NUM(256, 13, 3, 8192u)
+#undef SG_NUM
+  if (hn[4])
+    k_spgemm_long<1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col, B->a,
                                           B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
-  if (midok) { amgd_free(midok); amgd_free(densel); }
   uint64_t nz = amgd_scan_u64(cnt2, rn);
   if (g_sg_slot >= 0)
     g_sg_bytes += 12 * (A->nnz + B->nnz + nz) + 8 * ((uint64_t)A->rn + B->rn + rn + 3);
@@ -899,8 +905,14 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     amgd_compact_rows(cnt, tcol, ta, cnt2, rn, X->col, X->a);
     amgd_free(cnt); amgd_free(tcol); amgd_free(ta);
   }
-  amgd_free(ub); amgd_free(shortl); amgd_free(longl); amgd_free(counts);
+  amgd_free(ub); amgd_free(lists); amgd_free(counts);
   if (slab_v) { amgd_free(slab_v); amgd_free(slab_s); }
+  if (sglog) {
+    amgd_sync();
+    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
+            rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz, hc[0],
+            hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], (amgd_wtime() - t_start) * 1e3);
+  }
   return X;
 }
 

@@ -42,6 +42,15 @@ API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, doub
     case 2: X = amgd_mpm(alpha, A, beta, B); break;
     case 3: X = amgd_mxmpoint(A, B); break;
     case 4: X = amgd_min_skel(A); break;
+    case 5: {                     /* Q factors of the supports (rows of A) on B; X.a = packed Q */
+      uint64_t tot = 0, *qoff = NULL;
+      double *Q = amgd_qfactor(A, B, &qoff, &tot);
+      X = (dcsr *)malloc(sizeof(dcsr));
+      X->rn = A->rn; X->cn = 0; X->nnz = tot; X->ro = qoff; X->a = Q;
+      X->col = (uint32_t *)amgd_alloc(tot * 4 + 4);
+      amgd_memset(X->col, 0, tot * 4 + 4);
+      break;
+    }
     default: return -2;
   }
   down(X, HX);

@@ -656,6 +656,20 @@ static void build_Q(double *Q, const u32 *Qj, u32 nz, const ocsr *At, double *sq
     qk[k] = -alpha;
   }
 }
+/* kernel-level checker (tests/test_gpu_kernels.py): Q factors of every row of
+ * Wt (supports) against At, packed one after another in row order */
+API void oracle_qfactor(u32 wrn, const u64 *wro, const u32 *wcol, u32 arn, const u64 *aro,
+                        const u32 *acol, const double *aa, double *Q) {
+  ocsr At = {arn, arn, (u64 *)aro, (u32 *)acol, (double *)aa};
+  u64 off = 0;
+  for (u32 c = 0; c < wrn; c++) {
+    u32 nz = (u32)(wro[c + 1] - wro[c]);
+    double *s1 = NEW(double, nz + 1), *s2 = NEW(double, nz + 1);
+    build_Q(Q + off, wcol + wro[c], nz, &At, s1, s2);
+    free(s1); free(s2);
+    off += (u64)nz * (nz + 1) / 2;
+  }
+}
 static u32 max_row(const ocsr *A) {
   u32 mx = 0;
   for (u32 i = 0; i < A->rn; i++) { u64 l = A->ro[i + 1] - A->ro[i]; if (l > mx) mx = (u32)l; }

@@ -1,6 +1,8 @@
 """Kernel-level parity of the HIP primitives against host restatements of the
 reference operations (tests/refops.py), bit for bit, through the library's
 test hooks (amgd_testapi.c)."""
+import zlib
+
 import numpy as np
 import pytest
 
@@ -124,11 +126,13 @@ def _seq(p):
     return s
 
 
-@pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel"])
+@pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel",
+                                  "hover", "big"])
 def test_exact_dot_matches_sequential(kind):
-    """The binade-parallel exact sum equals the left-to-right loop bit for bit."""
-    rng = np.random.default_rng(hash(kind) % 2**32)
-    n = 300000
+    """The binade-parallel exact sum (single block below 64K products, chunk
+    speculation over all CUs above) equals the left-to-right loop bit for bit."""
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))
+    n = 3000000 if kind == "big" else 300000
     if kind == "normal":
         a, b = rng.standard_normal(n), rng.standard_normal(n)
     elif kind == "positive":
@@ -139,6 +143,10 @@ def test_exact_dot_matches_sequential(kind):
         a = np.ones(n); a[0] = 2.0 ** 53; b = np.ones(n)
     elif kind == "zeros":
         a = rng.standard_normal(n); a[: n // 2] = 0.0; a[n // 2 + 5: n // 2 + 9000] = 0.0; b = rng.standard_normal(n)
+    elif kind == "hover":     # running sum crosses the binade boundary at 1.0 again and again
+        a = rng.choice([-1.0, 1.0], n) * 2.0 ** -30; a[0] = 1.0; b = np.ones(n)
+    elif kind == "big":       # more chunks than one record batch
+        a, b = rng.standard_normal(n) + 0.01, rng.standard_normal(n) + 0.02
     elif kind == "range":
         a = rng.standard_normal(n) * 10.0 ** rng.integers(-40, 40, n); b = rng.standard_normal(n)
     else:
@@ -154,3 +162,80 @@ def test_exact_dot_matches_sequential(kind):
         plain = oa.test_dot(mode, a, b, plain=True)
         assert np.float64(got).view(np.uint64) == np.float64(ref).view(np.uint64), (mode, got, ref)
         assert np.float64(plain).view(np.uint64) == np.float64(ref).view(np.uint64), (mode, plain, ref)
+
+
+def _dup_cols(A, rng, frac=0.1):
+    """duplicate some entries of A's rows (the reference's mxm: the last one wins)"""
+    ro, cols, vals = [0], [], []
+    for i in range(A.rn):
+        for k in range(A.row_off[i], A.row_off[i + 1]):
+            cols.append(A.col[k]); vals.append(A.a[k])
+            if rng.random() < frac:
+                cols.append(A.col[k]); vals.append(rng.standard_normal())
+        ro.append(len(cols))
+    return refops.Csr(A.rn, A.cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+
+
+@pytest.mark.parametrize("case", ["short_b_rows", "block_bin", "sym_overflow", "dups"])
+def test_spgemm_row_bins(case):
+    """every row bin of the SpGEMM: wave hashes of 512/2048/4096 slots, the
+    256-thread 8192-slot hash, symbolic overflow to the dense slab, long A rows
+    over short B rows (many k layers per chunk), duplicate A columns"""
+    rng = np.random.default_rng({"short_b_rows": 11, "block_bin": 12, "sym_overflow": 13,
+                                 "dups": 14}[case])
+    if case == "short_b_rows":        # Af*W shape: long A rows, 1..6 entries per B row
+        A = refops.rand_csr(rng, 120, 3000, 0.3)
+        B = refops.rand_csr(rng, 3000, 5000, 0.0007, minrow=1)
+    elif case == "block_bin":         # 2048 < distinct <= 4096
+        A = refops.rand_csr(rng, 24, 2000, 0.5, ints=True)
+        B = refops.rand_csr(rng, 2000, 3000, 0.013, ints=True)
+    elif case == "sym_overflow":      # > 8192 distinct: symbolic overflow, dense slab
+        A = refops.rand_csr(rng, 6, 1000, 0.4)
+        B = refops.rand_csr(rng, 1000, 20000, 0.02)
+    else:
+        A = _dup_cols(refops.rand_csr(rng, 80, 900, 0.2, ints=True), rng)
+        B = refops.rand_csr(rng, 900, 1200, 0.01, ints=True)
+    assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
+
+
+def _oracle_qfactor(W, A):
+    import ctypes as C
+    import os
+    lib = C.CDLL(os.path.join(os.path.dirname(__file__), "..", "oracle", "build", "liboracle.so"))
+    nzs = np.diff(W.row_off)
+    Q = np.zeros(int((nzs * (nzs + 1) // 2).sum()) + 1)
+    wro = np.ascontiguousarray(W.row_off, dtype=np.uint64)
+    wcol = np.ascontiguousarray(W.col, dtype=np.uint32)
+    aro = np.ascontiguousarray(A.row_off, dtype=np.uint64)
+    acol = np.ascontiguousarray(A.col, dtype=np.uint32)
+    aa = np.ascontiguousarray(A.a, dtype=np.float64)
+    lib.oracle_qfactor(C.c_uint32(W.rn), wro.ctypes.data_as(C.c_void_p), wcol.ctypes.data_as(C.c_void_p),
+                       C.c_uint32(A.rn), aro.ctypes.data_as(C.c_void_p), acol.ctypes.data_as(C.c_void_p),
+                       aa.ctypes.data_as(C.c_void_p), Q.ctypes.data_as(C.c_void_p))
+    return Q[:-1]
+
+
+def test_qfactor_tiers_bitexact():
+    """Q factors for supports in every tier (LDS 64 / LDS 128 / block / cooperative
+    grid) against the oracle's restatement of interp's Q loop, bit for bit"""
+    from omp_amg_amd import problems
+    m = 20
+    Ai, Aj, Av = problems.poisson3d(m, 27)
+    o = np.lexsort((Aj, Ai))
+    aro, acol, aa = problems.coo_to_csr_np(np.asarray(Ai)[o], np.asarray(Aj)[o], np.asarray(Av)[o])
+    A = refops.Csr(m ** 3, m ** 3, aro, acol, aa)
+    rng = np.random.default_rng(21)
+    sizes = [1, 5, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
+    ro, cols = [0], []
+    for nz in sizes:
+        lo = int(rng.integers(0, m ** 3 - 3 * nz))
+        c = np.sort(rng.choice(np.arange(lo, lo + 3 * nz), size=nz, replace=False))
+        cols.extend(c.tolist())
+        ro.append(len(cols))
+    ro.append(len(cols))                      # one empty support
+    W = refops.Csr(len(sizes) + 1, m ** 3, np.array(ro), np.array(cols, dtype=np.int64),
+                   np.ones(len(cols)))
+    X = oa.test_csr_op(5, W, A)
+    ref = _oracle_qfactor(W, A)
+    assert X.nnz == len(ref)
+    assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
