@@ -10,9 +10,11 @@ workload: BASELINE.json configs[1] -- 3D 7-point Poisson 256^3 CSR (16.7M rows,
 value   : whole-job rows/s = (ranks x rows) / max-over-ranks seconds per step.
           Round 1 runs one independent replica per GPU (DESIGN.md "Multi-GPU:
           replicas only"), so scaling is "weak".
-roofline: the Galerkin RAP SpGEMM kernels (A_{l+1} = W'AfP + A_cf W + A_cc and
-          AfP = Af W), event-timed live on the library stream; algorithmic bytes
-          = 12 B per nnz of each operand and result + 8 B per row.
+roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
+          and AfP = Af W; instantiated with RAP=1 so rocprof lists them apart),
+          event-timed live on the library stream; algorithmic bytes = 12 B per
+          nnz of each operand and result + 8 B per row (DESIGN.md);
+          tools/rap_from_prof.py sums the same kernels from a rocprofv3 summary.
 cpu_baseline: the reference's own serial setup (oracle/_ref/libref_amg.so,
           compiled from /root/reference sources) on a bounded sample, rank 0 only.
 
@@ -42,36 +44,84 @@ def parse():
     p.add_argument("--fast-dots", action="store_true",
                    help="tree-ordered global dots instead of reference order (not parity-certified)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-m", type=int, default=24, help="reference CPU sample grid edge")
+    p.add_argument("--cpu-m", type=int, default=20,
+                   help="reference CPU sample grid edge (20: a size the reference terminates on)")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--cpu-child", nargs=2, type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic", type=float, default=None,
                    help="RAP HBM bytes per launch from a rocprofv3 PMC pass (profiles/)")
     return p.parse_args()
 
 
-def cpu_baseline(m):
-    """Reference serial setup (compiled from /root/reference by oracle/Makefile)
-    on a bounded sample; falls back to our CPU restatement if _ref is absent."""
+def cpu_child(m, reps):
+    """(child process) time the reference serial setup; prints one JSON line"""
     from omp_amg_amd import abi, problems
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_amg.so")
     kind = "reference"
     if not os.path.exists(ref):
         ref = os.path.join(ROOT, "oracle", "build", "liboracle.so")
         kind = "port"
-    if not os.path.exists(ref):
-        return None
     lib = abi.bind_setup(ctypes.CDLL(ref))
     Ai, Aj, Av = problems.poisson3d(m, 7)
     t0 = time.perf_counter()
-    h = abi.run_setup(lib, Ai, Aj, Av)
+    for _ in range(reps):
+        h = abi.run_setup(lib, Ai, Aj, Av)
     dt = time.perf_counter() - t0
-    rows = m ** 3
-    return {"value": rows / dt, "unit": "rows/s", "cores": 1, "kind": kind,
-            "sample": f"3D 7-point Poisson {m}^3 ({rows} rows, {h.nlevels} levels), "
-                      f"full serial amg_setup, {dt:.2f} s on one host core"}
+    print(json.dumps({"kind": kind, "secs": dt, "rows": m ** 3, "reps": reps, "levels": h.nlevels}))
+
+
+def cpu_baseline(m, reps):
+    """The reference's own serial setup (oracle/_ref/libref_amg.so, compiled from
+    /root/reference by oracle/Makefile) on a bounded sample, in a child process:
+    the reference crashes or never terminates on many inputs (DESIGN.md
+    "Reference UB"), so it must not be able to take the bench down with it.
+    Falls back to the oracle (kind "port") where _ref is absent."""
+    import subprocess
+    if not (os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_amg.so"))
+            or os.path.exists(os.path.join(ROOT, "oracle", "build", "liboracle.so"))):
+        return None
+    secs, done, fails, d = 0.0, 0, 0, None
+    for _ in range(3 * reps):          # each rep in its own process: the reference's heap
+        if done == reps:               # overruns make it crash now and then on 7-point grids
+            break
+        try:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", str(m), "1"],
+                               capture_output=True, text=True, timeout=240)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            secs += d["secs"]
+            done += 1
+        except Exception:  # noqa: BLE001 -- crash / timeout of the reference
+            fails += 1
+    if done == 0:
+        return {"value": None, "unit": "rows/s", "cores": 1, "kind": "reference",
+                "sample": f"reference serial setup on 3D 7-point Poisson {m}^3 crashed {fails}x"}
+    d["reps"], d["secs"] = done, secs
+    return {"value": d["rows"] * d["reps"] / d["secs"], "unit": "rows/s", "cores": 1, "kind": d["kind"],
+            "sample": f"3D 7-point Poisson {m}^3 ({d['rows']} rows, {d['levels']} levels) x{d['reps']}, "
+                      f"full serial amg_setup, {d['secs']:.2f} s on one host core ({fails} crashed runs discarded; the reference's mxm is "
+                      f"O(rows^2) and it does not terminate on many larger grids, so 256^3 is out of its reach)"}
+
+
+def heartbeat(period=30.0):
+    """progress line on stderr while a long setup runs (keeps batch runners from
+    taking a silent multi-minute setup for a hang)"""
+    import threading
+    t0 = time.time()
+    stop = threading.Event()
+
+    def run():
+        while not stop.wait(period):
+            print(f"[bench] {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+    return stop
 
 
 def main():
     args = parse()
+    if args.cpu_child:
+        cpu_child(*args.cpu_child)
+        return
+    hb = heartbeat()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -143,14 +193,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": args.traffic,
-                         "kernel": "k_spgemm_short<1>/k_spgemm_long<1> (RAP + AfP products)",
+                         "kernel": "k_sg_row<NT,LG,1,1> + k_spgemm_long<1,1>: numeric passes of the RAP "
+                                   "SpGEMMs (Af*W, W'*AfP, Acf*W) of every level, HIP-event timed",
                          "algorithmic_bytes_per_setup": rap_bytes / args.steps,
                          "kernel_ms_per_setup": rap_ms / args.steps},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_m)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps)
         print(json.dumps(out), flush=True)
     ds.close()
+    oa.lib().amgd_shutdown()
+    hb.set()
     if dist is not None:
         dist.destroy_process_group()
 

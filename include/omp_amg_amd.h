@@ -34,6 +34,9 @@ typedef struct {
 } amgd_stats;
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */
+/* release every device buffer, event and the stream of the library (hierarchies
+   not yet freed become invalid); amgd_init may be called again afterwards */
+void amgd_shutdown(void);
 /* Global dot products (PCG, Lanczos): 1 = summed in the reference's left-to-right
    order (default; hierarchy bit-identical to the reference), 0 = fixed-order tree
    (faster; differs in the last bits, which the reference's chaotic constraint

@@ -872,3 +872,27 @@ extern "C" double amgd_fro_minus_eye(const dcsr *A) {
   k_fro_rows<<<nb, RED_THREADS, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, red_buf());
   return sum_finish(nb);
 }
+
+// release every device resource of the library (pool, scratch, events, stream);
+// any device pointer handed out before is invalid afterwards
+extern "C" void amgd_rt_shutdown(void) {
+  if (!g_inited) return;
+  HIPCK(hipStreamSynchronize(g_stream));
+  for (auto &b : g_free) (void)hipFree(b.p);
+  for (auto &b : g_used) (void)hipFree(b.p);
+  g_free.clear();
+  g_used.clear();
+  g_inuse = 0;
+  if (g_red) { (void)hipFree(g_red); g_red = nullptr; }
+  if (g_red_h) { (void)hipHostFree(g_red_h); g_red_h = nullptr; }
+  if (g_tinit) {
+    for (int i = 0; i < NTIMERS; i++) {
+      for (auto &pr : g_pend[i]) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+      g_pend[i].clear();
+    }
+    g_tinit = false;
+  }
+  (void)hipStreamDestroy(g_stream);
+  g_stream = nullptr;
+  g_inited = false;
+}

@@ -572,6 +572,7 @@ static void add_time(double *acc, double *t0) {
 }
 
 API int amgd_init(int device) { return amgd_rt_init(device); }
+API void amgd_shutdown(void) { amgd_rt_shutdown(); }
 API void amgd_set_exact_dots(int on) { amgd_set_exact(on); }
 API const char *amgd_error(void) { return amgd_last_error(); }
 API void amgd_get_stats(amgd_stats *st) { *st = g_st; }

@@ -6,7 +6,9 @@
 
 Bar (DESIGN.md "Parity"): level sizes, C/F masks, idc/idf and every CSR
 pattern identical; W/AfP/Af/A values within 1e-12 relative to each matrix's
-largest entry; Chebyshev D / rho within 1e-9 (Lanczos dots are tree-ordered).
+largest entry (north_star); Chebyshev D / rho within 1e-9.  With the default
+reference-order dots the hierarchy is in fact bit-identical, which
+test_gpu_bitexact_vs_reference_fixture holds it to.
 """
 import os
 
@@ -27,6 +29,16 @@ def test_gpu_matches_reference_fixture(case):
     ref = parity.from_npz(z)
     h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
     bad = parity.compare(ref, h, exact=False, rtol=RTOL)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_gpu_bitexact_vs_reference_fixture(case):
+    """every double of the hierarchy equal to the reference's, bit for bit"""
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    bad = parity.compare(ref, h, exact=True)
     assert not bad, bad
 
 

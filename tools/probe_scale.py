@@ -8,6 +8,17 @@ sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(_
 import omp_amg_amd as oa
 from omp_amg_amd import problems
 
+import threading
+_t0 = time.time()
+
+
+def _beat():
+    while True:
+        time.sleep(30)
+        print(f"[probe] {time.time() - _t0:.0f} s", file=sys.stderr, flush=True)
+
+
+threading.Thread(target=_beat, daemon=True).start()
 modes = [True]
 if "--fast-only" in sys.argv:
     modes = [False]
@@ -25,3 +36,4 @@ for m in sizes:
         keep = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()}
         print(json.dumps({"m": m, "rows": m ** 3, "exact": exact, "gen_s": round(gen, 1), **keep}), flush=True)
     ds.close()
+oa.lib().amgd_shutdown()

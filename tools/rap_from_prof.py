@@ -1,0 +1,17 @@
+"""Sum the RAP SpGEMM numeric kernels (template RAP=1 instantiations) in a
+rocprofv3 --stats kernel_stats.csv, to cross-check bench.py's event-timed
+roofline.kernel_ms_per_setup.  Usage: python tools/rap_from_prof.py <kernel_stats.csv> [setups]"""
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+setups = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+pat = re.compile(r"k_sg_row<\d+, \d+, 1, 1>|k_spgemm_long<1, 1>")
+tot, calls = 0.0, 0
+for r in rows:
+    if pat.search(r["Name"]):
+        tot += float(r["TotalDurationNs"])
+        calls += int(r["Calls"])
+        print(f"{float(r['TotalDurationNs']) / 1e6:10.2f} ms {int(r['Calls']):6d} calls  {r['Name'][:70]}")
+print(f"RAP numeric SpGEMM kernels: {tot / 1e6 / setups:.2f} ms per setup over {calls // setups} launches")
