@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
         L.amgd_test_free.argtypes = [C.POINTER(HCsr)]
         L.amgd_test_dot.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.amgd_test_dot.restype = C.c_double
+        L.amgd_test_lmop_mode.argtypes = [C.c_int]
+        L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         _lib = L
     return _lib
 
@@ -227,3 +229,15 @@ def test_dot(mode: int, a, b=None, plain: bool = False, exact: bool = True) -> f
     a = np.ascontiguousarray(a, dtype=np.float64)
     b = np.ascontiguousarray(a if b is None else b, dtype=np.float64)
     return lib().amgd_test_dot(mode, len(a), a.ctypes.data, b.ctypes.data, int(plain), int(exact))
+
+
+def lmop_mode(mode: int) -> None:
+    """interp_lmop path: 0 = row-pull where order-exact (default), 1 = general key/sort walk"""
+    lib().amgd_test_lmop_mode(int(mode))
+
+
+def lmop_stats(reset: bool = True) -> dict:
+    """interp_lmop path counters since the last reset"""
+    out = (C.c_uint64 * 4)()
+    lib().amgd_test_lmop_stats(out, int(reset))
+    return {"fast": out[0], "general": out[1], "dirty_prefix": out[2], "misses": out[3]}

@@ -123,6 +123,9 @@ void amgd_coarsen_mask1(const double *w, double ctol2, const double *g, uint8_t 
                         double *x, uint32_t n);
 void amgd_mat_max(const dcsr *S, const dcsr *St, const uint8_t *f, const double *x, double tol,
                   double *amax_tmp, double *y);
+void amgd_mat_amax(const dcsr *S, const uint8_t *f, double tol, double *amax);
+void amgd_mat_max_gather(const dcsr *St, const uint8_t *f, const double *x, const double *amax,
+                         double *y);
 void amgd_coarsen_mask2(double *g, const double *m, uint8_t *mask, double *x, uint32_t n);
 void amgd_coarsen_mask3(const double *m, uint8_t *mask, uint8_t *vc, uint8_t *vf, double *vfd,
                         uint32_t n, uint32_t *anyvc);
@@ -133,7 +136,13 @@ dcsr *amgd_min_skel(const dcsr *R);
 double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out, uint64_t *qtotal);
 void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
                  const double *u, const double *lambda, double *out);
-void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff, const double *u);
+/* S := interp_lmop contributions (S pattern = W_skel*W_skel'); kpos from amgd_lmop_kpos */
+void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt, const double *Q,
+               const uint64_t *qoff, const double *u);
+uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm);
+void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses */
+void amgd_lmop_stats_reset(void);
+void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, const double *rs,
                         const double *w, const double *sumR, double thr,
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);

@@ -30,4 +30,22 @@ __device__ __forceinline__ unsigned wave_append(unsigned *counter, bool pred) {
 #define GRID_STRIDE(i, n) \
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)(n); \
        i += (uint64_t)gridDim.x * blockDim.x)
+// inclusive block scan of one u32 per thread (NT = 64 or 256)
+template <int NT>
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t *wtot) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  if (NT == 64) return v;
+  const int w = threadIdx.x >> 6;
+  if (lane == 63) wtot[w] = v;
+  __syncthreads();
+  uint32_t add = 0;
+  for (int q = 0; q < w; q++) add += wtot[q];
+  __syncthreads();
+  return v + add;
+}
 #endif

@@ -630,15 +630,17 @@ __global__ void k_csq(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
 }
 extern void amgd_row_of_entry_launch(const uint64_t *ro, uint32_t rn, uint32_t *row);
 
-extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff,
-                          const double *u) {
+// General path: adds the contributions of coarse points c in [cb, ce) to S->a
+// (which the caller has zeroed or already holds the contributions of c < cb).
+extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff,
+                                  const double *u, uint32_t cb, uint32_t ce) {
   hipStream_t s = amgd_s();
-  amgd_memset(S->a, 0, S->nnz * 8);
   uint32_t rn = Wt->rn;
-  if (rn == 0 || Wt->nnz == 0) return;
+  if (ce > rn) ce = rn;
+  if (cb >= ce || Wt->nnz == 0) return;
   uint64_t *coff = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
   k_csq<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, coff);
-  uint64_t total = amgd_scan_u64(coff, rn);
+  amgd_scan_u64(coff, rn);
   std::vector<uint64_t> hcoff(rn + 1), hro(rn + 1);
   amgd_d2h(hcoff.data(), coff, (rn + 1) * 8);
   amgd_d2h(hro.data(), Wt->ro, (rn + 1) * 8);
@@ -653,7 +655,7 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64
     k_blockmax<<<grid_for(n64), 256, 0, s>>>(rmax, srn, 6, b64, n64);
     k_blockmax<<<grid_for(n4k), 256, 0, s>>>(rmax, srn, 12, b4k, n4k);
   }
-  const uint64_t CH = std::min<uint64_t>(total, 1ull << 26);   // contributions per chunk
+  const uint64_t CH = std::max<uint64_t>(1, std::min<uint64_t>(hcoff[ce] - hcoff[cb], 1ull << 26));
   uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);
   double *val = (double *)amgd_alloc(CH * 8 + 8), *val2 = (double *)amgd_alloc(CH * 8 + 8);
   size_t tb = 0;
@@ -661,11 +663,11 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wt, const double *Q, const uint64
   while (eb < 64 && (S->nnz >> eb) != 0) eb++;   // keys are 0..S->nnz
   HIPCK(rocprim::radix_sort_pairs(nullptr, tb, key, key2, val, val2, (size_t)CH, 0, eb, s));
   void *tmp = amgd_alloc(tb + 16);
-  uint32_t c0 = 0;
-  while (c0 < rn) {
+  uint32_t c0 = cb;
+  while (c0 < ce) {
     uint32_t c1 = c0;
     // take whole coarse rows while they fit (a single oversized row gets its own chunk)
-    while (c1 < rn && (hcoff[c1 + 1] - hcoff[c0] <= CH || c1 == c0)) c1++;
+    while (c1 < ce && (hcoff[c1 + 1] - hcoff[c0] <= CH || c1 == c0)) c1++;
     uint64_t n = hcoff[c1] - hcoff[c0];
     if (n > CH) {   // one huge support: grow buffers for it
       amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2); amgd_free(tmp);

@@ -64,6 +64,43 @@ static void dump_csr(const char *name, const dcsr *A) {
   snprintf(n2, sizeof n2, "%s_a", name); dump_dev(n2, A->a, A->nnz * 8);
 }
 
+/* phase profile (AMGD_PHASES=1): device-synchronised time per (level, phase),
+   printed at the end of the setup; costs one stream sync per mark */
+enum { PH_COARSEN, PH_SMOOTH, PH_IPRE, PH_QF, PH_W0, PH_SPAT, PH_LMOP, PH_PCG, PH_W, PH_AFW, PH_R,
+       PH_FS, PH_EXP, PH_FINAL, PH_RAP, PH_N };
+static const char *ph_name[PH_N] = {"coarsen", "smoother", "interp0", "qfactor", "W0", "S_pat",
+                                    "lmop", "pcg", "W", "AfW", "R", "find_sup", "expand",
+                                    "final", "rap"};
+#define PH_MAXL 64
+static double g_ph[PH_MAXL][PH_N], g_ph_t;
+static int g_phases = -1;
+static int phases_on(void) {
+  if (g_phases < 0) { const char *e = getenv("AMGD_PHASES"); g_phases = e && *e && *e != '0'; }
+  return g_phases;
+}
+static void ph(int id) {
+  if (!phases_on()) return;
+  amgd_sync();
+  double t = amgd_wtime();
+  if (id >= 0 && g_lvl < PH_MAXL) g_ph[g_lvl][id] += (t - g_ph_t) * 1e3;
+  g_ph_t = t;
+}
+static void ph_report(uint32_t nl) {
+  if (!phases_on()) return;
+  double tot[PH_N] = {0};
+  fprintf(stderr, "phase ms per level:\nlvl");
+  for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9s", ph_name[p]);
+  fprintf(stderr, "\n");
+  for (uint32_t l = 0; l < nl && l < PH_MAXL; l++) {
+    fprintf(stderr, "%3u", l);
+    for (int p = 0; p < PH_N; p++) { fprintf(stderr, " %9.1f", g_ph[l][p]); tot[p] += g_ph[l][p]; }
+    fprintf(stderr, "\n");
+  }
+  fprintf(stderr, "sum");
+  for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9.1f", tot[p]);
+  fprintf(stderr, "\n");
+}
+
 /* ------------------------------------------------------------------------ */
 /* coarsen (amg_setup.c:2737)                                                */
 /* ------------------------------------------------------------------------ */
@@ -114,9 +151,10 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
       break;
     }
     amgd_coarsen_mask1(w, ctol * ctol, g, mask, x, n);
-    amgd_mat_max(S, St, vf, x, 0.1, amax, m);      /* m = mat_max(S,vf,mask.*g)  */
+    amgd_mat_amax(S, vf, 0.1, amax);               /* Amax: same (S, vf) for both calls */
+    amgd_mat_max_gather(St, vf, x, amax, m);       /* m = mat_max(S,vf,mask.*g)  */
     amgd_coarsen_mask2(g, m, mask, x, n);
-    amgd_mat_max(S, St, vf, x, 0.1, amax, m);      /* m = mat_max(S,vf,mask.*id) */
+    amgd_mat_max_gather(St, vf, x, amax, m);       /* m = mat_max(S,vf,mask.*id) */
     amgd_coarsen_mask3(m, mask, vc, vf, vfd, n, anyvc);
   }
   dcsr_free(&S); dcsr_free(&St);
@@ -293,25 +331,37 @@ static uint32_t pcg(double *x, const dcsr *A, double *r, const double *M, double
 /* ------------------------------------------------------------------------ */
 typedef struct {
   dcsr *Wt;          /* W_skel^T: coarse x fine pattern */
+  uint32_t *kpos;    /* per W_skel entry: its position in the support (row of Wt) */
   double *Q;         /* packed Q factors per coarse column */
   uint64_t *qoff;
+  dcsr *S;           /* constraint operator of this skeleton (solve_constraint), kept for
+                        the final solve: same skeleton, alpha and u -> same S */
+  dcsr *W0;          /* W0 of this skeleton (lambda = 0), likewise reused */
 } skel_factor;
 
 static void factor_free(skel_factor *f) {
   dcsr_free(&f->Wt);
+  amgd_free(f->kpos);
   amgd_free(f->Q);
   amgd_free(f->qoff);
+  if (f->S) dcsr_free(&f->S);
+  if (f->W0) dcsr_free(&f->W0);
 }
 
 /* solve_constraint (amg_setup.c:1499) */
-static void solve_constraint(double *lam, const dcsr *W_skel, const skel_factor *fac, const dcsr *W0,
+static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, const dcsr *W0,
                              const double *alpha, const double *u, const double *v, double tol) {
   uint32_t nf = W_skel->rn, nc = W_skel->cn;
   double *au2 = dalloc(nc);
   amgd_vop(au2, u, u, nc, AMGD_V_MUL);
   amgd_vop(au2, au2, alpha, nc, AMGD_V_MUL);
-  dcsr *S = amgd_spgemm(W_skel, fac->Wt);            /* W_skel * W_skel' (mxm iftrsp=1) */
-  amgd_lmop(S, fac->Wt, fac->Q, fac->qoff, au2);
+  if (!fac->S) {
+    fac->S = amgd_spgemm(W_skel, fac->Wt);           /* W_skel * W_skel' (mxm iftrsp=1) */
+    ph(PH_SPAT);
+    amgd_lmop(fac->S, W_skel, fac->kpos, fac->Wt, fac->Q, fac->qoff, au2);
+    ph(PH_LMOP);
+  }
+  dcsr *S = fac->S;
   dump_csr("S", S);
   double *resid = dalloc(nf), *d = dalloc(nf);
   amgd_spmv(W0, u, resid, 1.0, v, -1.0, NULL);        /* resid = v - W0*u */
@@ -322,9 +372,7 @@ static void solve_constraint(double *lam, const dcsr *W_skel, const skel_factor 
   double *q = dalloc(ncond), *xx = dalloc(ncond);
   if (ncond != nf) {                                   /* S = S(i,i); lam(~i) = 0 */
     amgd_vzero_where(lam, dl, nf);
-    dcsr *Ss = amgd_sub_mat(S, dl, dl);
-    dcsr_free(&S);
-    S = Ss;
+    S = amgd_sub_mat(S, dl, dl);
     double *rc = dalloc(nf), *dc = dalloc(nf), *lc = dalloc(nf);
     amgd_vcompact(rc, resid, dl, nf);
     amgd_vcompact(dc, d, dl, nf);
@@ -340,27 +388,33 @@ static void solve_constraint(double *lam, const dcsr *W_skel, const skel_factor 
     pcg(xx, S, q, d, tol, resid);
     amgd_vop(lam, lam, xx, nf, AMGD_V_ADD);
   }
-  dcsr_free(&S);
+  if (S != fac->S) dcsr_free(&S);
   amgd_free(au2); amgd_free(resid); amgd_free(d); amgd_free(dl); amgd_free(q); amgd_free(xx);
+  ph(PH_PCG);
 }
 
 /* solve_weights (amg_setup.c:1437): W0 (lambda = 0), constraint lam, W */
-static void solve_weights(dcsr **W, dcsr **W0, double *lam, const dcsr *W_skel,
-                          const skel_factor *fac, const dcsr *Amt, const double *alpha,
+static void solve_weights(dcsr **W, const dcsr **W0, double *lam, const dcsr *W_skel,
+                          skel_factor *fac, const dcsr *Amt, const double *alpha,
                           const double *u, const double *v, double tol) {
   uint32_t nf = W_skel->rn, nc = W_skel->cn;
   double *au = dalloc(nc), *zeros = dzeros(nf);
   amgd_vop(au, alpha, u, nc, AMGD_V_MUL);
-  dcsr *W0t = dcsr_empty_like_pattern(fac->Wt);
-  amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, zeros, W0t->a);
-  *W0 = amgd_transpose(W0t, NULL);
-  dcsr_free(&W0t);
+  if (!fac->W0) {
+    dcsr *W0t = dcsr_empty_like_pattern(fac->Wt);
+    amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, zeros, W0t->a);
+    fac->W0 = amgd_transpose(W0t, NULL);
+    dcsr_free(&W0t);
+    ph(PH_W0);
+  }
+  *W0 = fac->W0;
   solve_constraint(lam, W_skel, fac, *W0, alpha, u, v, tol);
   dcsr *Wt = dcsr_empty_like_pattern(fac->Wt);
   amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, lam, Wt->a);
   *W = amgd_transpose(Wt, NULL);
   dcsr_free(&Wt);
   amgd_free(au); amgd_free(zeros);
+  ph(PH_W);
 }
 
 
@@ -409,6 +463,7 @@ static dcsr *find_support(const dcsr *R, double goal) {
 /* expand_support (amg_setup.c:907) */
 static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, double gamma) {
   dcsr *M = find_support(R, gamma);
+  ph(PH_FS);
   dcsr *ns = amgd_mpm(1., M, 1., W_skel);
   dcsr_free(&M);
   uint32_t nbad = 0;
@@ -416,6 +471,7 @@ static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, d
   if (nbad == 0) {
     amgd_skel_binarize(ns, 0);
     amgd_free(bad);
+    ph(PH_EXP);
     return ns;
   }
   dcsr *R0W = amgd_mxmpoint(R0, W_skel);
@@ -429,6 +485,7 @@ static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, d
   amgd_skel_binarize(out, 1);
   dcsr_free(&N); dcsr_free(&ns); dcsr_free(&Xf);
   amgd_free(ones); amgd_free(pi); amgd_free(pj); amgd_free(bad);
+  ph(PH_EXP);
   return out;
 }
 
@@ -471,12 +528,19 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
   dcsr *W = NULL;
   uint64_t prev_nnz = (uint64_t)-1;
   int it = 0;
+  ph(PH_IPRE);
   for (;;) {
     it++;
     skel_factor fac;
-    fac.Wt = amgd_transpose(W_skel, NULL);
+    memset(&fac, 0, sizeof fac);
+    uint64_t *wperm = NULL;
+    fac.Wt = amgd_transpose(W_skel, &wperm);
+    fac.kpos = amgd_lmop_kpos(fac.Wt, wperm);
+    amgd_free(wperm);
     fac.Q = amgd_qfactor(fac.Wt, Af, &fac.qoff, NULL);
-    dcsr *Wtmp, *W0;
+    ph(PH_QF);
+    dcsr *Wtmp;
+    const dcsr *W0;
     g_it = it;
     dump_csr("Wskel", W_skel);
     dump_dev("alpha", alpha, (size_t)cnc * 8);
@@ -491,6 +555,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     AfW = amgd_spgemm(Af, Wtmp);
     dcsr *Arhat = amgd_mpm(1., AfW, 1., Ar);
     dcsr_free(&AfW);
+    ph(PH_AFW);
     dcsr *Arr = amgd_mpm(1.0, Arhat, 1.0, Ar);
     dcsr *ArW = amgd_mxmpoint(Wtmp, Arr);
     dcsr_free(&Arr);
@@ -518,14 +583,16 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     int stalled = prev_nnz == W_skel->nnz;   /* reference would loop forever */
     if (stalled) g_ub++;
     prev_nnz = W_skel->nnz;
+    ph(PH_R);
     if (n == 0 || w1m <= gamma2 || stalled) {
-      dcsr_free(&W0);
+      /* same skeleton, alpha and u: the factor's S and W0 are reused */
       solve_weights(&W, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
       double *wuc = dalloc(rnf);
       amgd_spmv(W, uc, wuc, 0., NULL, 1., NULL);
       amgd_scale_diag_match(W, v, wuc);
       amgd_free(wuc);
-      dcsr_free(&Wtmp); dcsr_free(&W0); dcsr_free(&Arhat0); dcsr_free(&Arhat);
+      ph(PH_FINAL);
+      dcsr_free(&Wtmp); dcsr_free(&Arhat0); dcsr_free(&Arhat);
       dcsr_free(&R0); dcsr_free(&R);
       factor_free(&fac);
       break;
@@ -534,7 +601,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     dcsr *nsk = expand_support(W_skel, R, R0, gamma2);
     dcsr_free(&W_skel);
     W_skel = nsk;
-    dcsr_free(&Wtmp); dcsr_free(&W0); dcsr_free(&Arhat0); dcsr_free(&Arhat);
+    dcsr_free(&Wtmp); dcsr_free(&Arhat0); dcsr_free(&Arhat);
     dcsr_free(&R0); dcsr_free(&R);
     factor_free(&fac);
   }
@@ -623,6 +690,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     uint32_t rn = A->rn, cn = A->cn;
     g_lvl = (int)level;
     L->A = A;
+    ph(-1);
     if (verbose()) printf("Level %u, dim(A) = %u, nnz(A)/dim(A) = %f\n", level + 1, cn,
                           cn ? (double)A->nnz / cn : 0.0);
     if (cn <= 1) {
@@ -636,6 +704,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     coarsen(A, vc, ctol);
     amgd_u8_not(vc, vf, rn);
     L->vc = vc;
+    ph(PH_COARSEN);
     add_time(&g_st.t_coarsen_ms, &t0);
     /* --- smoother --- */
     dcsr *Af = amgd_sub_mat(A, vf, vf);
@@ -667,6 +736,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     }
     L->D = D;
     L->Af = Af;
+    ph(PH_SMOOTH);
     add_time(&g_st.t_smoother_ms, &t0);
     /* --- interpolation --- */
     dcsr *Afc = amgd_sub_mat(A, vf, vc), *Ac = amgd_sub_mat(A, vc, vc);
@@ -694,10 +764,13 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     dcsr_free(&Wt); dcsr_free(&WtAfP); dcsr_free(&Acf); dcsr_free(&AcfW); dcsr_free(&Atmp);
     dcsr_free(&Afc); dcsr_free(&Ac);
     amgd_free(vf);
+    ph(PH_RAP);
     add_time(&g_st.t_rap_ms, &t0);
     level++;
   }
   h->nlevels = level + 1;
+  ph_report(h->nlevels);
+  if (phases_on()) memset(g_ph, 0, sizeof g_ph);
   amgd_sync();
   g_st.t_total_ms = (amgd_wtime() - t_start) * 1e3;
   g_st.rap_kernel_ms = amgd_timer_ms(0);

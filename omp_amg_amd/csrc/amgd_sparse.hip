@@ -559,25 +559,6 @@ __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int
 
 __device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) { return (j * 2654435761u) >> (32 - lg); }
 
-// inclusive block scan of one u32 per thread (NT = 64 or 256)
-template <int NT>
-__device__ __forceinline__ uint32_t block_incl_scan(uint32_t v, uint32_t *wtot) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
-  }
-  if (NT == 64) return v;
-  const int w = threadIdx.x >> 6;
-  if (lane == 63) wtot[w] = v;
-  __syncthreads();
-  uint32_t add = 0;
-  for (int q = 0; q < w; q++) add += wtot[q];
-  __syncthreads();
-  return v + add;
-}
-
 // MODE 0: count distinct columns (cap: overflow -> OVERFLOW_MARK)
 // MODE 1: numeric, write nonzeros sorted at xro[i], count to cnt[i]
 // RAP 1: the same kernel instantiated separately for the Galerkin products, so

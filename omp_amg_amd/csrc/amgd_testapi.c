@@ -121,3 +121,10 @@ API void amgd_test_free(hcsr *H) {
   free(H->ro); free(H->col); free(H->a);
   H->ro = NULL; H->col = NULL; H->a = NULL;
 }
+
+/* interp_lmop path control and counters: [fast, general, dirty-prefix, misses] */
+API void amgd_test_lmop_mode(int m) { amgd_lmop_set_mode(m); }
+API void amgd_test_lmop_stats(uint64_t *out, int reset) {
+  amgd_lmop_stats(out);
+  if (reset) amgd_lmop_stats_reset();
+}

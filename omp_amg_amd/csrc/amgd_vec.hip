@@ -147,77 +147,90 @@ extern "C" void amgd_coarsen_mask1(const double *w, double ctol2, const double *
                                    double *x, uint32_t n) {
   if (n) k_mask1<<<grid_for(n), 256, 0, amgd_s()>>>(w, ctol2, g, mask, x, n);
 }
-// mat_max (amg_setup.c:3535) as an ordered gather over S^T:
-//   Amax_i = tol * max_{j in row i, f[col]!=0} |a_ij| (from 0, strict >)
+// mat_max (amg_setup.c:3535) as a gather over S^T, split in two launches:
+//   Amax_i = tol * max_{j in row i, f[col]!=0} |a_ij|        (amgd_mat_amax)
 //   y_k = max over rows i of column k with f[k]!=0 && |a_ik| >= Amax_i of x_i
-__global__ void k_amax(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
-                       const uint8_t *f, double tol, double *amax) {
-  GRID_STRIDE(i, rn) {
+//                                                             (amgd_mat_max_gather)
+// Both are max-reductions (order-free, exact), so G lanes share a row: G is the
+// power of two nearest the mean row length (4..64), each group reduces with
+// xor-shuffles inside the wavefront.  Amax depends only on (S, f), so the
+// coarsening sweep computes it once for both of its mat_max calls.
+template <int G>
+__global__ __launch_bounds__(256) void k_amax_g(const uint64_t *ro, const uint32_t *col,
+                                                const double *a, uint32_t rn, const uint8_t *f,
+                                                double tol, double *amax) {
+  const uint32_t sub = threadIdx.x & (G - 1);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
+  for (uint64_t i = g0; i < rn; i += gs) {
     double m = 0;
-    for (uint64_t k = ro[i]; k < ro[i + 1]; k++)
-      if (f[col[k]] != 0 && fabs(a[k]) > m) m = fabs(a[k]);
-    amax[i] = m * tol;
+    for (uint64_t k = ro[i] + sub; k < ro[i + 1]; k += G) {
+      double v = fabs(a[k]);
+      if (f[col[k]] != 0 && v > m) m = v;
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) { double u = __shfl_xor(m, o, 64); m = u > m ? u : m; }
+    if (sub == 0) amax[i] = m * tol;
   }
 }
-__global__ void k_matmax_gather(const uint64_t *tro, const uint32_t *tcol, const double *ta,
-                                uint32_t n, const uint8_t *f, const double *x, const double *amax,
-                                double *y) {
-  GRID_STRIDE(k, n) {
+template <int G>
+__global__ __launch_bounds__(256) void k_matmax_gather_g(const uint64_t *tro, const uint32_t *tcol,
+                                                         const double *ta, uint32_t n,
+                                                         const uint8_t *f, const double *x,
+                                                         const double *amax, double *y) {
+  const uint32_t sub = threadIdx.x & (G - 1);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
+  for (uint64_t k = g0; k < n; k += gs) {
     double m = -DBL_MAX;
     if (f[k] != 0)
-      for (uint64_t t = tro[k]; t < tro[k + 1]; t++) {
+      for (uint64_t t = tro[k] + sub; t < tro[k + 1]; t += G) {
         uint32_t i = tcol[t];
         if (fabs(ta[t]) < amax[i]) continue;
         double xi = x[i];
         if (xi > m) m = xi;
       }
-    y[k] = m;
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) { double u = __shfl_xor(m, o, 64); m = u > m ? u : m; }
+    if (sub == 0) y[k] = m;
   }
 }
-__global__ __launch_bounds__(256) void k_amax_wave(const uint64_t *ro, const uint32_t *col,
-                                                   const double *a, uint32_t rn, const uint8_t *f,
-                                                   double tol, double *amax) {
-  const int lane = threadIdx.x & 63;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < rn; i += (uint64_t)gridDim.x * 4) {
-    double m = 0;
-    for (uint64_t k = ro[i] + lane; k < ro[i + 1]; k += 64)
-      if (f[col[k]] != 0 && fabs(a[k]) > m) m = fabs(a[k]);
-    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_down(m, o, 64); m = u > m ? u : m; }
-    if (lane == 0) amax[i] = m * tol;
-  }
+static int lanes_for(uint64_t nnz, uint64_t rn) {
+  uint64_t avg = rn ? (nnz + rn - 1) / rn : 1;
+  int G = 4;
+  while (G < 64 && (uint64_t)G * 2 <= avg) G <<= 1;
+  return G;
 }
-__global__ __launch_bounds__(256) void k_matmax_gather_wave(const uint64_t *tro, const uint32_t *tcol,
-                                                            const double *ta, uint32_t n,
-                                                            const uint8_t *f, const double *x,
-                                                            const double *amax, double *y) {
-  const int lane = threadIdx.x & 63;
-  for (uint64_t k = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += (uint64_t)gridDim.x * 4) {
-    double m = -DBL_MAX;
-    if (f[k] != 0)
-      for (uint64_t t = tro[k] + lane; t < tro[k + 1]; t += 64) {
-        uint32_t i = tcol[t];
-        if (fabs(ta[t]) < amax[i]) continue;
-        double xi = x[i];
-        if (xi > m) m = xi;
-      }
-    for (int o = 32; o > 0; o >>= 1) { double u = __shfl_down(m, o, 64); m = u > m ? u : m; }
-    if (lane == 0) y[k] = m;
+#define MM_LAUNCH(KER, G, n, ...)                                                              \
+  do {                                                                                         \
+    int gb_ = grid_for((uint64_t)(n) * (G), 256, 65536);                                       \
+    KER<G><<<gb_, 256, 0, amgd_s()>>>(__VA_ARGS__);                                            \
+  } while (0)
+#define MM_DISPATCH(KER, G, n, ...)                                                            \
+  switch (G) {                                                                                 \
+    case 4: MM_LAUNCH(KER, 4, n, __VA_ARGS__); break;                                          \
+    case 8: MM_LAUNCH(KER, 8, n, __VA_ARGS__); break;                                          \
+    case 16: MM_LAUNCH(KER, 16, n, __VA_ARGS__); break;                                        \
+    case 32: MM_LAUNCH(KER, 32, n, __VA_ARGS__); break;                                        \
+    default: MM_LAUNCH(KER, 64, n, __VA_ARGS__); break;                                        \
   }
+extern "C" void amgd_mat_amax(const dcsr *S, const uint8_t *f, double tol, double *amax) {
+  if (!S->rn) return;
+  int G = lanes_for(S->nnz, S->rn);
+  MM_DISPATCH(k_amax_g, G, S->rn, S->ro, S->col, S->a, S->rn, f, tol, amax);
+  KCHECK();
+}
+extern "C" void amgd_mat_max_gather(const dcsr *St, const uint8_t *f, const double *x,
+                                    const double *amax, double *y) {
+  if (!St->rn) return;
+  int G = lanes_for(St->nnz, St->rn);
+  MM_DISPATCH(k_matmax_gather_g, G, St->rn, St->ro, St->col, St->a, St->rn, f, x, amax, y);
+  KCHECK();
 }
 extern "C" void amgd_mat_max(const dcsr *S, const dcsr *St, const uint8_t *f, const double *x,
                              double tol, double *amax, double *y) {
-  if (!S->rn) return;
-  if (S->nnz >= 24ull * S->rn) {   // long rows: one wavefront per row (max is order-free)
-    int g = (int)std::min<uint64_t>((S->rn + 3) / 4, 65536);
-    k_amax_wave<<<g, 256, 0, amgd_s()>>>(S->ro, S->col, S->a, S->rn, f, tol, amax);
-    k_matmax_gather_wave<<<g, 256, 0, amgd_s()>>>(St->ro, St->col, St->a, St->rn, f, x, amax, y);
-    KCHECK();
-    return;
-  }
-  k_amax<<<grid_for(S->rn), 256, 0, amgd_s()>>>(S->ro, S->col, S->a, S->rn, f, tol, amax);
-  k_matmax_gather<<<grid_for(St->rn), 256, 0, amgd_s()>>>(St->ro, St->col, St->a, St->rn, f, x,
-                                                           amax, y);
-  KCHECK();
+  amgd_mat_amax(S, f, tol, amax);
+  amgd_mat_max_gather(St, f, x, amax, y);
 }
 // g = g - m; mask = mask & (g >= 0); g = id; x = mask .* id
 __global__ void k_mask2(double *g, const double *m, uint8_t *mask, double *x, uint32_t n) {

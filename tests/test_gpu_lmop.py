@@ -1,0 +1,42 @@
+"""interp_lmop (amg_setup.c:1589): the row-pull path (omp_amg_amd/csrc/amgd_lmop.hip)
+against the general key/sort walk, bit for bit, on whole setups.
+
+The fixtures (test_gpu_parity.py) already pin the default path to the reference;
+here the two device paths are run on the same inputs and every double of the two
+hierarchies must agree, and the counters must show the fast path was taken."""
+import numpy as np
+import pytest
+
+import omp_amg_amd as oa
+from omp_amg_amd import abi, parity, problems
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(Ai, Aj, Av, mode):
+    oa.lmop_mode(mode)
+    oa.lmop_stats(reset=True)
+    try:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.lmop_mode(0)
+    return h, oa.lmop_stats(reset=True)
+
+
+@pytest.mark.parametrize("gen", [
+    ("p7_16", lambda: problems.poisson3d(16)),
+    ("p7_20x12x9", lambda: problems.poisson3d(9, mx=20, my=12)),
+    ("aniso_14", lambda: problems.poisson3d(14, eps=1e-3)),
+    ("p27_10", lambda: problems.poisson3d(10, 27)),
+    ("p2d9_40", lambda: problems.poisson2d(40, 9)),
+    ("sem_e3_N3", lambda: problems.sem_laplacian(3, 3, 3, 3, seed=5, jitter=0.3)),
+], ids=lambda g: g[0])
+def test_lmop_fast_equals_general(gen):
+    Ai, Aj, Av = gen[1]()
+    hg, sg = _run(Ai, Aj, Av, 1)
+    hf, sf = _run(Ai, Aj, Av, 0)
+    assert sg["fast"] == 0 and sg["general"] > 0
+    assert sf["fast"] > 0, sf
+    assert sf["misses"] == 0, sf
+    bad = parity.compare(hg, hf, exact=True)
+    assert not bad, bad
