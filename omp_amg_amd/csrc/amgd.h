@@ -77,7 +77,8 @@ dcsr *amgd_build_csr(uint64_t nz, const uint32_t *Ai, const uint32_t *Aj, const 
 dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V,
                    uint32_t rn, uint32_t cn, int drop_zero);
 dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *vc);
-dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out);  /* perm: CSC idx -> CSR idx */
+dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out);
+dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask);  /* rows with mask==0 emptied */  /* perm: CSC idx -> CSR idx */
 dcsr *amgd_spgemm(const dcsr *A, const dcsr *B);           /* A*B, reference semantics */
 dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *B);
 dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B);
@@ -143,8 +144,10 @@ uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm);
 void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses */
 void amgd_lmop_stats_reset(void);
 void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
-uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, const double *rs,
-                        const double *w, const double *sumR, double thr,
+/* one find_support sweep: select/remove, then re-sum rs (rows) and sumR (columns) that lost
+   an entry */
+uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
+                        const double *w, double *sumR, double thr,
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
 uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad);
 uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_t **pi, uint32_t **pj);

@@ -721,16 +721,30 @@ extern "C" void amgd_csc_gemv(const dcsr *Rt, const uint64_t *perm, const double
 }
 // Per bad column c (w_c > (1+theta)*goal && sumR_c != 0): first row of the max of
 // R(i,c)*rs_i (amg_setup.c:1343-1364), removed from R (both CSR and CSC copies).
+// The bad columns are listed first (one thread per column), then one wavefront
+// per listed column does the (value, position) max, first position on ties.
+__global__ void k_fs_badlist(const double *w, const double *sumR, double thr, uint32_t n,
+                             uint32_t *list, unsigned *cnt) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t iters = (n + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {      // uniform trip count (wave_append)
+    uint64_t c = i0 + it * stride;
+    bool take = c < n && w[c] > thr && sumR[c] != 0.;
+    unsigned p = wave_append(cnt, take);
+    if (take) list[p] = (uint32_t)c;
+  }
+}
 __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const uint32_t *trow,
                                                    const uint64_t *perm, double *ta, double *a,
-                                                   const double *rs, const double *w,
-                                                   const double *sumR, double thr, uint32_t n,
-                                                   uint32_t *si, uint32_t *sj, unsigned *cnt) {
-  // one wavefront per column; (value, position) max with the first position on ties
+                                                   const double *rs, const uint32_t *list,
+                                                   const unsigned *nlist, uint32_t *si,
+                                                   uint32_t *sj, unsigned *cnt) {
   const int lane = threadIdx.x & 63;
-  for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n;
-       c += (uint64_t)gridDim.x * 4) {
-    if (!(w[c] > thr && sumR[c] != 0.)) continue;
+  const uint32_t n = *nlist;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n;
+       r += (uint64_t)gridDim.x * 4) {
+    const uint32_t c = list[r];
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
     for (uint64_t q = tro[c] + lane; q < tro[c + 1]; q += 64) {
@@ -745,23 +759,63 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     if (lane == 0) {
       unsigned p = atomicAdd(&cnt[0], 1u);
       si[p] = best != ~0ull ? trow[best] : 0u;
-      sj[p] = (uint32_t)c;
+      sj[p] = c;
       if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
     }
   }
 }
+// ordered row sums (from +0, left to right) of the listed rows: re-sums a row of R
+// after an entry of it was removed (the removed entry is an exact zero now)
+__global__ __launch_bounds__(256) void k_list_rowsum(const uint64_t *ro, const double *a,
+                                                     const uint32_t *list, uint32_t n, double *out) {
+  __shared__ double buf[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
+    const uint32_t i = list[r];
+    const uint64_t k0 = ro[i], k1 = ro[i + 1];
+    double t = 0;
+    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
+      if (c0 + lane < k1) buf[w][lane] = a[c0 + lane];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane == 0) {
+        const int m = (int)min((uint64_t)64, k1 - c0);
+        for (int q = 0; q < m; q++) t += buf[w][q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) out[i] = t;
+  }
+}
+// One selection sweep: select + remove, then bring rs (row sums of R) and sumR
+// (column sums) up to date for the rows / columns that lost an entry.
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
-                                   const double *rs, const double *w, const double *sumR,
+                                   double *rs, const double *w, double *sumR,
                                    double thr, uint32_t *sel_i, uint32_t *sel_j,
                                    uint32_t *nremoved) {
-  unsigned *cnt = (unsigned *)amgd_alloc(8);
-  amgd_memset(cnt, 0, 8);
-  if (Rt->rn)
-    k_fs_select<<<(int)std::min<uint64_t>((Rt->rn + 3) / 4, 65536), 256, 0, amgd_s()>>>(
-        Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, w, sumR, thr, Rt->rn, sel_i, sel_j, cnt);
+  hipStream_t s = amgd_s();
+  const uint32_t nc = Rt->rn;
+  uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
+  unsigned *cnt = (unsigned *)amgd_alloc(16);
+  amgd_memset(cnt, 0, 16);
+  if (nc) {
+    k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
+    k_fs_select<<<(int)std::min<uint64_t>((nc + 3) / 4, 16384), 256, 0, s>>>(
+        Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, cnt + 2, sel_i, sel_j, cnt);
+  }
   KCHECK();
   unsigned h[2];
   amgd_d2h(h, cnt, 8);
+  if (h[1]) {
+    const int g = (int)std::min<uint64_t>(((uint64_t)h[0] + 3) / 4, 16384);
+    k_list_rowsum<<<g, 256, 0, s>>>(Rl->ro, Rl->a, sel_i, h[0], rs);
+    k_list_rowsum<<<g, 256, 0, s>>>(Rt->ro, Rt->a, sel_j, h[0], sumR);
+    KCHECK();
+  }
+  amgd_free(list);
   amgd_free(cnt);
   *nremoved = h[1];
   return h[0];

@@ -431,9 +431,12 @@ static dcsr *find_support(const dcsr *R, double goal) {
   uint32_t *si = (uint32_t *)amgd_alloc(cap * 4), *sj = (uint32_t *)amgd_alloc(cap * 4);
   double theta = 0.5;
   int it = 0;
+  /* rs = R*1 and sumR = sum(R,1) change only where a sweep removed an entry:
+     computed in full once, then re-summed for those rows / columns (amgd_fs_select) */
+  amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);            /* rs = R*1 */
+  amgd_colsum(Rt, sumR);
   for (;;) {
     it++;
-    amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);          /* rs = R*1 */
     amgd_spmvt(Rt, rs, w);                                /* w = R'*rs (row order) */
     amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w2);                              /* w2 = R'*(R*w) */
@@ -443,7 +446,6 @@ static dcsr *find_support(const dcsr *R, double goal) {
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
-    amgd_colsum(Rt, sumR);
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     ns += nsel;
@@ -460,8 +462,28 @@ static dcsr *find_support(const dcsr *R, double goal) {
   return Sk;
 }
 
+/* R0 = |Dfsqrti*(Af*W0 + Ar)|*Dcs (amg_setup.c:870-895), needed only on the bad rows of
+   expand_support: the product is formed for those rows alone (rows are independent, so
+   they carry exactly the reference's values; the others are never read) */
+typedef struct {
+  const dcsr *Af, *W0, *Ar;
+  const double *Dfsqrti, *Dcs;
+} r0_ctx;
+static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr);
+static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
+  dcsr *Afb = amgd_rows_masked(c->Af, bad);
+  dcsr *AfW0 = amgd_spgemm(Afb, c->W0);
+  dcsr_free(&Afb);
+  dcsr *Arb = amgd_rows_masked(c->Ar, bad);
+  dcsr *Arhat0 = amgd_mpm(1., AfW0, 1., Arb);
+  dcsr_free(&AfW0); dcsr_free(&Arb);
+  dcsr *R0 = scale_abs_scale(Arhat0, c->Dfsqrti, c->Dcs);
+  dcsr_free(&Arhat0);
+  return R0;
+}
+
 /* expand_support (amg_setup.c:907) */
-static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, double gamma) {
+static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const r0_ctx *r0c, double gamma) {
   dcsr *M = find_support(R, gamma);
   ph(PH_FS);
   dcsr *ns = amgd_mpm(1., M, 1., W_skel);
@@ -474,9 +496,10 @@ static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const dcsr *R0, d
     ph(PH_EXP);
     return ns;
   }
+  dcsr *R0 = r0_rows(r0c, bad);
   dcsr *R0W = amgd_mxmpoint(R0, W_skel);
   dcsr *Xf = amgd_mpm(1., R0, -1., R0W);
-  dcsr_free(&R0W);
+  dcsr_free(&R0W); dcsr_free(&R0);
   uint32_t *pi = NULL, *pj = NULL;
   uint64_t np = amgd_expand_pick(Xf, bad, &pi, &pj);
   double *ones = dones(np);
@@ -549,10 +572,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     dump_csr("W0", W0);
     dump_csr("Wtmp", Wtmp);
     dump_dev("lam_out", lam, (size_t)rnf * 8);
-    dcsr *AfW = amgd_spgemm(Af, W0);
-    dcsr *Arhat0 = amgd_mpm(1., AfW, 1., Ar);
-    dcsr_free(&AfW);
-    AfW = amgd_spgemm(Af, Wtmp);
+    dcsr *AfW = amgd_spgemm(Af, Wtmp);
     dcsr *Arhat = amgd_mpm(1., AfW, 1., Ar);
     dcsr_free(&AfW);
     ph(PH_AFW);
@@ -566,7 +586,6 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     amgd_vunary(Dcs, cnc, AMGD_V_INV);
     amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
     dcsr *R = scale_abs_scale(Arhat, Dfsqrti, Dcs);  /* |Dfsqrti*Arhat|*Dcsqrti */
-    dcsr *R0 = scale_abs_scale(Arhat0, Dfsqrti, Dcs);
     dcsr *Rt = amgd_transpose(R, NULL);
     amgd_spmv(R, onesc, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w1);                         /* w1 = ((R*1)'*R)' */
@@ -592,17 +611,18 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
       amgd_scale_diag_match(W, v, wuc);
       amgd_free(wuc);
       ph(PH_FINAL);
-      dcsr_free(&Wtmp); dcsr_free(&Arhat0); dcsr_free(&Arhat);
-      dcsr_free(&R0); dcsr_free(&R);
+      dcsr_free(&Wtmp); dcsr_free(&Arhat);
+      dcsr_free(&R);
       factor_free(&fac);
       break;
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
-    dcsr *nsk = expand_support(W_skel, R, R0, gamma2);
+    r0_ctx r0c = {Af, W0, Ar, Dfsqrti, Dcs};
+    dcsr *nsk = expand_support(W_skel, R, &r0c, gamma2);
     dcsr_free(&W_skel);
     W_skel = nsk;
-    dcsr_free(&Wtmp); dcsr_free(&Arhat0); dcsr_free(&Arhat);
-    dcsr_free(&R0); dcsr_free(&R);
+    dcsr_free(&Wtmp); dcsr_free(&Arhat);
+    dcsr_free(&R);
     factor_free(&fac);
   }
   dcsr_free(&W_skel); dcsr_free(&Amt);
