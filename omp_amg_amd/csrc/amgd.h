@@ -85,6 +85,8 @@ dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B);
 /* z = (y ? alpha*y + beta*t : beta*t) [* f] with t = M x summed in column order */
 void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                double beta, const uint8_t *f);
+/* z[list[r]] = row list[r] of M times x (x == NULL: row sums), left to right */
+void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x, double *z);
 /* z = M^T x, per column in ascending row order; Mt = transpose(M) */
 void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
 void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */

@@ -295,8 +295,8 @@ __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
 }
 // columns binned by support size nz (empty supports skipped) against lim[0..nb-2]
 __global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, uint32_t l0, uint32_t l1, uint32_t l2,
-                         int nb, uint32_t *lists, unsigned *cnt) {
-  const uint32_t lim[3] = {l0, l1, l2};
+                         uint32_t l3, int nb, uint32_t *lists, unsigned *cnt) {
+  const uint32_t lim[4] = {l0, l1, l2, l3};
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (rn + stride - 1) / stride;
@@ -332,7 +332,7 @@ static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
   if (Wt->rn) {
-    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, 0, 0, 2, rs.sl, cnt);
+    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, 0, 0, 0, 2, rs.sl, cnt);
     k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 4));
   }
   unsigned h[8];
@@ -347,6 +347,7 @@ static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
 }
 static void free_split(RowSplit &rs) { amgd_free(rs.sl); }
 
+#define QF_T0 32
 #define QF_T1 64
 #define QF_T2 128
 #define QF_T3 1024
@@ -363,28 +364,33 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
   uint64_t tot = amgd_scan_u64(qoff, rn);
   double *Q = (double *)amgd_alloc(tot * 8 + 8);
-  uint32_t *lists = (uint32_t *)amgd_alloc(4 * L * 4);
+  uint32_t *lists = (uint32_t *)amgd_alloc(5 * L * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
-  unsigned hn[4] = {0, 0, 0, 0};
+  unsigned hn[5] = {0, 0, 0, 0, 0};
   if (rn) {
-    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, QF_T1, QF_T2, QF_T3, 4, lists, cnt);
+    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, QF_T0, QF_T1, QF_T2, QF_T3, 5, lists, cnt);
     KCHECK();
-    amgd_d2h(hn, cnt, 16);
+    amgd_d2h(hn, cnt, 20);
   }
+  // tiers by support size: the LDS triangle sized to the tier keeps small supports at
+  // high occupancy (nz <= 32: 4 KB per wavefront)
   if (hn[0])
-    k_qfactor_lds<QF_T1><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
+    k_qfactor_lds<QF_T0><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
         lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   if (hn[1])
-    k_qfactor_lds<QF_T2><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
+    k_qfactor_lds<QF_T1><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
         lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   if (hn[2])
-    k_qfactor_mid<<<(int)std::min<unsigned>(hn[2], 8192u), 256, 0, s>>>(
+    k_qfactor_lds<QF_T2><<<(int)std::min<unsigned>(hn[2], 65536u), 64, 0, s>>>(
         lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (hn[3])
+    k_qfactor_mid<<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
+        lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   KCHECK();
-  if (hn[3]) {                    // huge supports, one cooperative launch each
-    std::vector<uint32_t> big(hn[3]);
-    amgd_d2h(big.data(), lists + 3 * L, (size_t)hn[3] * 4);
+  if (hn[4]) {                    // huge supports, one cooperative launch each
+    std::vector<uint32_t> big(hn[4]);
+    amgd_d2h(big.data(), lists + 4 * L, (size_t)hn[4] * 4);
     std::vector<uint64_t> ro(rn + 1);
     amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
     for (uint32_t c : big) {
@@ -416,8 +422,8 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   }
   if (sglog) {
     amgd_sync();
-    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u Q %lu  %.2f ms\n", rn,
-            (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], (unsigned long)tot,
+    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u/%u Q %lu  %.2f ms\n", rn,
+            (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], hn[4], (unsigned long)tot,
             (amgd_wtime() - t_start) * 1e3);
   }
   amgd_free(lists); amgd_free(cnt);
@@ -735,33 +741,46 @@ __global__ void k_fs_badlist(const double *w, const double *sumR, double thr, ui
     if (take) list[p] = (uint32_t)c;
   }
 }
+// G lanes per listed column (G = the power of two nearest the mean column length)
+template <int G>
 __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const uint32_t *trow,
                                                    const uint64_t *perm, double *ta, double *a,
                                                    const double *rs, const uint32_t *list,
                                                    const unsigned *nlist, uint32_t *si,
-                                                   uint32_t *sj, unsigned *cnt) {
-  const int lane = threadIdx.x & 63;
+                                                   uint32_t *sj, unsigned *removed) {
+  const uint32_t sub = threadIdx.x & (G - 1);
   const uint32_t n = *nlist;
-  for (uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n;
-       r += (uint64_t)gridDim.x * 4) {
+  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
+  for (uint64_t r = g0; r < n; r += gs) {
     const uint32_t c = list[r];
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
-    for (uint64_t q = tro[c] + lane; q < tro[c + 1]; q += 64) {
+    for (uint64_t q = tro[c] + sub; q < tro[c + 1]; q += G) {
       double x = ta[q] * rs[trow[q]];
       if (x > mx) { mx = x; best = q; }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      double om = __shfl_down(mx, o, 64);
-      unsigned long long ob = __shfl_down((unsigned long long)best, o, 64);
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+      double om = __shfl_xor(mx, o, 64);
+      unsigned long long ob = __shfl_xor((unsigned long long)best, o, 64);
       if (om > mx || (om == mx && ob < best)) { mx = om; best = ob; }
     }
-    if (lane == 0) {
-      unsigned p = atomicAdd(&cnt[0], 1u);
-      si[p] = best != ~0ull ? trow[best] : 0u;
-      sj[p] = c;
-      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; atomicAdd(&cnt[1], 1u); }
+    if (sub == 0) {              // slot r of the list: no contended counter
+      si[r] = best != ~0ull ? trow[best] : 0u;
+      sj[r] = c;
+      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
     }
+  }
+}
+// short rows: one thread per listed row, in order
+__global__ void k_list_rowsum_t(const uint64_t *ro, const double *a, const uint32_t *list,
+                                uint32_t n, double *out) {
+  GRID_STRIDE(r, n) {
+    const uint32_t i = list[r];
+    double t = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++) t += a[k];
+    out[i] = t;
   }
 }
 // ordered row sums (from +0, left to right) of the listed rows: re-sums a row of R
@@ -803,16 +822,36 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   amgd_memset(cnt, 0, 16);
   if (nc) {
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
-    k_fs_select<<<(int)std::min<uint64_t>((nc + 3) / 4, 16384), 256, 0, s>>>(
-        Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, cnt + 2, sel_i, sel_j, cnt);
+    uint64_t avg = (Rt->nnz + nc - 1) / nc;
+    int G = 4;
+    while (G < 64 && (uint64_t)G * 2 <= avg) G <<= 1;
+    const int gb = grid_for((uint64_t)nc * G, 256, 16384);
+#define FS_SEL(GG)                                                                        \
+    k_fs_select<GG><<<gb, 256, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, cnt + 2, \
+                                       sel_i, sel_j, cnt + 1)
+    switch (G) {
+      case 4: FS_SEL(4); break;
+      case 8: FS_SEL(8); break;
+      case 16: FS_SEL(16); break;
+      case 32: FS_SEL(32); break;
+      default: FS_SEL(64); break;
+    }
+#undef FS_SEL
   }
   KCHECK();
-  unsigned h[2];
-  amgd_d2h(h, cnt, 8);
+  unsigned h[4];
+  amgd_d2h(h, cnt, 12);
+  h[0] = h[2];                    // selections = bad columns (one per column)
   if (h[1]) {
-    const int g = (int)std::min<uint64_t>(((uint64_t)h[0] + 3) / 4, 16384);
-    k_list_rowsum<<<g, 256, 0, s>>>(Rl->ro, Rl->a, sel_i, h[0], rs);
-    k_list_rowsum<<<g, 256, 0, s>>>(Rt->ro, Rt->a, sel_j, h[0], sumR);
+    const dcsr *M[2] = {Rl, Rt};
+    const uint32_t *L[2] = {sel_i, sel_j};
+    double *O[2] = {rs, sumR};
+    for (int q = 0; q < 2; q++) {
+      if (M[q]->nnz <= 32ull * M[q]->rn)
+        k_list_rowsum_t<<<grid_for(h[0]), 256, 0, s>>>(M[q]->ro, M[q]->a, L[q], h[0], O[q]);
+      else
+        amgd_spmv_rows(M[q], L[q], h[0], nullptr, O[q]);
+    }
     KCHECK();
   }
   amgd_free(list);

@@ -67,10 +67,10 @@ static void dump_csr(const char *name, const dcsr *A) {
 /* phase profile (AMGD_PHASES=1): device-synchronised time per (level, phase),
    printed at the end of the setup; costs one stream sync per mark */
 enum { PH_COARSEN, PH_SMOOTH, PH_IPRE, PH_QF, PH_W0, PH_SPAT, PH_LMOP, PH_PCG, PH_W, PH_AFW, PH_R,
-       PH_FS, PH_EXP, PH_FINAL, PH_RAP, PH_N };
+       PH_FS, PH_FS_MV, PH_FS_MAX, PH_FS_SEL, PH_EXP, PH_EXP_R0, PH_FINAL, PH_RAP, PH_N };
 static const char *ph_name[PH_N] = {"coarsen", "smoother", "interp0", "qfactor", "W0", "S_pat",
-                                    "lmop", "pcg", "W", "AfW", "R", "find_sup", "expand",
-                                    "final", "rap"};
+                                    "lmop", "pcg", "W", "AfW", "R", "fs_setup", "fs_spmv",
+                                    "fs_max", "fs_sel", "expand", "exp_R0", "final", "rap"};
 #define PH_MAXL 64
 static double g_ph[PH_MAXL][PH_N], g_ph_t;
 static int g_phases = -1;
@@ -435,13 +435,16 @@ static dcsr *find_support(const dcsr *R, double goal) {
      computed in full once, then re-summed for those rows / columns (amgd_fs_select) */
   amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);            /* rs = R*1 */
   amgd_colsum(Rt, sumR);
+  ph(PH_FS);
   for (;;) {
     it++;
     amgd_spmvt(Rt, rs, w);                                /* w = R'*rs (row order) */
     amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w2);                              /* w2 = R'*(R*w) */
+    ph(PH_FS_MV);
     amgd_vdiv_guard(vv, w2, w, nc);
     double mv = amgd_max_first(vv, nc, NULL), mw = mv;   /* max(v) twice, amg_setup.c:1316-1317 */
+    ph(PH_FS_MAX);
     if (mv < goal || mw < goal) break;
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
@@ -449,6 +452,7 @@ static dcsr *find_support(const dcsr *R, double goal) {
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     ns += nsel;
+    ph(PH_FS_SEL);
     if (nrem == 0) { g_ub++; break; }                    /* no progress: reference loops */
     if (ns + nc > cap) { g_ub++; break; }
   }
@@ -486,6 +490,8 @@ static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
 static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const r0_ctx *r0c, double gamma) {
   dcsr *M = find_support(R, gamma);
   ph(PH_FS);
+  if (phases_on() && verbose())
+    printf("    find_support: R %u x %u nnz %lu\n", R->rn, R->cn, (unsigned long)R->nnz);
   dcsr *ns = amgd_mpm(1., M, 1., W_skel);
   dcsr_free(&M);
   uint32_t nbad = 0;
@@ -496,7 +502,10 @@ static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const r0_ctx *r0c
     ph(PH_EXP);
     return ns;
   }
+  ph(PH_EXP);
   dcsr *R0 = r0_rows(r0c, bad);
+  ph(PH_EXP_R0);
+  if (verbose()) printf("    expand_support: %u bad rows of %u\n", nbad, W_skel->rn);
   dcsr *R0W = amgd_mxmpoint(R0, W_skel);
   dcsr *Xf = amgd_mpm(1., R0, -1., R0W);
   dcsr_free(&R0W); dcsr_free(&R0);

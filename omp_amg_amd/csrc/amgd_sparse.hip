@@ -332,10 +332,120 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
     }
   }
 }
+// long rows, one row per LANE: each wavefront owns 64 rows and walks them in
+// rounds of 16 entries; a round is loaded cooperatively (each load instruction
+// covers four 16-entry row segments, 128 B each) into an LDS tile, and every lane
+// then adds its own row's 16 products in order.  The sum is the reference's
+// left-to-right sum and all 64 lanes add at once (k_spmv_wave leaves 63 idle).
+// LIST: the rows are list[0..n) instead of 0..n.
+#define SL_SEG 16
+#define SL_MIN_ROWS 65536   // >= 1024 wavefronts of 64 rows: enough to fill 256 CUs
+template <bool LIST>
+__global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, uint32_t n,
+                                                   const uint32_t *list, const double *x,
+                                                   double *z, double alpha, const double *y,
+                                                   double beta, const uint8_t *f) {
+  __shared__ double buf[4][64][SL_SEG + 1];
+  __shared__ uint64_t rk0[4][64];
+  __shared__ uint32_t rlen[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * 64; rb < n;
+       rb += (uint64_t)gridDim.x * 4 * 64) {
+    const uint64_t r = rb + lane;
+    const bool own = r < n;
+    const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
+    const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    const uint32_t len = (uint32_t)(k1 - k0);
+    rk0[w][lane] = k0;
+    rlen[w][lane] = len;
+    uint32_t mx = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double t = 0;
+    const uint32_t sub = lane & (SL_SEG - 1), grp = lane >> 4;
+    for (uint32_t off = 0; off < mx; off += SL_SEG) {
+#pragma unroll 4
+      for (int q = 0; q < 16; q++) {
+        const int rr = q * 4 + grp;
+        const uint32_t e = off + sub;
+        double v = 0.0;
+        if (e < rlen[w][rr]) {
+          const uint64_t k = rk0[w][rr] + e;
+          v = x ? a[k] * x[col[k]] : a[k];
+        }
+        buf[w][rr][sub] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (off < len) {
+        const uint32_t m = min((uint32_t)SL_SEG, len - off);
+        for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (own) {
+      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) v = v * (f[i] ? 1.0 : 0.0);
+      z[i] = v;
+    }
+  }
+}
+// ordered sums (x == nullptr) or products of the listed rows only
+__global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, const uint32_t *col,
+                                                        const double *a, const uint32_t *list,
+                                                        uint32_t n, const double *x, double *z) {
+  __shared__ double buf[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
+    const uint32_t i = list[r];
+    const uint64_t k0 = ro[i], k1 = ro[i + 1];
+    double t = 0;
+    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
+      const uint64_t k = c0 + lane;
+      if (k < k1) buf[w][lane] = x ? a[k] * x[col[k]] : a[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane == 0) {
+        const int m = (int)min((uint64_t)64, k1 - c0);
+        for (int q = 0; q < m; q++) t += buf[w][q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) z[i] = t;
+  }
+}
+extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x,
+                               double *z) {
+  if (!n) return;
+  if (n < SL_MIN_ROWS) {          // too few rows to fill the chip one row per lane
+    int g = (int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536);
+    k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
+    KCHECK();
+    return;
+  }
+  int g = (int)std::min<uint64_t>(((uint64_t)n + 255) / 256, 16384);
+  k_spmv_lane<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n, list, x, z, 0.0, nullptr,
+                                             1.0, nullptr);
+  KCHECK();
+}
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
   if (M->rn == 0) return;
-  if (M->nnz >= 32ull * M->rn) {
+  if (M->nnz >= 32ull * M->rn && M->rn >= SL_MIN_ROWS) {
+    int g = (int)std::min<uint64_t>(((uint64_t)M->rn + 255) / 256, 16384);
+    k_spmv_lane<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z, alpha,
+                                                y, beta, f);
+  } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
     k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   } else {
@@ -586,6 +696,7 @@ __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int
 
 __device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) { return (j * 2654435761u) >> (32 - lg); }
 
+#define SG_U 4   // sub-chunks whose product loads are issued together
 // MODE 0: count distinct columns (cap: overflow -> OVERFLOW_MARK)
 // MODE 1: numeric, write nonzeros sorted at xro[i], count to cnt[i]
 // RAP 1: the same kernel instantiated separately for the Galerkin products, so
@@ -635,57 +746,75 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
       wav[t] = av;
       __syncthreads();
       const uint32_t T = wend[NT - 1];
-      for (uint32_t q0 = 0; q0 < T; q0 += NT) {
-        const uint32_t q = q0 + t;
-        const bool v = q < T;
-        int l = 0;
-        uint32_t sl = 0;
-        double p = 0.0;
-        if (v) {
-          int lo = 0, hi = NT - 1;
-          while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (wend[mid] > q) hi = mid;
-            else lo = mid + 1;
-          }
-          l = lo;
-          uint32_t st = l ? wend[l - 1] : 0u;
-          uint64_t kb = wbst[l] + (q - st);
-          uint32_t j = bcol[kb];
-          if (MODE) p = ba[kb] * wav[l];
-          sl = sg_hash(j, LG);
-          while (true) {
-            uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
-            if (old == EMPTY_KEY) {
-              if (MODE == 0 && atomicAdd(&nfill, 1u) >= cap) ovf = 1;
-              break;
-            }
-            if (old == j) break;
-            sl = (sl + 1) & (S - 1);
-          }
-        }
-        if (MODE == 1) {
-          // layers of this chunk: A-entries [lf, ll] (uniform bounds)
-          uint32_t qa = q0, qb = min(q0 + NT, T) - 1;
-          int lf = 0, ll = 0;
-          {
+      for (uint32_t q0 = 0; q0 < T; q0 += NT * SG_U) {
+        // fetch the (column, product) of SG_U sub-chunks first: their loads are
+        // independent, so one latency round serves SG_U sub-chunks
+        int lq[SG_U];
+        uint32_t jq[SG_U];
+        double pq[SG_U];
+#pragma unroll
+        for (int u = 0; u < SG_U; u++) {
+          const uint32_t q = q0 + u * NT + t;
+          lq[u] = -1;
+          jq[u] = 0;
+          pq[u] = 0.0;
+          if (q < T) {
             int lo = 0, hi = NT - 1;
-            while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qa) hi = mid; else lo = mid + 1; }
-            lf = lo;
-            lo = lf; hi = NT - 1;
-            while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qb) hi = mid; else lo = mid + 1; }
-            ll = lo;
-          }
-          if (lf == ll) {                  // one B row: distinct columns, no collision
-            if (v) hv[sl] = hv[sl] + p;
-          } else {
-            for (int lay = lf; lay <= ll; lay++) {
-              if (v && l == lay) hv[sl] = hv[sl] + p;
-              __syncthreads();
+            while (lo < hi) {
+              int mid = (lo + hi) >> 1;
+              if (wend[mid] > q) hi = mid;
+              else lo = mid + 1;
             }
+            const uint32_t st = lo ? wend[lo - 1] : 0u;
+            const uint64_t kb = wbst[lo] + (q - st);
+            jq[u] = bcol[kb];
+            if (MODE) pq[u] = ba[kb] * wav[lo];
+            lq[u] = lo;
           }
         }
-        __syncthreads();
+        // then insert and add sub-chunk by sub-chunk, in product order
+#pragma unroll
+        for (int u = 0; u < SG_U; u++) {
+          const uint32_t qs = q0 + u * NT;
+          if (qs >= T) break;              // uniform over the block
+          const bool v = lq[u] >= 0;
+          uint32_t sl = 0;
+          if (v) {
+            const uint32_t j = jq[u];
+            sl = sg_hash(j, LG);
+            while (true) {
+              uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
+              if (old == EMPTY_KEY) {
+                if (MODE == 0 && atomicAdd(&nfill, 1u) >= cap) ovf = 1;
+                break;
+              }
+              if (old == j) break;
+              sl = (sl + 1) & (S - 1);
+            }
+          }
+          if (MODE == 1) {
+            // layers of this sub-chunk: A-entries [lf, ll] (uniform bounds)
+            uint32_t qa = qs, qb = min(qs + NT, T) - 1;
+            int lf = 0, ll = 0;
+            {
+              int lo = 0, hi = NT - 1;
+              while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qa) hi = mid; else lo = mid + 1; }
+              lf = lo;
+              lo = lf; hi = NT - 1;
+              while (lo < hi) { int mid = (lo + hi) >> 1; if (wend[mid] > qb) hi = mid; else lo = mid + 1; }
+              ll = lo;
+            }
+            if (lf == ll) {                // one B row: distinct columns, no collision
+              if (v) hv[sl] = hv[sl] + pq[u];
+            } else {
+              for (int lay = lf; lay <= ll; lay++) {
+                if (v && lq[u] == lay) hv[sl] = hv[sl] + pq[u];
+                __syncthreads();
+              }
+            }
+          }
+          __syncthreads();
+        }
         if (MODE == 0 && ovf) break;
       }
       __syncthreads();

@@ -74,6 +74,27 @@ def test_spmv_ordered():
     assert np.array_equal(oa.test_spmv(L, xl), refops.spmv(L, xl))
 
 
+def test_spmv_lane_ragged():
+    """lane-per-row kernel (mean row >= 32): ragged rows, empty rows, rows shorter and
+    longer than its 16-entry rounds, 64-row groups that end mid-wave"""
+    rng = np.random.default_rng(23)
+    rn, cn = 1000 + 37, 3000
+    ro, cols, vals = [0], [], []
+    for i in range(rn):
+        k = int(rng.choice([0, 1, 15, 16, 17, 40, 63, 64, 65, 300, 1200]))
+        c = np.sort(rng.choice(cn, size=k, replace=False))
+        cols.extend(c.tolist())
+        vals.extend((rng.standard_normal(k) * 10.0 ** rng.integers(-8, 8, size=k)).tolist())
+        ro.append(len(cols))
+    L = refops.Csr(rn, cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64),
+                   np.array(vals))
+    assert L.a.size >= 32 * rn
+    x = rng.standard_normal(cn)
+    y = rng.standard_normal(rn)
+    assert np.array_equal(oa.test_spmv(L, x), refops.spmv(L, x))
+    assert np.array_equal(oa.test_spmv(L, x, 1.0, y, -1.0), refops.spmv(L, x, 1.0, y, -1.0))
+
+
 def test_min_skel():
     rng = np.random.default_rng(4)
     R = refops.rand_csr(rng, 300, 100, 0.03)
@@ -216,7 +237,7 @@ def _oracle_qfactor(W, A):
 
 
 def test_qfactor_tiers_bitexact():
-    """Q factors for supports in every tier (LDS 64 / LDS 128 / block / cooperative
+    """Q factors for supports in every tier (LDS 32 / 64 / 128 / block / cooperative
     grid) against the oracle's restatement of interp's Q loop, bit for bit"""
     from omp_amg_amd import problems
     m = 20
@@ -225,7 +246,7 @@ def test_qfactor_tiers_bitexact():
     aro, acol, aa = problems.coo_to_csr_np(np.asarray(Ai)[o], np.asarray(Aj)[o], np.asarray(Av)[o])
     A = refops.Csr(m ** 3, m ** 3, aro, acol, aa)
     rng = np.random.default_rng(21)
-    sizes = [1, 5, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
+    sizes = [1, 5, 31, 32, 33, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
     ro, cols = [0], []
     for nz in sizes:
         lo = int(rng.integers(0, m ** 3 - 3 * nz))
