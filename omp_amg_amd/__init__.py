@@ -86,6 +86,7 @@ def lib() -> C.CDLL:
         L.amgd_test_dot.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.amgd_test_dot.restype = C.c_double
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
+        L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         _lib = L
     return _lib
@@ -241,3 +242,8 @@ def lmop_stats(reset: bool = True) -> dict:
     out = (C.c_uint64 * 4)()
     lib().amgd_test_lmop_stats(out, int(reset))
     return {"fast": out[0], "general": out[1], "dirty_prefix": out[2], "misses": out[3]}
+
+
+def spgemm_flat(on: bool) -> None:
+    """SpGEMM kernels: True = flat enumeration only, False = automatic (k-sequential for long B rows)"""
+    lib().amgd_test_spgemm_flat(int(on))

@@ -101,6 +101,20 @@ static void ph_report(uint32_t nl) {
   fprintf(stderr, "\n");
 }
 
+/* X = A*B, given At = A' and Bt = B'.  When A has long columns (mean row of At
+   >= 64) and B short rows, X' = Bt*At has long B-operand rows and takes the
+   k-sequential SpGEMM kernels; it is the same Gustavson sum (k ascending over the
+   shared index, products commute, same exact-zero drop), transposed back stably.
+   Bit-identical to amgd_spgemm(A, B) either way. */
+static dcsr *spgemm_via_t(const dcsr *A, const dcsr *At, const dcsr *B, const dcsr *Bt) {
+  const uint64_t avg_at = At && At->rn ? At->nnz / At->rn : 0, avg_b = B->rn ? B->nnz / B->rn : 0;
+  if (!At || !Bt || avg_at < 64 || avg_b >= 64) return amgd_spgemm(A, B);
+  dcsr *Xt = amgd_spgemm(Bt, At);
+  dcsr *X = amgd_transpose(Xt, NULL);
+  dcsr_free(&Xt);
+  return X;
+}
+
 /* ------------------------------------------------------------------------ */
 /* coarsen (amg_setup.c:2737)                                                */
 /* ------------------------------------------------------------------------ */
@@ -336,7 +350,7 @@ typedef struct {
   uint64_t *qoff;
   dcsr *S;           /* constraint operator of this skeleton (solve_constraint), kept for
                         the final solve: same skeleton, alpha and u -> same S */
-  dcsr *W0;          /* W0 of this skeleton (lambda = 0), likewise reused */
+  dcsr *W0, *W0t;    /* W0 of this skeleton (lambda = 0) and its transpose, likewise reused */
 } skel_factor;
 
 static void factor_free(skel_factor *f) {
@@ -346,6 +360,7 @@ static void factor_free(skel_factor *f) {
   amgd_free(f->qoff);
   if (f->S) dcsr_free(&f->S);
   if (f->W0) dcsr_free(&f->W0);
+  if (f->W0t) dcsr_free(&f->W0t);
 }
 
 /* solve_constraint (amg_setup.c:1499) */
@@ -394,9 +409,9 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
 }
 
 /* solve_weights (amg_setup.c:1437): W0 (lambda = 0), constraint lam, W */
-static void solve_weights(dcsr **W, const dcsr **W0, double *lam, const dcsr *W_skel,
-                          skel_factor *fac, const dcsr *Amt, const double *alpha,
-                          const double *u, const double *v, double tol) {
+static void solve_weights(dcsr **W, dcsr **Wt_out, const dcsr **W0, double *lam,
+                          const dcsr *W_skel, skel_factor *fac, const dcsr *Amt,
+                          const double *alpha, const double *u, const double *v, double tol) {
   uint32_t nf = W_skel->rn, nc = W_skel->cn;
   double *au = dalloc(nc), *zeros = dzeros(nf);
   amgd_vop(au, alpha, u, nc, AMGD_V_MUL);
@@ -404,7 +419,7 @@ static void solve_weights(dcsr **W, const dcsr **W0, double *lam, const dcsr *W_
     dcsr *W0t = dcsr_empty_like_pattern(fac->Wt);
     amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, zeros, W0t->a);
     fac->W0 = amgd_transpose(W0t, NULL);
-    dcsr_free(&W0t);
+    fac->W0t = W0t;
     ph(PH_W0);
   }
   *W0 = fac->W0;
@@ -412,7 +427,8 @@ static void solve_weights(dcsr **W, const dcsr **W0, double *lam, const dcsr *W_
   dcsr *Wt = dcsr_empty_like_pattern(fac->Wt);
   amgd_qapply(fac->Wt, fac->Q, fac->qoff, Amt, au, lam, Wt->a);
   *W = amgd_transpose(Wt, NULL);
-  dcsr_free(&Wt);
+  if (Wt_out) *Wt_out = Wt;
+  else dcsr_free(&Wt);
   amgd_free(au); amgd_free(zeros);
   ph(PH_W);
 }
@@ -470,14 +486,15 @@ static dcsr *find_support(const dcsr *R, double goal) {
    expand_support: the product is formed for those rows alone (rows are independent, so
    they carry exactly the reference's values; the others are never read) */
 typedef struct {
-  const dcsr *Af, *W0, *Ar;
+  const dcsr *Af, *W0, *W0t, *Ar;
   const double *Dfsqrti, *Dcs;
 } r0_ctx;
 static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr);
 static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
   dcsr *Afb = amgd_rows_masked(c->Af, bad);
-  dcsr *AfW0 = amgd_spgemm(Afb, c->W0);
-  dcsr_free(&Afb);
+  dcsr *AfbT = amgd_transpose(Afb, NULL);
+  dcsr *AfW0 = spgemm_via_t(Afb, AfbT, c->W0, c->W0t);
+  dcsr_free(&Afb); dcsr_free(&AfbT);
   dcsr *Arb = amgd_rows_masked(c->Ar, bad);
   dcsr *Arhat0 = amgd_mpm(1., AfW0, 1., Arb);
   dcsr_free(&AfW0); dcsr_free(&Arb);
@@ -529,7 +546,8 @@ static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr) 
   return R;
 }
 
-static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, double gamma2, double tol) {
+static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, const dcsr *Ar,
+                           double gamma2, double tol) {
   uint32_t rnf = Af->rn, rnc = Ac->rn, cnc = Ac->cn, cnr = Ar->cn;
   double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
   amgd_diag(Af, Df);
@@ -577,13 +595,14 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     dump_csr("Wskel", W_skel);
     dump_dev("alpha", alpha, (size_t)cnc * 8);
     dump_dev("lam_in", lam, (size_t)rnf * 8);
-    solve_weights(&Wtmp, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
+    dcsr *Wtmp_t = NULL;
+    solve_weights(&Wtmp, &Wtmp_t, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
     dump_csr("W0", W0);
     dump_csr("Wtmp", Wtmp);
     dump_dev("lam_out", lam, (size_t)rnf * 8);
-    dcsr *AfW = amgd_spgemm(Af, Wtmp);
+    dcsr *AfW = spgemm_via_t(Af, AfT, Wtmp, Wtmp_t);
     dcsr *Arhat = amgd_mpm(1., AfW, 1., Ar);
-    dcsr_free(&AfW);
+    dcsr_free(&AfW); dcsr_free(&Wtmp_t);
     ph(PH_AFW);
     dcsr *Arr = amgd_mpm(1.0, Arhat, 1.0, Ar);
     dcsr *ArW = amgd_mxmpoint(Wtmp, Arr);
@@ -614,7 +633,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
     ph(PH_R);
     if (n == 0 || w1m <= gamma2 || stalled) {
       /* same skeleton, alpha and u: the factor's S and W0 are reused */
-      solve_weights(&W, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
+      solve_weights(&W, NULL, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
       double *wuc = dalloc(rnf);
       amgd_spmv(W, uc, wuc, 0., NULL, 1., NULL);
       amgd_scale_diag_match(W, v, wuc);
@@ -626,7 +645,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *Ac, const dcsr *Ar, doubl
       break;
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
-    r0_ctx r0c = {Af, W0, Ar, Dfsqrti, Dcs};
+    r0_ctx r0c = {Af, W0, fac.W0t, Ar, Dfsqrti, Dcs};
     dcsr *nsk = expand_support(W_skel, R, &r0c, gamma2);
     dcsr_free(&W_skel);
     W_skel = nsk;
@@ -773,19 +792,22 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     L->idc = (unsigned long *)amgd_alloc((size_t)rnc * 8 + 8);
     L->idf = (unsigned long *)amgd_alloc((size_t)rnf * 8 + 8);
     amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, rn, L->idc, L->idf);
-    dcsr *W = interpolation(Af, Ac, Afc, gamma2, itol);
+    /* Af' for the transposed products (only where Af's rows are long enough to pay) */
+    dcsr *AfT = Af->rn && Af->nnz >= 64ull * Af->rn ? amgd_transpose(Af, NULL) : NULL;
+    dcsr *W = interpolation(Af, AfT, Ac, Afc, gamma2, itol);
     L->W = W;
     add_time(&g_st.t_interp_ms, &t0);
     /* --- Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) --- */
     amgd_spgemm_set_timer(0);
-    dcsr *AfW = amgd_spgemm(Af, W);
+    dcsr *Wt = amgd_transpose(W, NULL);
+    dcsr *AfW = spgemm_via_t(Af, AfT, W, Wt);
     dcsr *AfP = amgd_mpm(1., AfW, 1., Afc);
     dcsr_free(&AfW);
     L->AfP = AfP;
-    dcsr *Wt = amgd_transpose(W, NULL);
     dcsr *WtAfP = amgd_spgemm(Wt, AfP);
     dcsr *Acf = amgd_transpose(Afc, NULL);
-    dcsr *AcfW = amgd_spgemm(Acf, W);
+    dcsr *AcfW = spgemm_via_t(Acf, Afc, W, Wt);      /* Acf' = Afc exactly */
+    if (AfT) dcsr_free(&AfT);
     amgd_spgemm_set_timer(-1);
     dcsr *Atmp = amgd_mpm(1., WtAfP, 1., AcfW);
     A = amgd_mpm(1., Atmp, 1, Ac);

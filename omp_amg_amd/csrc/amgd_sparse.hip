@@ -696,6 +696,77 @@ __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int
 
 __device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) { return (j * 2654435761u) >> (32 - lg); }
 
+// Emit a finished row from the LDS hash: occupied nonzero slots are compacted to
+// the front (order kept), bitonic-sorted by column and written at xro[i].
+template <int NT, uint32_t S>
+__device__ __forceinline__ void sg_emit(uint32_t *hk, double *hv, uint32_t *wtot, uint32_t *scr,
+                                        int t, uint64_t ob, uint32_t *xcol, double *xa,
+                                        uint64_t *cnt_i) {
+  uint32_t base = 0;
+  for (uint32_t c0 = 0; c0 < S; c0 += NT) {
+    uint32_t s = c0 + t;
+    uint32_t key = hk[s];
+    double val = hv[s];
+    bool take = key != EMPTY_KEY && val != 0.0;
+    uint32_t inc = block_incl_scan<NT>(take ? 1u : 0u, wtot);
+    uint32_t tot = __shfl(inc, 63, 64);
+    if (NT > 64) {
+      if (t == NT - 1) scr[0] = inc;
+      __syncthreads();
+      tot = scr[0];
+    }
+    __syncthreads();
+    if (take) {
+      hk[base + inc - 1] = key;
+      hv[base + inc - 1] = val;
+    }
+    base += tot;
+    __syncthreads();
+  }
+  const uint32_t n = base;
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t s = n + t; s < P; s += NT) hk[s] = EMPTY_KEY;
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1)
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t tt = t; tt < P / 2; tt += NT) {
+        uint32_t lo = 2 * tt - (tt & (stride - 1));
+        uint32_t hi = lo + stride;
+        bool up = (lo & size) == 0;
+        uint32_t kl = hk[lo], kh = hk[hi];
+        if ((kl > kh) == up) {
+          hk[lo] = kh; hk[hi] = kl;
+          double x = hv[lo]; hv[lo] = hv[hi]; hv[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  for (uint32_t s = t; s < n; s += NT) { xcol[ob + s] = hk[s]; xa[ob + s] = hv[s]; }
+  if (t == 0) *cnt_i = n;
+  __syncthreads();
+}
+
+// insert key j into the open-addressing LDS hash (linear probing); returns the slot,
+// counts newly filled slots in *nfill
+// (at most S probes: a full table -- only possible in a symbolic pass past its
+// capacity -- returns EMPTY_KEY instead of spinning)
+template <int LG>
+__device__ __forceinline__ uint32_t sg_insert(uint32_t *hk, uint32_t j, unsigned *nfill, bool count) {
+  constexpr uint32_t S = 1u << LG;
+  uint32_t sl = sg_hash(j, LG);
+  for (uint32_t probe = 0; probe < S; probe++) {
+    uint32_t old = atomicCAS(&hk[sl], EMPTY_KEY, j);
+    if (old == EMPTY_KEY) {
+      if (count) atomicAdd(nfill, 1u);
+      return sl;
+    }
+    if (old == j) return sl;
+    sl = (sl + 1) & (S - 1);
+  }
+  return EMPTY_KEY;
+}
+
 #define SG_U 4   // sub-chunks whose product loads are issued together
 // MODE 0: count distinct columns (cap: overflow -> OVERFLOW_MARK)
 // MODE 1: numeric, write nonzeros sorted at xro[i], count to cnt[i]
@@ -825,51 +896,96 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
       __syncthreads();
       continue;
     }
-    // compact occupied nonzero slots to the front (in place, order kept)
-    uint32_t base = 0;
-    for (uint32_t c0 = 0; c0 < S; c0 += NT) {
-      uint32_t s = c0 + t;
-      uint32_t key = hk[s];
-      double val = hv[s];
-      bool take = key != EMPTY_KEY && val != 0.0;
-      uint32_t inc = block_incl_scan<NT>(take ? 1u : 0u, wtot);
-      uint32_t tot = __shfl(inc, 63, 64);
-      if (NT > 64) {
-        if (t == NT - 1) wend[0] = inc;
-        __syncthreads();
-        tot = wend[0];
-      }
-      __syncthreads();
-      if (take) {
-        hk[base + inc - 1] = key;
-        hv[base + inc - 1] = val;
-      }
-      base += tot;
-      __syncthreads();
+    sg_emit<NT, S>(hk, hv, wtot, wend, t, xro[i], xcol, xa, &cnt[i]);
+  }
+}
+
+// k-sequential SpGEMM row kernel for long B rows (the avg B row spans the block):
+// one row per work-group; the A entries are taken one at a time in ascending k and
+// all NT threads cover that B row (coalesced, every product is a distinct column),
+// then a barrier orders layer k before layer k+1 -- the reference's order with no
+// per-product layer search.  MODE 0 counts distinct columns (no ordering needed),
+// MODE 1 accumulates and emits like k_sg_row.
+template <int NT, int LG, int MODE, int RAP = 0>
+__global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t nrows,
+                                                const uint64_t *aro, const uint32_t *acol,
+                                                const double *aa, const uint64_t *bro,
+                                                const uint32_t *bcol, const double *ba,
+                                                uint32_t cap, uint64_t *cnt, const uint64_t *xro,
+                                                uint32_t *xcol, double *xa) {
+  constexpr uint32_t S = 1u << LG;
+  __shared__ uint32_t hk[S];
+  __shared__ double hv[MODE ? S : 1];
+  __shared__ uint64_t wbs[NT];
+  __shared__ uint32_t wlen[NT];
+  __shared__ double wav[NT];
+  __shared__ uint32_t wtot[NT / 64 + 1];
+  __shared__ unsigned nfill;
+  __shared__ int ovf;
+  const int t = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t i = rows[r];
+    for (uint32_t s = t; s < S; s += NT) {
+      hk[s] = EMPTY_KEY;
+      if (MODE) hv[s] = 0.0;
     }
-    const uint32_t n = base;
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t s = n + t; s < P; s += NT) hk[s] = EMPTY_KEY;
+    if (t == 0) { nfill = 0; ovf = 0; }
     __syncthreads();
-    for (uint32_t size = 2; size <= P; size <<= 1)
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t tt = t; tt < P / 2; tt += NT) {
-          uint32_t lo = 2 * tt - (tt & (stride - 1));
-          uint32_t hi = lo + stride;
-          bool up = (lo & size) == 0;
-          uint32_t kl = hk[lo], kh = hk[hi];
-          if ((kl > kh) == up) {
-            hk[lo] = kh; hk[hi] = kl;
-            double x = hv[lo]; hv[lo] = hv[hi]; hv[hi] = x;
-          }
+    const uint64_t a0 = aro[i], a1 = aro[i + 1];
+    for (uint64_t wb = a0; wb < a1; wb += NT) {
+      const uint64_t ka = wb + t;
+      uint32_t len = 0;
+      uint64_t bs = 0;
+      double av = 0.0;
+      if (ka < a1) {
+        const uint32_t k = acol[ka];
+        if (!(ka + 1 < a1 && acol[ka + 1] == k)) {   // duplicate columns: the last one wins
+          bs = bro[k];
+          len = (uint32_t)(bro[k + 1] - bs);
+          av = aa[ka];
         }
-        __syncthreads();
       }
-    const uint64_t ob = xro[i];
-    for (uint32_t s = t; s < n; s += NT) { xcol[ob + s] = hk[s]; xa[ob + s] = hv[s]; }
-    if (t == 0) cnt[i] = n;
-    __syncthreads();
+      wbs[t] = bs;
+      wlen[t] = len;
+      wav[t] = av;
+      __syncthreads();
+      const int ne = (int)min((uint64_t)NT, a1 - wb);
+      for (int e = 0; e < ne; e++) {
+        const uint32_t L = wlen[e];
+        if (L == 0) continue;                        // uniform
+        const uint64_t b0 = wbs[e];
+        const double a = wav[e];
+        for (uint32_t j0 = 0; j0 < L; j0 += 2 * NT) {
+          const uint32_t ja = j0 + t, jb = j0 + NT + t;
+          uint32_t ca = 0, cb = 0;
+          double pa = 0.0, pb = 0.0;
+          if (ja < L) { ca = bcol[b0 + ja]; if (MODE) pa = ba[b0 + ja] * a; }
+          if (jb < L) { cb = bcol[b0 + jb]; if (MODE) pb = ba[b0 + jb] * a; }
+          if (ja < L) {
+            const uint32_t sl = sg_insert<LG>(hk, ca, &nfill, MODE == 0);
+            if (MODE) hv[sl] = hv[sl] + pa;
+            else if (sl == EMPTY_KEY) ovf = 1;
+          }
+          if (jb < L) {
+            const uint32_t sl = sg_insert<LG>(hk, cb, &nfill, MODE == 0);
+            if (MODE) hv[sl] = hv[sl] + pb;
+            else if (sl == EMPTY_KEY) ovf = 1;
+          }
+          if (MODE == 0 && (ovf || nfill > cap)) break;   // racy LDS read: early exit only
+        }
+        if (MODE == 1) __syncthreads();              // layer k before layer k+1
+        else if (ovf || nfill > cap) break;
+      }
+      __syncthreads();
+      if (MODE == 0 && (ovf || nfill > cap)) break;
+    }
+    if (MODE == 0) {
+      __syncthreads();
+      if (t == 0) cnt[i] = (ovf || nfill > cap) ? OVERFLOW_MARK : (uint64_t)nfill;
+      __syncthreads();
+      continue;
+    }
+    sg_emit<NT, S>(hk, hv, wtot, wlen, t, xro[i], xcol, xa, &cnt[i]);
   }
 }
 
@@ -944,6 +1060,13 @@ void amgd_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *
 
 // event timing of the numeric SpGEMM kernels (the RAP products) + algorithmic bytes:
 // A (12 B/nnz + 8 B/row), B (12 B/nnz + 8 B/row) and X (12 B/nnz + 8 B/row) once each.
+#define KSEQ_MIN 64
+static int g_sg_flat = -1;      // AMGD_SG_FLAT=1 / amgd_spgemm_force_flat(1): flat kernels only
+static bool sg_force_flat() {
+  if (g_sg_flat < 0) { const char *e = getenv("AMGD_SG_FLAT"); g_sg_flat = (e && *e && *e != '0') ? 1 : 0; }
+  return g_sg_flat == 1;
+}
+extern "C" void amgd_spgemm_force_flat(int on) { g_sg_flat = on ? 1 : 0; }
 static int g_sg_slot = -1;
 static uint64_t g_sg_bytes = 0;
 extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
@@ -978,13 +1101,28 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     amgd_d2h(hc, counts, 8);
   }
   // symbolic: distinct count per row (row order in the lists is arbitrary; rows are independent)
-  if (hc[0])
-    k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
-        lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
-  if (hc[1])
-    k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
-        lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
-        nullptr);
+  // long B rows (mean >= KSEQ_MIN): the k-sequential kernels; short ones: flat enumeration
+  const uint64_t avgB = B->rn ? B->nnz / B->rn : 0;
+  const bool kseq = avgB >= KSEQ_MIN && !sg_force_flat();
+  const bool wide = avgB >= 256;
+  if (hc[0]) {
+    if (kseq)
+      k_sg_kseq<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
+          lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
+    else
+      k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
+          lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
+  }
+  if (hc[1]) {
+    if (kseq)
+      k_sg_kseq<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
+          nullptr);
+    else
+      k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
+          nullptr);
+  }
   KCHECK();
   // numeric bins by distinct count: wave/512, wave/2048, wave/4096, block/8192 slots, dense slab
   unsigned hn[SG_MAXBIN] = {0};
@@ -1015,20 +1153,32 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   HIPCK(hipMemsetAsync(cnt2, 0, L * 8, s));
   if (hn[4]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
   if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
-#define SG_NUM(NT, LG, bin, gmax)                                                               \
+#define SG_NUM(KER, NT, LG, bin, gmax)                                                          \
   if (hn[bin]) {                                                                                \
     if (rap)                                                                                    \
-      k_sg_row<NT, LG, 1, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(            \
+      KER<NT, LG, 1, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
     else                                                                                        \
-      k_sg_row<NT, LG, 1, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(            \
+      KER<NT, LG, 1, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
   }
   const bool rap = g_sg_slot >= 0;
-  SG_NUM(64, 9, 0, 65536u)
-  SG_NUM(64, 11, 1, 65536u)
-  SG_NUM(64, 12, 2, 65536u)
-  SG_NUM(256, 13, 3, 8192u)
+  if (kseq && wide) {
+    SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
+    SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
+    SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
+    SG_NUM(k_sg_kseq, 256, 13, 3, 8192u)
+  } else if (kseq) {
+    SG_NUM(k_sg_kseq, 64, 9, 0, 65536u)
+    SG_NUM(k_sg_kseq, 64, 11, 1, 65536u)
+    SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
+    SG_NUM(k_sg_kseq, 256, 13, 3, 8192u)
+  } else {
+    SG_NUM(k_sg_row, 64, 9, 0, 65536u)
+    SG_NUM(k_sg_row, 64, 11, 1, 65536u)
+    SG_NUM(k_sg_row, 64, 12, 2, 65536u)
+    SG_NUM(k_sg_row, 256, 13, 3, 8192u)
+  }
 #undef SG_NUM
   if (hn[4]) {
     if (rap)
@@ -1058,10 +1208,18 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   amgd_free(ub); amgd_free(lists); amgd_free(counts);
   if (slab_v) { amgd_free(slab_v); amgd_free(slab_s); }
   if (sglog) {
+    uint64_t prods = 0;
+    if (rn) {   // products = sum of the per-row upper bounds (recomputed: ub was freed)
+      uint64_t *u2 = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+      k_spgemm_ub<<<grid_for(rn), 256, 0, s>>>(A->ro, A->col, rn, B->ro, u2);
+      prods = amgd_scan_u64(u2, rn);
+      amgd_free(u2);
+    }
     amgd_sync();
-    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
-            rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz, hc[0],
-            hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], (amgd_wtime() - t_start) * 1e3);
+    double ms = (amgd_wtime() - t_start) * 1e3;
+    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
+            rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz,
+            (unsigned long)prods, prods / (ms * 1e6), hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], ms);
   }
   return X;
 }

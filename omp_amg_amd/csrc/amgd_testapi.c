@@ -128,3 +128,7 @@ API void amgd_test_lmop_stats(uint64_t *out, int reset) {
   amgd_lmop_stats(out);
   if (reset) amgd_lmop_stats_reset();
 }
+
+/* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
+extern void amgd_spgemm_force_flat(int on);
+API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }

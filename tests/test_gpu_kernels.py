@@ -38,6 +38,46 @@ def test_spgemm_dense_overflow_rows():
     assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
 
 
+@pytest.mark.parametrize("case", ["narrow", "wide", "dense_rows", "dups_cancel"])
+def test_spgemm_kseq_long_b_rows(case):
+    """k-sequential kernels (mean B row >= 64): every numeric bin incl. the dense slab,
+    duplicate columns in A rows (last one wins) and exact cancellation"""
+    rng = np.random.default_rng({"narrow": 31, "wide": 32, "dense_rows": 33, "dups_cancel": 34}[case])
+    if case == "narrow":        # mean B row ~100: wave-sized blocks for the small bins
+        A = refops.rand_csr(rng, 400, 300, 0.02)
+        B = refops.rand_csr(rng, 300, 3000, 0.035)
+    elif case == "wide":        # mean B row ~600: 256-thread blocks everywhere
+        A = refops.rand_csr(rng, 200, 150, 0.04)
+        B = refops.rand_csr(rng, 150, 6000, 0.1)
+    elif case == "dense_rows":  # > 4096 distinct columns in some rows
+        A = refops.rand_csr(rng, 20, 200, 0.3)
+        B = refops.rand_csr(rng, 200, 9000, 0.05)
+    else:
+        A = refops.rand_csr(rng, 150, 120, 0.05, ints=True)
+        B = refops.rand_csr(rng, 120, 400, 0.3, ints=True)
+        # duplicate a few A columns in place (sorted rows keep them adjacent)
+        cols, vals, ro = [], [], [0]
+        for i in range(A.rn):
+            s, e = A.row_off[i], A.row_off[i + 1]
+            for k in range(s, e):
+                cols.append(A.col[k]); vals.append(A.a[k])
+                if k % 7 == 0:
+                    cols.append(A.col[k]); vals.append(A.a[k] + 1.0)
+            ro.append(len(cols))
+        A = refops.Csr(A.rn, A.cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+    assert B.a.size >= 64 * B.rn
+    R = refops.spgemm(A, B)
+    oa.spgemm_flat(False)
+    X = oa.test_csr_op(0, A, B)
+    oa.spgemm_flat(True)
+    try:
+        Y = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_flat(False)
+    assert refops.same(X, R)
+    assert refops.same(Y, R)
+
+
 def test_spgemm_empty_rows():
     rng = np.random.default_rng(3)
     A = refops.rand_csr(rng, 50, 40, 0.02)
