@@ -102,13 +102,13 @@ static void ph_report(uint32_t nl) {
 }
 
 /* X = A*B, given At = A' and Bt = B'.  When A has long columns (mean row of At
-   >= 64) and B short rows, X' = Bt*At has long B-operand rows and takes the
-   k-sequential SpGEMM kernels; it is the same Gustavson sum (k ascending over the
+   >= 64 and at least twice B's mean row), X' = Bt*At has the longer B-operand
+   rows and runs better on the k-sequential SpGEMM kernels; it is the same Gustavson sum (k ascending over the
    shared index, products commute, same exact-zero drop), transposed back stably.
    Bit-identical to amgd_spgemm(A, B) either way. */
 static dcsr *spgemm_via_t(const dcsr *A, const dcsr *At, const dcsr *B, const dcsr *Bt) {
   const uint64_t avg_at = At && At->rn ? At->nnz / At->rn : 0, avg_b = B->rn ? B->nnz / B->rn : 0;
-  if (!At || !Bt || avg_at < 64 || avg_b >= 64) return amgd_spgemm(A, B);
+  if (!At || !Bt || avg_at < 64 || avg_at < 2 * avg_b) return amgd_spgemm(A, B);
   dcsr *Xt = amgd_spgemm(Bt, At);
   dcsr *X = amgd_transpose(Xt, NULL);
   dcsr_free(&Xt);

@@ -1129,7 +1129,8 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   if (rn) {
     HIPCK(hipMemsetAsync(counts, 0, 64, s));
     SgBins b;
-    b.lim[0] = 256; b.lim[1] = 1024; b.lim[2] = 2048; b.lim[3] = 4096;
+    // (k-sequential kernels take the 8192-slot table up to 75% load)
+    b.lim[0] = 256; b.lim[1] = 1024; b.lim[2] = 2048; b.lim[3] = kseq ? 6144 : 4096;
     k_bin_rows<<<grid_for(rn), 256, 0, s>>>(cnt, rn, b, 5, 1, lists, counts);
     KCHECK();
     amgd_d2h(hn, counts, 20);
