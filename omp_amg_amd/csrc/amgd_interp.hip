@@ -373,6 +373,51 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
     KCHECK();
     amgd_d2h(hn, cnt, 20);
   }
+  // Huge supports (the orphan support gathered at coarse point 0): one cooperative
+  // launch each on a side stream, issued before the other tiers so that its
+  // latency-bound k-loop runs beside them instead of after them.  The stream is
+  // idle here (the tier counts were just read back), so no event is needed before.
+  static hipStream_t s2 = nullptr;
+  static hipEvent_t ev2 = nullptr;
+  std::vector<void *> coop_bufs;
+  if (hn[4]) {
+    if (!s2) {
+      HIPCK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      HIPCK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
+    }
+    std::vector<uint32_t> big(hn[4]);
+    amgd_d2h(big.data(), lists + 4 * L, (size_t)hn[4] * 4);
+    std::vector<uint64_t> ro(rn + 1);
+    amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
+    for (uint32_t c : big) {
+      uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
+      if (nz > QF_COOP_MAX) {
+        fprintf(stderr, "omp_amg_amd: support of %u points exceeds QF_COOP_MAX\n", nz);
+        abort();
+      }
+      double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
+      double *s2v = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
+      unsigned *bar = (unsigned *)amgd_alloc(16);
+      HIPCK(hipMemsetAsync(bar, 0, 16, s2));
+      coop_bufs.push_back(s1b);
+      coop_bufs.push_back(bar);
+      int G = (int)std::min<uint32_t>((nz + 63) / 64, 256u);
+      const uint64_t *pwro = Wt->ro, *paro = A->ro, *pqoff = qoff;
+      const uint32_t *pwcol = Wt->col, *pacol = A->col;
+      const double *paa = A->a;
+      void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2v, &qk, &bar};
+      static bool attr = false;
+      if (!attr) {
+        HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
+        attr = true;
+      }
+      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
+                                       (unsigned)(2 * (size_t)nz * 8), s2));
+      KCHECK();
+    }
+    HIPCK(hipEventRecord(ev2, s2));
+  }
   // tiers by support size: the LDS triangle sized to the tier keeps small supports at
   // high occupancy (nz <= 32: 4 KB per wavefront)
   if (hn[0])
@@ -388,37 +433,9 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
     k_qfactor_mid<<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
         lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   KCHECK();
-  if (hn[4]) {                    // huge supports, one cooperative launch each
-    std::vector<uint32_t> big(hn[4]);
-    amgd_d2h(big.data(), lists + 4 * L, (size_t)hn[4] * 4);
-    std::vector<uint64_t> ro(rn + 1);
-    amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
-    for (uint32_t c : big) {
-      uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
-      if (nz > QF_COOP_MAX) {
-        fprintf(stderr, "omp_amg_amd: support of %u points exceeds QF_COOP_MAX\n", nz);
-        abort();
-      }
-      double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
-      double *s2 = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
-      unsigned *bar = (unsigned *)amgd_alloc(16);
-      amgd_memset(bar, 0, 16);
-      int G = (int)std::min<uint32_t>((nz + 63) / 64, 256u);
-      const uint64_t *pwro = Wt->ro, *paro = A->ro, *pqoff = qoff;
-      const uint32_t *pwcol = Wt->col, *pacol = A->col;
-      const double *paa = A->a;
-      void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2, &qk, &bar};
-      static bool attr = false;
-      if (!attr) {
-        HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
-        attr = true;
-      }
-      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
-                                       (unsigned)(2 * (size_t)nz * 8), s));
-      KCHECK();
-      amgd_free(s1b); amgd_free(bar);
-    }
+  if (hn[4]) {                    // the library stream waits for the side stream
+    HIPCK(hipStreamWaitEvent(s, ev2, 0));
+    for (void *p : coop_bufs) amgd_free(p);   // reuse is ordered after the wait
   }
   if (sglog) {
     amgd_sync();
