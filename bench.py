@@ -204,7 +204,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps)
         print(json.dumps(out), flush=True)
     ds.close()
-    oa.lib().amgd_shutdown()
+    # (no amgd_shutdown here: the process exits and the driver reclaims everything;
+    # tearing the HIP stream down before exit crashes rocprofv3's own finalisation)
     hb.set()
     if dist is not None:
         dist.destroy_process_group()

@@ -38,6 +38,7 @@ void amgd_rt_shutdown(void);             /* free everything; pointers become inv
 void amgd_pool_release(void);            /* return every cached block to the driver */
 size_t amgd_pool_bytes_in_use(void);
 size_t amgd_pool_peak_bytes(void);
+void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease);
 void amgd_h2d(void *d, const void *h, size_t n);
 void amgd_d2h(void *h, const void *d, size_t n);
 void amgd_d2d(void *d, const void *s, size_t n);

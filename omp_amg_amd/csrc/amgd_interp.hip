@@ -908,10 +908,11 @@ extern "C" uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad) {
 __global__ __launch_bounds__(64) void k_expand_pick(const uint64_t *ro, const uint32_t *col,
                                                     const double *a, uint32_t rn,
                                                     const uint8_t *bad, uint32_t *scol,
-                                                    double *sval, uint32_t *pj, uint64_t *cnt) {
+                                                    double *sval, uint32_t *pj, uint64_t *cnt,
+                                                    int keep_unmasked) {
   const int lane = threadIdx.x;
   for (uint32_t i = blockIdx.x; i < rn; i += gridDim.x) {
-    if (!bad[i]) { if (lane == 0) cnt[i] = 0; continue; }
+    if (!bad[i]) { if (lane == 0 && !keep_unmasked) cnt[i] = 0; continue; }
     uint64_t r0 = ro[i];
     uint32_t L = (uint32_t)(ro[i + 1] - r0);
     for (uint32_t e = lane; e < L; e += 64) {
@@ -948,6 +949,75 @@ __global__ __launch_bounds__(64) void k_expand_pick(const uint64_t *ro, const ui
     __syncthreads();
   }
 }
+// Long bad rows: the same ranking by an LDS bitonic sort on (|value| descending,
+// position ascending) -- a strict total order, so it equals the stable merge order
+// of the reference's qsort -- instead of the O(L^2) rank count.  Rows longer than
+// EP_MAXL keep the rank-count kernel.
+#define EP_MAXL 4096
+__global__ __launch_bounds__(256) void k_expand_pick_sort(const uint64_t *ro, const uint32_t *col,
+                                                          const double *a, uint32_t rn,
+                                                          const uint8_t *bad, uint32_t *scol,
+                                                          double *sval, uint32_t *pj,
+                                                          uint64_t *cnt, unsigned *longrows) {
+  __shared__ double kv[EP_MAXL];
+  __shared__ uint32_t kp[EP_MAXL];
+  __shared__ uint32_t Nsh;
+  const int t = threadIdx.x;
+  for (uint32_t i = blockIdx.x; i < rn; i += gridDim.x) {
+    if (!bad[i]) { if (t == 0) cnt[i] = 0; continue; }
+    const uint64_t r0 = ro[i];
+    const uint32_t L = (uint32_t)(ro[i + 1] - r0);
+    if (L > EP_MAXL) { if (t == 0) { cnt[i] = ~0ull; atomicAdd(longrows, 1u); } continue; }
+    uint32_t P = 1;
+    while (P < L) P <<= 1;
+    for (uint32_t e = t; e < P; e += 256) {
+      kv[e] = e < L ? fabs(a[r0 + e]) : -1.0;
+      kp[e] = e;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1)
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t tt = t; tt < P / 2; tt += 256) {
+          const uint32_t lo = 2 * tt - (tt & (stride - 1)), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const double vl = kv[lo], vh = kv[hi];
+          const uint32_t pl = kp[lo], ph = kp[hi];
+          const bool hi_first = vh > vl || (vh == vl && ph < pl);   // hi ranks before lo
+          if (hi_first == up) { kv[lo] = vh; kv[hi] = vl; kp[lo] = ph; kp[hi] = pl; }
+        }
+        __syncthreads();
+      }
+    for (uint32_t r = t; r < L; r += 256) {
+      scol[r0 + r] = col[r0 + kp[r]];
+      sval[r0 + r] = kv[r];
+    }
+    __syncthreads();
+    if (t == 0) {
+      double tot = 0.0;
+      for (uint32_t p = 0; p < L; p++) if (kv[p] != 0.) tot += kv[p];
+      double V = tot * 0.5;
+      uint32_t c = 0;
+      if (V != 0.) {
+        double sum = 0.0;
+        for (uint32_t p = 0; p < L; p++) {
+          if (kv[p] != 0.) sum += kv[p];
+          if (sum - V < 0) c++;
+        }
+      }
+      uint32_t N = c + 1;
+      Nsh = N < L ? N : L;
+      cnt[i] = Nsh;
+    }
+    __syncthreads();
+    const uint32_t N = Nsh;
+    for (uint32_t p = t; p < N; p += 256) pj[r0 + p] = col[r0 + kp[p]];
+    __syncthreads();
+  }
+}
+// rows the sort kernel left (cnt == ~0): the rank-count kernel on just those
+__global__ void k_long_mask(const uint64_t *cnt, uint32_t rn, uint8_t *m) {
+  GRID_STRIDE(i, rn) m[i] = cnt[i] == ~0ull ? 1 : 0;
+}
 __global__ void k_pick_compact(const uint64_t *ro, const uint64_t *off, const uint32_t *pj,
                                uint32_t rn, uint32_t *oi, uint32_t *oj) {
   GRID_STRIDE(i, rn) {
@@ -967,7 +1037,23 @@ extern "C" uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)Xf->rn + 1) * 8);
   if (Xf->rn) {
     int g = (int)std::min<uint32_t>(Xf->rn, 65536u);
-    k_expand_pick<<<g, 64, 0, s>>>(Xf->ro, Xf->col, Xf->a, Xf->rn, bad, scol, sval, tj, cnt);
+    if (Xf->nnz >= 64ull * Xf->rn) {      // long rows: LDS sort, then the few longer ones
+      unsigned *nl = (unsigned *)amgd_alloc(4);
+      amgd_memset(nl, 0, 4);
+      k_expand_pick_sort<<<g, 256, 0, s>>>(Xf->ro, Xf->col, Xf->a, Xf->rn, bad, scol, sval, tj,
+                                           cnt, nl);
+      unsigned hl = 0;
+      amgd_d2h(&hl, nl, 4);
+      if (hl) {
+        uint8_t *lm = (uint8_t *)amgd_alloc((size_t)Xf->rn + 1);
+        k_long_mask<<<grid_for(Xf->rn), 256, 0, s>>>(cnt, Xf->rn, lm);
+        k_expand_pick<<<g, 64, 0, s>>>(Xf->ro, Xf->col, Xf->a, Xf->rn, lm, scol, sval, tj, cnt, 1);
+        amgd_free(lm);
+      }
+      amgd_free(nl);
+    } else {
+      k_expand_pick<<<g, 64, 0, s>>>(Xf->ro, Xf->col, Xf->a, Xf->rn, bad, scol, sval, tj, cnt, 0);
+    }
     KCHECK();
   }
   uint64_t n = amgd_scan_u64(cnt, Xf->rn);

@@ -77,6 +77,12 @@ extern "C" void amgd_set_stream(void *s) { amgd_s(); g_stream = (hipStream_t)s; 
 struct Blk { void *p; size_t sz; };
 static std::vector<Blk> g_free, g_used;
 static size_t g_inuse = 0, g_peak = 0;
+// pool statistics (AMGD_PHASES report): driver allocations, their time, cache flushes
+static uint64_t g_nmalloc = 0, g_nrelease = 0;
+static double g_tmalloc = 0, g_bmalloc = 0;
+extern "C" void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease) {
+  *nmalloc = g_nmalloc; *gbytes = g_bmalloc / 1e9; *ms = g_tmalloc * 1e3; *nrelease = g_nrelease;
+}
 
 extern "C" void *amgd_alloc(size_t bytes) {
   amgd_s();
@@ -93,13 +99,18 @@ extern "C" void *amgd_alloc(size_t bytes) {
     g_free.pop_back();
   } else {
     b.sz = sz;
+    auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&b.p, sz);
     if (e != hipSuccess) {
       // release the cache and retry once before failing loudly
       (void)hipGetLastError();
       amgd_pool_release();
+      g_nrelease++;
       HIPCK(hipMalloc(&b.p, sz));
     }
+    g_tmalloc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    g_nmalloc++;
+    g_bmalloc += (double)sz;
   }
   g_used.push_back(b);
   g_inuse += b.sz;

@@ -99,6 +99,11 @@ static void ph_report(uint32_t nl) {
   fprintf(stderr, "sum");
   for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9.1f", tot[p]);
   fprintf(stderr, "\n");
+  uint64_t nm, nr;
+  double gb, ms;
+  amgd_pool_stats(&nm, &gb, &ms, &nr);
+  fprintf(stderr, "pool: %lu driver allocations, %.1f GB, %.1f ms in hipMalloc, %lu cache flushes\n",
+          (unsigned long)nm, gb, ms, (unsigned long)nr);
 }
 
 /* X = A*B, given At = A' and Bt = B'.  When A has long columns (mean row of At

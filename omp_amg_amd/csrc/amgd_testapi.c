@@ -51,6 +51,17 @@ API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, doub
       amgd_memset(X->col, 0, tot * 4 + 4);
       break;
     }
+    case 6: {                     /* expand_support picks on every row of A: X = pattern (ones) */
+      uint8_t *all = (uint8_t *)amgd_alloc((size_t)A->rn + 1);
+      amgd_memset(all, 1, (size_t)A->rn + 1);
+      uint32_t *pi = NULL, *pj = NULL;
+      uint64_t np = amgd_expand_pick(A, all, &pi, &pj);
+      double *ones = (double *)amgd_alloc(np * 8 + 8);
+      amgd_vfill(ones, np, 1.0);
+      X = amgd_coo2csr(np, pi, pj, ones, A->rn, A->cn, 1);
+      amgd_free(all); amgd_free(pi); amgd_free(pj); amgd_free(ones);
+      break;
+    }
     default: return -2;
   }
   down(X, HX);

@@ -123,3 +123,34 @@ def same(X, Y):
     return (X.rn == Y.rn and X.cn == Y.cn and np.array_equal(X.row_off, Y.row_off)
             and np.array_equal(X.col, Y.col)
             and np.array_equal(np.asarray(X.a).view(np.uint64), np.asarray(Y.a).view(np.uint64)))
+
+
+def expand_pick(X):
+    """expand_support's pick per row (amg_setup.c:1000-1115): |X| ranked by descending
+    value, ties in column order (glibc qsort, stable); running sum of the nonzero
+    values against half the total; the first N = 1 + #{sum - V < 0} ranks (capped at
+    the row length) are picked.  Returns the picked pattern as a Csr of ones."""
+    ro, cols = [0], []
+    for i in range(X.rn):
+        s, e = X.row_off[i], X.row_off[i + 1]
+        v = np.abs(np.asarray(X.a[s:e]))
+        order = sorted(range(e - s), key=lambda q: (-v[q], q))
+        sv = [v[q] for q in order]
+        tot = 0.0
+        for x in sv:
+            if x != 0.0:
+                tot += x
+        V = tot * 0.5
+        c = 0
+        if V != 0.0:
+            run = 0.0
+            for x in sv:
+                if x != 0.0:
+                    run += x
+                if run - V < 0:
+                    c += 1
+        N = min(c + 1, e - s)
+        picked = sorted(int(X.col[s + q]) for q in order[:N])
+        cols.extend(picked)
+        ro.append(len(cols))
+    return Csr(X.rn, X.cn, np.array(ro), np.array(cols, dtype=np.int64), np.ones(len(cols)))

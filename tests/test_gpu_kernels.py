@@ -300,3 +300,21 @@ def test_qfactor_tiers_bitexact():
     ref = _oracle_qfactor(W, A)
     assert X.nnz == len(ref)
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("case", ["short", "long", "ties", "over_lds"])
+def test_expand_pick(case):
+    """expand_support's per-row pick: short rows (rank-count kernel), long rows (LDS
+    bitonic sort), tied values (stable order), rows past the LDS sort capacity"""
+    rng = np.random.default_rng({"short": 41, "long": 42, "ties": 43, "over_lds": 44}[case])
+    if case == "short":
+        X = refops.rand_csr(rng, 300, 200, 0.04)
+    elif case == "long":
+        X = refops.rand_csr(rng, 60, 5000, 0.05, minrow=70)
+    elif case == "ties":
+        X = refops.rand_csr(rng, 80, 3000, 0.05, ints=True, minrow=70)
+    else:
+        X = refops.rand_csr(rng, 6, 9000, 0.5)
+        X.a[::5] = 0.0
+    assert oa.test_csr_op(6, X).nnz == refops.expand_pick(X).nnz
+    assert refops.same(oa.test_csr_op(6, X), refops.expand_pick(X))

@@ -36,4 +36,5 @@ for m in sizes:
         keep = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()}
         print(json.dumps({"m": m, "rows": m ** 3, "exact": exact, "gen_s": round(gen, 1), **keep}), flush=True)
     ds.close()
-oa.lib().amgd_shutdown()
+# no amgd_shutdown at exit: tearing the HIP stream down first crashes rocprofv3's finalisation
+
