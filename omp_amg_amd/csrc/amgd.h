@@ -92,8 +92,11 @@ void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const doubl
 void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
 void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */
 void amgd_diag(const dcsr *A, double *D);
-enum { AMGD_DPLUS = 0, AMGD_DMINUS = 1, AMGD_DMULT = 2, AMGD_MULTD = 3 };
+enum { AMGD_DPLUS = 0, AMGD_DMINUS = 1, AMGD_DMULT = 2, AMGD_MULTD = 3,
+       AMGD_SCALE2 = 4, AMGD_SCALE_ABS = 5, AMGD_SCALE2_ABS = 6 };
 void amgd_diag_op(dcsr *A, const double *D, int op);
+/* fused: SCALE2 a=(a*Dl[i])*Dr[col]; SCALE_ABS a=|a*Dl[i]|*Dr[col]; SCALE2_ABS a=|(a*Dl[i])*Dr[col]| */
+void amgd_diag_op2(dcsr *A, const double *Dl, const double *Dr, int op);
 void amgd_vals_abs(dcsr *A);
 void amgd_vals_sqr(dcsr *A);
 void amgd_vals_scale(dcsr *A, double s);

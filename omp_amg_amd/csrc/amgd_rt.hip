@@ -14,6 +14,9 @@
 #include <vector>
 #include <algorithm>
 #include <chrono>
+#include <map>
+#include <unordered_map>
+#include <iterator>
 
 #include "amgd.h"
 #include "amgd_dev.h"
@@ -70,73 +73,126 @@ hipStream_t amgd_s() {
 extern "C" void *amgd_stream(void) { return (void *)amgd_s(); }
 extern "C" void amgd_set_stream(void *s) { amgd_s(); g_stream = (hipStream_t)s; }
 
-// ---------------- caching pool ----------------
-// hipFree synchronises the device and hipMalloc costs tens of us; the setup
-// allocates thousands of short-lived buffers per level, so freed blocks are
-// cached by size and reused (first fit within 2x).
-struct Blk { void *p; size_t sz; };
-static std::vector<Blk> g_free, g_used;
+// ---------------- HBM arena ----------------
+// hipMalloc costs tens of microseconds to milliseconds (and hipFree synchronises
+// the device); the setup makes ~10^4-10^5 short-lived allocations per run, of
+// sizes from bytes to tens of GB.  One arena is reserved at the first allocation
+// (all free HBM but a margin, AMGD_ARENA_GB overrides; 0 disables) and carved
+// best-fit, with neighbouring free blocks coalesced on release.  Requests the
+// arena cannot hold fall back to hipMalloc.  Blocks are recycled in stream order
+// (one library stream; the Q-factor side stream is joined before its blocks are
+// freed), so no block is reused while a kernel may still touch it.
+static char *g_arena = nullptr;
+static size_t g_arena_sz = 0;
+static bool g_arena_tried = false;
+static std::map<size_t, size_t> g_free_off;          // offset -> size
+static std::multimap<size_t, size_t> g_free_sz;      // size -> offset
+static std::unordered_map<void *, size_t> g_used;    // live block -> size
+static std::unordered_map<void *, size_t> g_direct;  // live hipMalloc fallbacks -> size
 static size_t g_inuse = 0, g_peak = 0;
-// pool statistics (AMGD_PHASES report): driver allocations, their time, cache flushes
+// statistics (AMGD_PHASES report): driver allocations (arena + fallbacks), their time
 static uint64_t g_nmalloc = 0, g_nrelease = 0;
 static double g_tmalloc = 0, g_bmalloc = 0;
 extern "C" void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease) {
   *nmalloc = g_nmalloc; *gbytes = g_bmalloc / 1e9; *ms = g_tmalloc * 1e3; *nrelease = g_nrelease;
 }
+static void free_insert(size_t off, size_t sz) {
+  auto nx = g_free_off.lower_bound(off);
+  if (nx != g_free_off.end() && nx->first == off + sz) {         // merge with the next block
+    auto r = g_free_sz.equal_range(nx->second);
+    for (auto it = r.first; it != r.second; ++it) if (it->second == nx->first) { g_free_sz.erase(it); break; }
+    sz += nx->second;
+    nx = g_free_off.erase(nx);
+  }
+  if (nx != g_free_off.begin()) {                                 // merge with the previous block
+    auto pv = std::prev(nx);
+    if (pv->first + pv->second == off) {
+      auto r = g_free_sz.equal_range(pv->second);
+      for (auto it = r.first; it != r.second; ++it) if (it->second == pv->first) { g_free_sz.erase(it); break; }
+      off = pv->first;
+      sz += pv->second;
+      g_free_off.erase(pv);
+    }
+  }
+  g_free_off[off] = sz;
+  g_free_sz.insert({sz, off});
+}
+static void arena_init() {
+  g_arena_tried = true;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) { (void)hipGetLastError(); return; }
+  const size_t margin = 24ull << 30;
+  size_t want = fr > margin ? fr - margin : 0;
+  const char *e = getenv("AMGD_ARENA_GB");
+  if (e && *e) want = std::min<size_t>(want, (size_t)atoll(e) << 30);
+  want &= ~((size_t)(2u << 20) - 1);
+  auto t0 = std::chrono::steady_clock::now();
+  while (want >= (1ull << 30)) {
+    if (hipMalloc((void **)&g_arena, want) == hipSuccess) break;
+    (void)hipGetLastError();
+    g_arena = nullptr;
+    want /= 2;
+  }
+  g_tmalloc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (!g_arena) return;
+  g_arena_sz = want;
+  g_nmalloc++;
+  g_bmalloc += (double)want;
+  free_insert(0, want);
+}
 
 extern "C" void *amgd_alloc(size_t bytes) {
   amgd_s();
-  size_t sz = (bytes + 511) & ~(size_t)511;
-  if (sz == 0) sz = 512;
-  int best = -1;
-  for (int i = 0; i < (int)g_free.size(); i++)
-    if (g_free[i].sz >= sz && g_free[i].sz <= 2 * sz + (1 << 20) &&
-        (best < 0 || g_free[i].sz < g_free[best].sz)) best = i;
-  Blk b;
-  if (best >= 0) {
-    b = g_free[best];
-    g_free[best] = g_free.back();
-    g_free.pop_back();
-  } else {
-    b.sz = sz;
+  if (!g_arena_tried) arena_init();
+  size_t sz = (bytes + 255) & ~(size_t)255;
+  if (sz == 0) sz = 256;
+  void *p = nullptr;
+  auto it = g_free_sz.lower_bound(sz);                           // best fit
+  if (it != g_free_sz.end()) {
+    const size_t bsz = it->first, off = it->second;
+    g_free_sz.erase(it);
+    g_free_off.erase(off);
+    if (bsz > sz) free_insert(off + sz, bsz - sz);
+    p = g_arena + off;
+  } else {                                                        // arena full: the driver
     auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipMalloc(&b.p, sz);
-    if (e != hipSuccess) {
-      // release the cache and retry once before failing loudly
-      (void)hipGetLastError();
-      amgd_pool_release();
-      g_nrelease++;
-      HIPCK(hipMalloc(&b.p, sz));
-    }
+    HIPCK(hipMalloc(&p, sz));
     g_tmalloc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     g_nmalloc++;
     g_bmalloc += (double)sz;
+    g_direct[p] = sz;
   }
-  g_used.push_back(b);
-  g_inuse += b.sz;
+  g_used[p] = sz;
+  g_inuse += sz;
   if (g_inuse > g_peak) g_peak = g_inuse;
-  return b.p;
+  return p;
 }
 
 extern "C" void amgd_free(void *p) {
   if (!p) return;
-  for (size_t i = g_used.size(); i-- > 0;)
-    if (g_used[i].p == p) {
-      g_inuse -= g_used[i].sz;
-      g_free.push_back(g_used[i]);
-      g_used[i] = g_used.back();
-      g_used.pop_back();
-      return;
-    }
-  fprintf(stderr, "omp_amg_amd: amgd_free of unknown pointer %p\n", p);
-  abort();
+  auto it = g_used.find(p);
+  if (it == g_used.end()) {
+    fprintf(stderr, "omp_amg_amd: amgd_free of unknown pointer %p\n", p);
+    abort();
+  }
+  const size_t sz = it->second;
+  g_used.erase(it);
+  g_inuse -= sz;
+  auto d = g_direct.find(p);
+  if (d != g_direct.end()) {        // a fallback block goes back to the driver (stream-ordered)
+    g_direct.erase(d);
+    HIPCK(hipStreamSynchronize(g_stream));
+    HIPCK(hipFree(p));
+    g_nrelease++;
+    return;
+  }
+  free_insert((size_t)((char *)p - g_arena), sz);
 }
 
 extern "C" void amgd_pool_release(void) {
+  // the arena stays reserved for the process; nothing is cached outside it
   if (!g_inited) return;
   HIPCK(hipStreamSynchronize(g_stream));
-  for (auto &b : g_free) HIPCK(hipFree(b.p));
-  g_free.clear();
 }
 extern "C" size_t amgd_pool_bytes_in_use(void) { return g_inuse; }
 extern "C" size_t amgd_pool_peak_bytes(void) { return g_peak; }
@@ -889,10 +945,15 @@ extern "C" double amgd_fro_minus_eye(const dcsr *A) {
 extern "C" void amgd_rt_shutdown(void) {
   if (!g_inited) return;
   HIPCK(hipStreamSynchronize(g_stream));
-  for (auto &b : g_free) (void)hipFree(b.p);
-  for (auto &b : g_used) (void)hipFree(b.p);
-  g_free.clear();
+  for (auto &d : g_direct) (void)hipFree(d.first);
+  g_direct.clear();
   g_used.clear();
+  g_free_off.clear();
+  g_free_sz.clear();
+  if (g_arena) (void)hipFree(g_arena);
+  g_arena = nullptr;
+  g_arena_sz = 0;
+  g_arena_tried = false;
   g_inuse = 0;
   if (g_red) { (void)hipFree(g_red); g_red = nullptr; }
   if (g_red_h) { (void)hipHostFree(g_red_h); g_red_h = nullptr; }

@@ -130,9 +130,7 @@ static dcsr *strength(const dcsr *A) {
   amgd_vunary(D, A->rn, AMGD_V_SQRT);
   amgd_vunary(D, A->rn, AMGD_V_INV);
   dcsr *S = dcsr_copy(A);
-  amgd_diag_op(S, D, AMGD_DMULT);
-  amgd_diag_op(S, D, AMGD_MULTD);
-  amgd_vals_abs(S);
+  amgd_diag_op2(S, D, D, AMGD_SCALE2_ABS);          /* |D*A*D| in one pass */
   amgd_diag(S, D);
   amgd_diag_op(S, D, AMGD_DMINUS);
   amgd_free(D);
@@ -545,9 +543,7 @@ static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const r0_ctx *r0c
 
 static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr) {
   dcsr *R = dcsr_copy(X);
-  amgd_diag_op(R, Dl, AMGD_DMULT);
-  amgd_vals_abs(R);
-  amgd_diag_op(R, Dr, AMGD_MULTD);
+  amgd_diag_op2(R, Dl, Dr, AMGD_SCALE_ABS);          /* |Dl*X|*Dr in one pass */
   return R;
 }
 
@@ -569,8 +565,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
   amgd_vunary(Dcinv, rnc, AMGD_V_INV);
   dcsr *ArD = dcsr_copy(Ar);
   amgd_vals_sqr(ArD);
-  amgd_diag_op(ArD, Dfinv, AMGD_DMULT);
-  amgd_diag_op(ArD, Dcinv, AMGD_MULTD);
+  amgd_diag_op2(ArD, Dfinv, Dcinv, AMGD_SCALE2);
   dcsr *W_skel = amgd_min_skel(ArD);                 /* one strongest C per F row */
   dcsr_free(&ArD);
   double *lam = dzeros(rnf), *alpha = dalloc(cnc);
@@ -772,8 +767,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
       amgd_d2d(Dh, D, (size_t)rnf * 8);
       amgd_vunary(Dh, rnf, AMGD_V_SQRT);
       dcsr *DAD = dcsr_copy(Af);
-      amgd_diag_op(DAD, Dh, AMGD_DMULT);
-      amgd_diag_op(DAD, Dh, AMGD_MULTD);
+      amgd_diag_op2(DAD, Dh, Dh, AMGD_SCALE2);
       double lambda[KMAX + 2];
       uint32_t k = lanczos(DAD, lambda);
       double a = lambda[0], b = lambda[k - 1];

@@ -496,10 +496,66 @@ __global__ void k_diag_op(const uint64_t *ro, const uint32_t *col, double *a, ui
     }
   }
 }
-extern "C" void amgd_diag_op(dcsr *A, const double *D, int op) {
-  if (A->rn) k_diag_op<<<grid_for(A->rn), 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, D, op);
+// G lanes per row (coalesced on long rows).  op: DPLUS / DMINUS touch the first
+// diagonal entry only (diagcsr_op, amg_setup.c:3389); DMULT a*=Dl[i]; MULTD a*=Dl[col];
+// SCALE2 a = (a*Dl[i])*Dr[col]; SCALE_ABS a = |a*Dl[i]|*Dr[col]; SCALE2_ABS a = |(a*Dl[i])*Dr[col]|
+// -- each the reference's sequence of separate passes, fused
+template <int G>
+__global__ __launch_bounds__(256) void k_diag_op_g(const uint64_t *ro, const uint32_t *col,
+                                                   double *a, uint32_t rn, const double *Dl,
+                                                   const double *Dr, int op) {
+  const uint32_t sub = threadIdx.x & (G - 1);
+  const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
+  for (uint64_t i = g0; i < rn; i += gs) {
+    const uint64_t k0 = ro[i], k1 = ro[i + 1];
+    if (op == AMGD_DPLUS || op == AMGD_DMINUS) {
+      uint64_t first = ~0ull;
+      for (uint64_t k = k0 + sub; k < k1; k += G)
+        if (col[k] == i) { first = k; break; }
+#pragma unroll
+      for (int o = G / 2; o > 0; o >>= 1) {
+        unsigned long long u = __shfl_xor((unsigned long long)first, o, 64);
+        first = u < first ? u : first;
+      }
+      if (sub == 0 && first != ~0ull)
+        a[first] = op == AMGD_DPLUS ? a[first] + Dl[i] : a[first] - Dl[i];
+      continue;
+    }
+    const double di = Dl[i];
+    for (uint64_t k = k0 + sub; k < k1; k += G) {
+      double v = a[k];
+      switch (op) {
+        case AMGD_DMULT: v = v * di; break;
+        case AMGD_MULTD: v = v * Dl[col[k]]; break;
+        case AMGD_SCALE2: v = (v * di) * Dr[col[k]]; break;
+        case AMGD_SCALE_ABS: v = fabs(v * di) * Dr[col[k]]; break;
+        default: v = fabs((v * di) * Dr[col[k]]); break;
+      }
+      a[k] = v;
+    }
+  }
+}
+static int row_lanes(uint64_t nnz, uint64_t rn) {
+  uint64_t avg = rn ? (nnz + rn - 1) / rn : 1;
+  int G = 4;
+  while (G < 64 && (uint64_t)G * 2 <= avg) G <<= 1;
+  return G;
+}
+extern "C" void amgd_diag_op2(dcsr *A, const double *Dl, const double *Dr, int op) {
+  if (!A->rn) return;
+  const int G = row_lanes(A->nnz, A->rn);
+  const int gb = grid_for((uint64_t)A->rn * G, 256, 65536);
+  switch (G) {
+    case 4: k_diag_op_g<4><<<gb, 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, Dl, Dr, op); break;
+    case 8: k_diag_op_g<8><<<gb, 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, Dl, Dr, op); break;
+    case 16: k_diag_op_g<16><<<gb, 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, Dl, Dr, op); break;
+    case 32: k_diag_op_g<32><<<gb, 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, Dl, Dr, op); break;
+    default: k_diag_op_g<64><<<gb, 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, Dl, Dr, op); break;
+  }
   KCHECK();
 }
+extern "C" void amgd_diag_op(dcsr *A, const double *D, int op) { amgd_diag_op2(A, D, nullptr, op); }
 __global__ void k_vals(double *a, uint64_t n, int op, double s) {
   GRID_STRIDE(k, n) {
     double v = a[k];
@@ -1218,9 +1274,10 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     }
     amgd_sync();
     double ms = (amgd_wtime() - t_start) * 1e3;
-    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
+    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  %s  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
             rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz,
-            (unsigned long)prods, prods / (ms * 1e6), hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], ms);
+            (unsigned long)prods, prods / (ms * 1e6), kseq ? (wide ? "kseq-w" : "kseq") : "flat",
+            hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], ms);
   }
   return X;
 }
