@@ -88,6 +88,8 @@ def lib() -> C.CDLL:
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+        L.amgd_test_qf_sparse.argtypes = [C.c_int]
+        L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -235,6 +237,19 @@ def test_dot(mode: int, a, b=None, plain: bool = False, exact: bool = True) -> f
 def lmop_mode(mode: int) -> None:
     """interp_lmop path: 0 = row-pull where order-exact (default), 1 = general key/sort walk"""
     lib().amgd_test_lmop_mode(int(mode))
+
+
+def qf_sparse(mode: int) -> None:
+    """huge-support Q factor: 0 dense cooperative, 1 sparse first (default),
+    2 sparse with a capacity too small to finish (exercises the dense fallback)"""
+    lib().amgd_test_qf_sparse(int(mode))
+
+
+def qf_stats() -> dict:
+    """huge supports factored sparse / sent to the dense kernel since the last call"""
+    out = (C.c_uint64 * 2)()
+    lib().amgd_test_qf_stats(out)
+    return {"sparse": int(out[0]), "fallback": int(out[1])}
 
 
 def lmop_stats(reset: bool = True) -> dict:

@@ -287,6 +287,187 @@ __global__ __launch_bounds__(64) void k_qfactor_coop(uint32_t c, const uint64_t 
   }
 }
 
+// huge supports, sparse form.  The orphan support's Gram matrix A(Qj,Qj) is nearly
+// diagonal (orphans are isolated points), so its factor is ~0.5% dense.  A product
+// term that is exactly zero cannot change a sum that starts at +0 (the sum never
+// becomes -0), so each sum of the dense loop equals the sum over its structurally
+// nonzero terms taken in the same order.  One block walks k; U is kept as rows
+// (ascending columns) plus per-column linked lists (ascending rows):
+//   s1 = A(sk, Qj[0..k]) nonzeros                (row of A, positions by bisection)
+//   s2[i], i in rows of U reached from s1's columns   (row dot, ascending j)
+//   qk[i'], i' in columns of the rows with s2 != 0    (column walk, ascending j)
+//   al = s1[k] - sum_m s1[m] qk[m]   (m ascending over s1's nonzeros)
+// The unstored entries of row k are qk*al = +0 * (negative) = -0; the triangle is
+// prefilled with -0.  Any non-finite value, al <= 0 or a capacity overflow sets the
+// status and the support is factored by the dense cooperative kernel instead.
+#define QS_NONE 0xffffffffu
+#define QS_SORT 2048
+struct QsBuf {
+  double *s1, *s2, *qk, *uval;
+  uint32_t *m2, *m3, *L2, *chead, *ctail, *ucol, *urow, *nxt, *rowptr;
+  uint32_t cap;
+  unsigned *status;
+};
+template <int NT>
+__device__ __forceinline__ void lds_sort_u32(uint32_t *x, uint32_t n) {
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < P; i += NT) x[i] = QS_NONE;
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= P; kk <<= 1)
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P; i += NT) {
+        uint32_t l = i ^ j;
+        if (l > i) {
+          uint32_t a = x[i], b = x[l];
+          if ((a > b) == ((i & kk) == 0)) { x[i] = b; x[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+}
+__global__ void k_fill_negzero(double *q, uint64_t n) {
+  GRID_STRIDE(i, n) q[i] = -0.0;
+}
+template <int NT>
+__global__ __launch_bounds__(NT) void k_qfactor_sparse(uint32_t c, const uint64_t *wro,
+                                                       const uint32_t *wcol, const uint64_t *aro,
+                                                       const uint32_t *acol, const double *aa,
+                                                       const uint64_t *qoff, double *Q, QsBuf b) {
+  __shared__ uint32_t L1[QS_SORT], L3[QS_SORT];
+  __shared__ unsigned n1, n2, n3, fail;
+  __shared__ double sh_al;
+  const uint32_t t = threadIdx.x;
+  const uint64_t w0 = wro[c];
+  const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+  const uint32_t *Qj = wcol + w0;
+  double *U = Q + qoff[c];
+  if (t == 0) { fail = 0; b.rowptr[0] = 0; }
+  for (uint32_t k = 0; k < nz; k++) {
+    if (t == 0) { n1 = 0; n2 = 0; n3 = 0; }
+    __syncthreads();
+    // s1: the first match of each support column in row sk (row_lookup), m <= k
+    const uint32_t sk = Qj[k];
+    const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
+    for (uint64_t e = a0 + t; e < a1; e += NT) {
+      const uint32_t j = acol[e];
+      if (e > a0 && acol[e - 1] == j) continue;
+      uint32_t lo = 0, hi = k + 1;
+      while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (Qj[mid] < j) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo <= k && Qj[lo] == j) {
+        const double v = aa[e];
+        if (v != 0.0) {
+          if (!isfinite(v)) fail = 1;
+          b.s1[lo] = v;
+          unsigned p = atomicAdd(&n1, 1u);
+          if (p < QS_SORT) L1[p] = lo;
+          else fail = 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (fail) break;
+    const uint32_t N1 = n1;
+    lds_sort_u32<NT>(L1, N1);
+    // rows i < k with a stored U[i][j], j in s1's columns
+    for (uint32_t q = t; q < N1; q += NT) {
+      const uint32_t j = L1[q];
+      if (j >= k) continue;
+      for (uint32_t e = b.chead[j]; e != QS_NONE; e = b.nxt[e]) {
+        const uint32_t i = b.urow[e];
+        if (atomicExch(&b.m2[i], 1u) == 0u) b.L2[atomicAdd(&n2, 1u)] = i;
+      }
+    }
+    __syncthreads();
+    const uint32_t N2 = n2;
+    for (uint32_t q = t; q < N2; q += NT) {         // s2[i] = sum_j U[i][j] s1[j]
+      const uint32_t i = b.L2[q];
+      double v = 0;
+      for (uint32_t e = b.rowptr[i]; e < b.rowptr[i + 1]; e++) v += b.uval[e] * b.s1[b.ucol[e]];
+      b.s2[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t q = t; q < N2; q += NT) {         // qk's candidate columns
+      const uint32_t i = b.L2[q];
+      if (b.s2[i] == 0.0) continue;
+      for (uint32_t e = b.rowptr[i]; e < b.rowptr[i + 1]; e++) {
+        const uint32_t i2 = b.ucol[e];
+        if (atomicExch(&b.m3[i2], 1u) == 0u) {
+          unsigned p = atomicAdd(&n3, 1u);
+          if (p < QS_SORT) L3[p] = i2;
+          else fail = 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (fail) break;
+    const uint32_t N3 = n3;
+    lds_sort_u32<NT>(L3, N3);
+    for (uint32_t q = t; q < N3; q += NT) {         // qk[i'] = sum_j U[j][i'] s2[j]
+      const uint32_t i2 = L3[q];
+      double y = 0;
+      for (uint32_t e = b.chead[i2]; e != QS_NONE; e = b.nxt[e]) y += b.uval[e] * b.s2[b.urow[e]];
+      b.qk[i2] = y;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double al = b.s1[k];
+      for (uint32_t q = 0; q < N1; q++) {
+        const uint32_t m = L1[q];
+        if (m < k) al -= b.s1[m] * b.qk[m];
+      }
+      if (!(al > 0.0) || !isfinite(al)) fail = 1;
+      sh_al = -1.0 / sqrt(al);
+      if (b.rowptr[k] + N3 + 1 > b.cap) fail = 1;
+    }
+    __syncthreads();
+    if (fail) break;
+    const double al = sh_al;
+    const uint32_t base = b.rowptr[k];
+    double *out = U + tri(k);
+    for (uint32_t q = t; q < N3; q += NT) {         // row k, ascending columns
+      const uint32_t i2 = L3[q], e = base + q;
+      const double v = b.qk[i2] * al;
+      if (!isfinite(v)) fail = 1;
+      out[i2] = v;
+      b.ucol[e] = i2;
+      b.urow[e] = k;
+      b.uval[e] = v;
+      b.nxt[e] = QS_NONE;
+      const uint32_t tl = b.ctail[i2];
+      if (tl == QS_NONE) b.chead[i2] = e;
+      else b.nxt[tl] = e;
+      b.ctail[i2] = e;
+      b.m3[i2] = 0;
+      b.qk[i2] = 0.0;
+    }
+    if (t == 0) {
+      const uint32_t e = base + N3;
+      out[k] = -al;
+      b.ucol[e] = k;
+      b.urow[e] = k;
+      b.uval[e] = -al;
+      b.nxt[e] = QS_NONE;
+      b.chead[k] = e;
+      b.ctail[k] = e;
+      b.rowptr[k + 1] = e + 1;
+    }
+    for (uint32_t q = t; q < N1; q += NT) b.s1[L1[q]] = 0.0;
+    for (uint32_t q = t; q < N2; q += NT) {
+      const uint32_t i = b.L2[q];
+      b.m2[i] = 0;
+      b.s2[i] = 0.0;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (t == 0) *b.status = fail;
+}
+
 __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
   GRID_STRIDE(c, rn) {
     uint64_t nz = wro[c + 1] - wro[c];
@@ -347,6 +528,21 @@ static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
 }
 static void free_split(RowSplit &rs) { amgd_free(rs.sl); }
 
+static int g_qf_sparse = -1;   // 0: dense cooperative only, 1: sparse first, 2: tiny capacity
+static int qf_sparse_mode() {
+  if (g_qf_sparse < 0) {
+    const char *e = getenv("AMGD_QF_SPARSE");
+    g_qf_sparse = e ? atoi(e) : 1;
+  }
+  return g_qf_sparse;
+}
+static unsigned long g_qf_stats[2];   // huge supports factored sparse / sent to the dense kernel
+extern "C" void amgd_qfactor_set_sparse(int m) { g_qf_sparse = m; }
+extern "C" void amgd_qfactor_stats(unsigned long *st) {
+  st[0] = g_qf_stats[0];
+  st[1] = g_qf_stats[1];
+  g_qf_stats[0] = g_qf_stats[1] = 0;
+}
 #define QF_T0 32
 #define QF_T1 64
 #define QF_T2 128
@@ -380,41 +576,83 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   static hipStream_t s2 = nullptr;
   static hipEvent_t ev2 = nullptr;
   std::vector<void *> coop_bufs;
+  std::vector<uint32_t> big, bignz;
+  std::vector<unsigned *> bigstat;
+  auto launch_coop = [&](uint32_t c, uint32_t nz) {
+    double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
+    double *s2v = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
+    unsigned *bar = (unsigned *)amgd_alloc(16);
+    HIPCK(hipMemsetAsync(bar, 0, 16, s2));
+    coop_bufs.push_back(s1b);
+    coop_bufs.push_back(bar);
+    int G = (int)std::min<uint32_t>((nz + 63) / 64, 256u);
+    const uint64_t *pwro = Wt->ro, *paro = A->ro, *pqoff = qoff;
+    const uint32_t *pwcol = Wt->col, *pacol = A->col;
+    const double *paa = A->a;
+    void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2v, &qk, &bar};
+    static bool attr = false;
+    if (!attr) {
+      HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
+      attr = true;
+    }
+    HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
+                                     (unsigned)(2 * (size_t)nz * 8), s2));
+    KCHECK();
+  };
   if (hn[4]) {
     if (!s2) {
       HIPCK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
       HIPCK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
     }
-    std::vector<uint32_t> big(hn[4]);
+    big.resize(hn[4]);
     amgd_d2h(big.data(), lists + 4 * L, (size_t)hn[4] * 4);
-    std::vector<uint64_t> ro(rn + 1);
+    std::vector<uint64_t> ro(rn + 1), qo(rn + 1);
     amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
+    amgd_d2h(qo.data(), qoff, (size_t)(rn + 1) * 8);
+    const int sp = qf_sparse_mode();
     for (uint32_t c : big) {
       uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
       if (nz > QF_COOP_MAX) {
         fprintf(stderr, "omp_amg_amd: support of %u points exceeds QF_COOP_MAX\n", nz);
         abort();
       }
-      double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
-      double *s2v = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
-      unsigned *bar = (unsigned *)amgd_alloc(16);
-      HIPCK(hipMemsetAsync(bar, 0, 16, s2));
-      coop_bufs.push_back(s1b);
-      coop_bufs.push_back(bar);
-      int G = (int)std::min<uint32_t>((nz + 63) / 64, 256u);
-      const uint64_t *pwro = Wt->ro, *paro = A->ro, *pqoff = qoff;
-      const uint32_t *pwcol = Wt->col, *pacol = A->col;
-      const double *paa = A->a;
-      void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2v, &qk, &bar};
-      static bool attr = false;
-      if (!attr) {
-        HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
-        attr = true;
+      bignz.push_back(nz);
+      if (!sp) {
+        bigstat.push_back(nullptr);
+        launch_coop(c, nz);
+        continue;
       }
-      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
-                                       (unsigned)(2 * (size_t)nz * 8), s2));
+      // sparse attempt; the dense kernel runs after the tiers if it reports failure
+      const uint64_t tn = (uint64_t)nz * (nz + 1) / 2;
+      const uint32_t cap = sp == 2 ? nz + 8 : (uint32_t)std::min<uint64_t>(tn, 1u << 24);
+      const size_t nd = (size_t)nz * 3 + cap, nu = (size_t)nz * 6 + (size_t)cap * 3 + 2;
+      char *mem = (char *)amgd_alloc(nd * 8 + nu * 4 + 64);
+      coop_bufs.push_back(mem);
+      QsBuf qb;
+      qb.s1 = (double *)mem;
+      qb.s2 = qb.s1 + nz;
+      qb.qk = qb.s2 + nz;
+      qb.uval = qb.qk + nz;
+      uint32_t *u = (uint32_t *)(qb.uval + cap);
+      qb.m2 = u;
+      qb.m3 = u + nz;
+      qb.L2 = u + 2 * (size_t)nz;
+      qb.chead = u + 3 * (size_t)nz;
+      qb.ctail = u + 4 * (size_t)nz;
+      qb.rowptr = u + 5 * (size_t)nz;               // nz + 1
+      qb.ucol = u + 6 * (size_t)nz + 1;
+      qb.urow = qb.ucol + cap;
+      qb.nxt = qb.urow + cap;
+      qb.status = qb.nxt + cap;
+      qb.cap = cap;
+      HIPCK(hipMemsetAsync(mem, 0, (size_t)nz * 3 * 8, s2));
+      HIPCK(hipMemsetAsync(qb.m2, 0, (size_t)nz * 3 * 4, s2));
+      HIPCK(hipMemsetAsync(qb.chead, 0xff, (size_t)nz * 2 * 4, s2));
+      k_fill_negzero<<<grid_for(tn), 256, 0, s2>>>(Q + qo[c], tn);
+      k_qfactor_sparse<256><<<1, 256, 0, s2>>>(c, Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q, qb);
       KCHECK();
+      bigstat.push_back(qb.status);
     }
     HIPCK(hipEventRecord(ev2, s2));
   }
@@ -434,14 +672,28 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
         lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   KCHECK();
   if (hn[4]) {                    // the library stream waits for the side stream
+    bool redo = false;
+    for (size_t q = 0; q < big.size(); q++) {
+      if (!bigstat[q]) continue;
+      unsigned st = 0;
+      HIPCK(hipMemcpyAsync(&st, bigstat[q], 4, hipMemcpyDeviceToHost, s2));
+      HIPCK(hipStreamSynchronize(s2));
+      if (st) {                     // dense cooperative factor (overwrites the triangle)
+        amgd_sync();                // scratch reuse is ordered after the library stream
+        launch_coop(big[q], bignz[q]);
+        redo = true;
+      }
+      g_qf_stats[st ? 1 : 0]++;
+    }
+    if (redo) HIPCK(hipEventRecord(ev2, s2));
     HIPCK(hipStreamWaitEvent(s, ev2, 0));
     for (void *p : coop_bufs) amgd_free(p);   // reuse is ordered after the wait
   }
   if (sglog) {
     amgd_sync();
-    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u/%u Q %lu  %.2f ms\n", rn,
-            (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], hn[4], (unsigned long)tot,
-            (amgd_wtime() - t_start) * 1e3);
+    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u/%u (huge nz %u) Q %lu  %.2f ms\n",
+            rn, (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], hn[4],
+            bignz.empty() ? 0u : bignz[0], (unsigned long)tot, (amgd_wtime() - t_start) * 1e3);
   }
   amgd_free(lists); amgd_free(cnt);
   *qoff_out = qoff;

@@ -140,6 +140,16 @@ API void amgd_test_lmop_stats(uint64_t *out, int reset) {
   if (reset) amgd_lmop_stats_reset();
 }
 
+/* huge-support Q factor: mode (0 dense, 1 sparse first, 2 sparse with a tiny
+   capacity, which forces the dense fallback) and [sparse, fallback] counters */
+API void amgd_test_qf_sparse(int m) { amgd_qfactor_set_sparse(m); }
+API void amgd_test_qf_stats(uint64_t *out) {
+  unsigned long st[2];
+  amgd_qfactor_stats(st);
+  out[0] = st[0];
+  out[1] = st[1];
+}
+
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
 extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }

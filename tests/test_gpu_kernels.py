@@ -276,9 +276,7 @@ def _oracle_qfactor(W, A):
     return Q[:-1]
 
 
-def test_qfactor_tiers_bitexact():
-    """Q factors for supports in every tier (LDS 32 / 64 / 128 / block / cooperative
-    grid) against the oracle's restatement of interp's Q loop, bit for bit"""
+def _qfactor_case(structure):
     from omp_amg_amd import problems
     m = 20
     Ai, Aj, Av = problems.poisson3d(m, 27)
@@ -286,17 +284,50 @@ def test_qfactor_tiers_bitexact():
     aro, acol, aa = problems.coo_to_csr_np(np.asarray(Ai)[o], np.asarray(Aj)[o], np.asarray(Av)[o])
     A = refops.Csr(m ** 3, m ** 3, aro, acol, aa)
     rng = np.random.default_rng(21)
-    sizes = [1, 5, 31, 32, 33, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
     ro, cols = [0], []
-    for nz in sizes:
-        lo = int(rng.integers(0, m ** 3 - 3 * nz))
-        c = np.sort(rng.choice(np.arange(lo, lo + 3 * nz), size=nz, replace=False))
-        cols.extend(c.tolist())
-        ro.append(len(cols))
+    if structure == "tiers":
+        sizes = [1, 5, 31, 32, 33, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
+        for nz in sizes:
+            lo = int(rng.integers(0, m ** 3 - 3 * nz))
+            c = np.sort(rng.choice(np.arange(lo, lo + 3 * nz), size=nz, replace=False))
+            cols.extend(c.tolist())
+            ro.append(len(cols))
+    else:                                      # huge supports only
+        if structure == "scattered":           # isolated points: a diagonal Gram matrix
+            c = np.sort(rng.choice(np.arange(0, m ** 3, 7), size=1100, replace=False))
+            cols.extend(c.tolist()); ro.append(len(cols))
+        c = np.arange(2000, 3300)              # a contiguous block: fill-in
+        cols.extend(c.tolist()); ro.append(len(cols))
+        c = np.sort(rng.choice(np.arange(m ** 3), size=1500, replace=False))
+        cols.extend(c.tolist()); ro.append(len(cols))
     ro.append(len(cols))                      # one empty support
-    W = refops.Csr(len(sizes) + 1, m ** 3, np.array(ro), np.array(cols, dtype=np.int64),
+    W = refops.Csr(len(ro) - 1, m ** 3, np.array(ro), np.array(cols, dtype=np.int64),
                    np.ones(len(cols)))
-    X = oa.test_csr_op(5, W, A)
+    return W, A
+
+
+@pytest.mark.parametrize("structure,mode", [("tiers", 1), ("tiers", 0), ("scattered", 1),
+                                            ("scattered", 2), ("scattered", 0)])
+def test_qfactor_tiers_bitexact(structure, mode):
+    """Q factors for supports in every tier (LDS 32 / 64 / 128 / block / huge) against
+    the oracle's restatement of interp's Q loop, bit for bit.  Huge supports run the
+    sparse kernel (mode 1), the dense cooperative kernel (mode 0), or the sparse
+    kernel with a capacity too small to finish, which must hand over to the dense one"""
+    W, A = _qfactor_case(structure)
+    oa.qf_sparse(mode)
+    oa.qf_stats()
+    try:
+        X = oa.test_csr_op(5, W, A)
+    finally:
+        oa.qf_sparse(1)
+    st = oa.qf_stats()
+    nhuge = int((np.diff(W.row_off) > 1024).sum())
+    if mode == 0:
+        assert st == {"sparse": 0, "fallback": 0}
+    elif mode == 2:
+        assert st == {"sparse": 0, "fallback": nhuge}
+    else:
+        assert st["sparse"] + st["fallback"] == nhuge and st["sparse"] > 0, st
     ref = _oracle_qfactor(W, A)
     assert X.nnz == len(ref)
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
