@@ -80,54 +80,123 @@ extern "C" dcsr *amgd_min_skel(const dcsr *R) {
 // ---------------------------------------------------------------------------
 #define QF_LDS_NZ 512
 
-template <int NZMAX>
-__global__ __launch_bounds__(64) void k_qfactor_lds(const uint32_t *rows, uint32_t nrows,
+// s1[m] = A(sk, Qj[m]) for m <= k (row_lookup's first match), by one coalesced pass over
+// row sk with each column located in the support by bisection in the LDS copy Qs of Qj
+// (k+1 bisections of the A row would be chains of dependent HBM loads).  Callers sync.
+template <int NT>
+__device__ __forceinline__ void gather_s1(double *s1, const uint32_t *Qs, uint32_t k,
+                                          const uint32_t *acol, const double *aa, uint64_t a0,
+                                          uint64_t a1) {
+  const uint32_t t = threadIdx.x;
+  // cost model in LDS-latency units (an HBM load ~ 4): scan = rounds over the row x
+  // (load + bisection in Qs), lookup = rounds over m x a bisection of dependent loads
+  const uint32_t len = (uint32_t)(a1 - a0);
+  const uint32_t lg_len = 32 - __clz(len | 1), lg_k = 32 - __clz(k + 1);
+  const uint32_t scan = ((len + NT - 1) / NT) * (4 + lg_k);
+  const uint32_t look = ((k + NT) / NT) * lg_len * 4;
+  if (look < scan) {
+    for (uint32_t m = t; m <= k; m += NT) s1[m] = row_lookup(acol, aa, a0, a1, Qs[m]);
+    return;
+  }
+  for (uint32_t m = t; m <= k; m += NT) s1[m] = 0.0;
+  __syncthreads();
+  for (uint64_t e = a0 + t; e < a1; e += NT) {
+    const uint32_t j = acol[e];
+    if (e > a0 && acol[e - 1] == j) continue;
+    uint32_t lo = 0, hi = k + 1;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (Qs[mid] < j) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo <= k && Qs[lo] == j) s1[lo] = aa[e];
+  }
+}
+
+// LDS-resident triangle.  Every dot is one ordered chain; the LDS reads of a chain
+// are issued LB at a time ahead of its adds (a read -> mul -> add chain per element
+// would pay the LDS latency on every term).  Reads past a chain's end stay inside
+// the padded arrays and their terms are not added.
+#define LB 8
+template <int NZMAX, int NT>
+__global__ __launch_bounds__(NT) void k_qfactor_lds(const uint32_t *rows, uint32_t nrows,
                                                     const uint64_t *wro, const uint32_t *wcol,
                                                     const uint64_t *aro, const uint32_t *acol,
                                                     const double *aa, const uint64_t *qoff,
                                                     double *Q) {
-  __shared__ double U[NZMAX * (NZMAX + 1) / 2];
-  __shared__ double s1[NZMAX], s2[NZMAX], qk[NZMAX];
+  constexpr uint32_t TN = NZMAX * (NZMAX + 1) / 2;
+  __shared__ double U[TN + NZMAX + LB];
+  __shared__ double s1[NZMAX + LB], s2[NZMAX + LB], qk[NZMAX + LB];
+  __shared__ uint32_t Qs[NZMAX];
   __shared__ double sh_al;
   const int t = threadIdx.x;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t c = rows[r];
     const uint64_t w0 = wro[c];
     const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
-    const uint32_t *Qj = wcol + w0;
+    for (uint32_t m = t; m < nz; m += NT) Qs[m] = wcol[w0 + m];
+    __syncthreads();
     for (uint32_t k = 0; k < nz; k++) {
-      const uint32_t sk = Qj[k];
-      const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
-      for (uint32_t m = t; m <= k; m += 64) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+      const uint32_t sk = Qs[k];
+      gather_s1<NT>(s1, Qs, k, acol, aa, aro[sk], aro[sk + 1]);
       __syncthreads();
-      for (uint32_t i = t; i < k; i += 64) {
+      for (uint32_t i = t; i < k; i += NT) {          // s2[i] = sum_{j<=i} U[i][j] s1[j]
         const double *Ui = U + tri(i);
         double v = 0;
-        for (uint32_t j = 0; j <= i; j++) v += Ui[j] * s1[j];
+        for (uint32_t j0 = 0; j0 <= i; j0 += LB) {
+          double u[LB], x[LB];
+#pragma unroll
+          for (int q = 0; q < LB; q++) { u[q] = Ui[j0 + q]; x[q] = s1[j0 + q]; }
+#pragma unroll
+          for (int q = 0; q < LB; q++)
+            if (j0 + q <= i) v += u[q] * x[q];
+        }
         s2[i] = v;
       }
       __syncthreads();
-      for (uint32_t i = t; i < k; i += 64) {
+      for (uint32_t i = t; i < k; i += NT) {          // qk[i] = sum_{j=i}^{k-1} U[j][i] s2[j]
         double y = 0;
-        for (uint32_t j = i; j < k; j++) y += U[tri(j) + i] * s2[j];
+        uint32_t off = (uint32_t)tri(i) + i;          // U[i][i]
+        for (uint32_t j0 = i; j0 < k; j0 += LB) {
+          double u[LB], x[LB];
+          uint32_t o = off;
+#pragma unroll
+          for (int q = 0; q < LB; q++) {
+            const uint32_t j = j0 + q;
+            u[q] = U[j < k ? o : 0];
+            x[q] = s2[j];
+            o += j + 1;
+          }
+#pragma unroll
+          for (int q = 0; q < LB; q++)
+            if (j0 + q < k) y += u[q] * x[q];
+          off = o;
+        }
         qk[i] = y;
       }
       __syncthreads();
       if (t == 0) {
         double al = s1[k];
-        for (uint32_t m = 0; m < k; m++) al -= s1[m] * qk[m];
+        for (uint32_t m0 = 0; m0 < k; m0 += LB) {
+          double x[LB], y[LB];
+#pragma unroll
+          for (int q = 0; q < LB; q++) { x[q] = s1[m0 + q]; y[q] = qk[m0 + q]; }
+#pragma unroll
+          for (int q = 0; q < LB; q++)
+            if (m0 + q < k) al -= x[q] * y[q];
+        }
         sh_al = -1.0 / sqrt(al);
       }
       __syncthreads();
       const double al = sh_al;
       double *out = U + tri(k);
-      for (uint32_t i = t; i < k; i += 64) out[i] = qk[i] * al;
+      for (uint32_t i = t; i < k; i += NT) out[i] = qk[i] * al;
       if (t == 0) out[k] = -al;
       __syncthreads();
     }
     double *Qc = Q + qoff[c];
     const uint32_t tn = nz * (nz + 1) / 2;
-    for (uint32_t e = t; e < tn; e += 64) Qc[e] = U[e];
+    for (uint32_t e = t; e < tn; e += NT) Qc[e] = U[e];
     __syncthreads();
   }
 }
@@ -174,18 +243,19 @@ __global__ __launch_bounds__(256) void k_qfactor_mid(const uint32_t *rows, uint3
                                                      const double *aa, const uint64_t *qoff,
                                                      double *Q) {
   __shared__ double s1[1024], s2[1024], qk[1024];
+  __shared__ uint32_t Qs[1024];
   __shared__ double sh_al;
   const int t = threadIdx.x, lane = t & 63;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t c = rows[r];
     const uint64_t w0 = wro[c];
     const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
-    const uint32_t *Qj = wcol + w0;
+    for (uint32_t m = t; m < nz; m += 256) Qs[m] = wcol[w0 + m];
     double *U = Q + qoff[c];
+    __syncthreads();
     for (uint32_t k = 0; k < nz; k++) {
-      const uint32_t sk = Qj[k];
-      const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
-      for (uint32_t m = t; m <= k; m += 256) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
+      const uint32_t sk = Qs[k];
+      gather_s1<256>(s1, Qs, k, acol, aa, aro[sk], aro[sk + 1]);
       __syncthreads();
       for (uint32_t i = t; i < k; i += 256) s2[i] = seq_dot_batched(U + tri(i), s1, i + 1);
       __syncthreads();
@@ -206,6 +276,164 @@ __global__ __launch_bounds__(256) void k_qfactor_mid(const uint32_t *rows, uint3
       for (uint32_t i = t; i < k; i += 256) out[i] = qk[i] * al;
       if (t == 0) out[k] = -al;
       __syncthreads();
+    }
+  }
+}
+
+// mid supports, blocked over B consecutive k-steps.  The rows s1_k (k in [k0, k0+B))
+// are rows of A, known in advance, so one pass over the finished rows i < k0 yields
+// s2_k[i] for all B steps (B ordered chains per lane, each U element read once for
+// B terms), and one pass over their columns yields the prefix j < k0 of every
+// qk_k[i] chain; each chain is then continued in order over j in [k0, k) as the
+// block's rows are produced.  The row produced at step k (U[k][j] = qk[j] al) feeds
+// s2_{k'}[k] of the later steps of the block on lanes of wave 0.  U is read twice per
+// B steps instead of twice per step; every sum keeps the reference's order.
+#define QB2 16
+template <int NZMAX, int B, int NTT = 256>
+__global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint32_t nrows,
+                                                     const uint64_t *wro, const uint32_t *wcol,
+                                                     const uint64_t *aro, const uint32_t *acol,
+                                                     const double *aa, const uint64_t *qoff,
+                                                     double *Q) {
+  constexpr uint32_t NT = NTT, RPT = (NZMAX + NT - 1) / NT, PAD = NZMAX + 16;
+  __shared__ uint32_t Qs[NZMAX];
+  __shared__ double S1[B * PAD], S2[B * PAD], qk[PAD];
+  __shared__ double sh_al;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t c = rows[r];
+    const uint64_t w0 = wro[c];
+    const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    for (uint32_t m = t; m < nz; m += NT) Qs[m] = wcol[w0 + m];
+    double *U = Q + qoff[c];
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < nz; k0 += B) {
+      const uint32_t bn = min((uint32_t)B, nz - k0);
+      // s1 rows of the block (zero, then scatter or look up)
+      for (uint32_t b = 0; b < bn; b++)
+        for (uint32_t m = t; m <= k0 + b; m += NT) S1[b * PAD + m] = 0.0;
+      __syncthreads();
+      for (uint32_t b = 0; b < bn; b++) {
+        const uint32_t k = k0 + b, sk = Qs[k];
+        const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
+        const uint32_t len = (uint32_t)(a1 - a0);
+        const uint32_t lg_len = 32 - __clz(len | 1), lg_k = 32 - __clz(k + 1);
+        if (((k + NT) / NT) * lg_len * 4 < ((len + NT - 1) / NT) * (4 + lg_k)) {
+          for (uint32_t m = t; m <= k; m += NT)
+            S1[b * PAD + m] = row_lookup(acol, aa, a0, a1, Qs[m]);
+        } else {
+          for (uint64_t e = a0 + t; e < a1; e += NT) {
+            const uint32_t j = acol[e];
+            if (e > a0 && acol[e - 1] == j) continue;
+            uint32_t lo = 0, hi = k + 1;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (Qs[mid] < j) lo = mid + 1;
+              else hi = mid;
+            }
+            if (lo <= k && Qs[lo] == j) S1[b * PAD + lo] = aa[e];
+          }
+        }
+      }
+      __syncthreads();
+      // s2_k[i], i < k0, for every step of the block: one pass over rows i
+      for (uint32_t i = t; i < k0; i += NT) {
+        double acc[B];
+#pragma unroll
+        for (int b = 0; b < B; b++) acc[b] = 0.0;
+        const double *Ui = U + tri(i);
+        for (uint32_t j0 = 0; j0 <= i; j0 += QB2) {
+          double u[QB2];
+#pragma unroll
+          for (int q = 0; q < QB2; q++) u[q] = (j0 + q <= i) ? Ui[j0 + q] : 0.0;
+#pragma unroll
+          for (int q = 0; q < QB2; q++)
+            if (j0 + q <= i) {
+#pragma unroll
+              for (int b = 0; b < B; b++) acc[b] += u[q] * S1[b * PAD + j0 + q];
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; b++)
+          if ((uint32_t)b < bn) S2[b * PAD + i] = acc[b];
+      }
+      __syncthreads();
+      // prefix j < k0 of qk_k[i] for every step: one pass over columns i < k0, the
+      // lanes of a wave walking j in lock-step (each load one row segment)
+      double part[RPT][B];
+#pragma unroll
+      for (uint32_t rr = 0; rr < RPT; rr++) {
+        const uint32_t ib = (t - lane) + rr * NT, i = ib + lane;
+#pragma unroll
+        for (int b = 0; b < B; b++) part[rr][b] = 0.0;
+        for (uint32_t j0 = ib; j0 < k0; j0 += QB2) {
+          double u[QB2];
+#pragma unroll
+          for (int q = 0; q < QB2; q++) {
+            const uint32_t j = j0 + q;
+            u[q] = (j < k0 && j >= i) ? U[tri(j) + i] : 0.0;
+          }
+#pragma unroll
+          for (int q = 0; q < QB2; q++) {
+            const uint32_t j = j0 + q;
+            if (j < k0 && j >= i) {
+#pragma unroll
+              for (int b = 0; b < B; b++) part[rr][b] += u[q] * S2[b * PAD + j];
+            }
+          }
+        }
+      }
+      // the steps of the block
+#pragma unroll
+      for (int b = 0; b < B; b++) {
+        if ((uint32_t)b < bn) {
+          const uint32_t k = k0 + b;
+#pragma unroll
+          for (uint32_t rr = 0; rr < RPT; rr++) {
+            const uint32_t i = t + rr * NT;
+            if (i < k) {
+              double y = i < k0 ? part[rr][b] : 0.0;
+              for (uint32_t j = max(i, k0); j < k; j++) y += U[tri(j) + i] * S2[b * PAD + j];
+              qk[i] = y;
+            }
+          }
+          __syncthreads();
+          if (t == 0) {
+            const double *s1 = S1 + b * PAD;
+            double al = s1[k];
+            for (uint32_t m0 = 0; m0 < k; m0 += LB) {
+              double x[LB], y[LB];
+#pragma unroll
+              for (int q = 0; q < LB; q++) { x[q] = s1[m0 + q]; y[q] = qk[m0 + q]; }
+#pragma unroll
+              for (int q = 0; q < LB; q++)
+                if (m0 + q < k) al -= x[q] * y[q];
+            }
+            sh_al = -1.0 / sqrt(al);
+          }
+          __syncthreads();
+          const double al = sh_al;
+          double *out = U + tri(k);
+          for (uint32_t i = t; i < k; i += NT) out[i] = qk[i] * al;
+          if (t == 0) out[k] = -al;
+          // s2_{k'}[k] for the later steps k' of the block, one chain per lane of wave 0
+          if (t < bn - 1 - b) {
+            const double *s1 = S1 + (b + 1 + t) * PAD;
+            double v = 0;
+            for (uint32_t j0 = 0; j0 < k; j0 += LB) {
+              double x[LB], y[LB];
+#pragma unroll
+              for (int q = 0; q < LB; q++) { x[q] = qk[j0 + q]; y[q] = s1[j0 + q]; }
+#pragma unroll
+              for (int q = 0; q < LB; q++)
+                if (j0 + q < k) v += (x[q] * al) * y[q];
+            }
+            v += (-al) * s1[k];
+            S2[(b + 1 + t) * PAD + k] = v;
+          }
+          __syncthreads();
+        }
+      }
     }
   }
 }
@@ -475,9 +703,11 @@ __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
   }
 }
 // columns binned by support size nz (empty supports skipped) against lim[0..nb-2]
-__global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, uint32_t l0, uint32_t l1, uint32_t l2,
-                         uint32_t l3, int nb, uint32_t *lists, unsigned *cnt) {
-  const uint32_t lim[4] = {l0, l1, l2, l3};
+struct BinLim {
+  uint32_t l[7];
+};
+__global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, BinLim lim, int nb, uint32_t *lists,
+                         unsigned *cnt) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (rn + stride - 1) / stride;
@@ -486,7 +716,7 @@ __global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, uint32_t l0, uint32_t
     uint64_t nz = c < rn ? wro[c + 1] - wro[c] : 0;
     int bin = nb - 1;
     for (int q = nb - 2; q >= 0; q--)
-      if (nz <= lim[q]) bin = q;
+      if (nz <= lim.l[q]) bin = q;
     for (int q = 0; q < nb; q++) {
       bool take = nz != 0 && bin == q;
       unsigned p = wave_append(&cnt[q], take);
@@ -513,7 +743,7 @@ static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
   if (Wt->rn) {
-    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, cap, 0, 0, 0, 2, rs.sl, cnt);
+    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, BinLim{{cap}}, 2, rs.sl, cnt);
     k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 4));
   }
   unsigned h[8];
@@ -535,6 +765,14 @@ static int qf_sparse_mode() {
     g_qf_sparse = e ? atoi(e) : 1;
   }
   return g_qf_sparse;
+}
+static int qf_blocked() {
+  static int b = -1;
+  if (b < 0) {
+    const char *e = getenv("AMGD_QF_BLOCKED");
+    b = e ? atoi(e) : 1;
+  }
+  return b;
 }
 static unsigned long g_qf_stats[2];   // huge supports factored sparse / sent to the dense kernel
 extern "C" void amgd_qfactor_set_sparse(int m) { g_qf_sparse = m; }
@@ -560,14 +798,17 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
   uint64_t tot = amgd_scan_u64(qoff, rn);
   double *Q = (double *)amgd_alloc(tot * 8 + 8);
-  uint32_t *lists = (uint32_t *)amgd_alloc(5 * L * 4);
+  // bins: LDS 32 / 64 / 128, blocked 256 / 512 / 1024, huge
+  constexpr int NB = 7, HUGE = 6;
+  uint32_t *lists = (uint32_t *)amgd_alloc(NB * L * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
-  unsigned hn[5] = {0, 0, 0, 0, 0};
+  unsigned hn[NB] = {0, 0, 0, 0, 0, 0, 0};
   if (rn) {
-    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, QF_T0, QF_T1, QF_T2, QF_T3, 5, lists, cnt);
+    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, BinLim{{QF_T0, QF_T1, QF_T2, 256, 512, QF_T3}},
+                                         NB, lists, cnt);
     KCHECK();
-    amgd_d2h(hn, cnt, 20);
+    amgd_d2h(hn, cnt, NB * 4);
   }
   // Huge supports (the orphan support gathered at coarse point 0): one cooperative
   // launch each on a side stream, issued before the other tiers so that its
@@ -600,13 +841,13 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
                                      (unsigned)(2 * (size_t)nz * 8), s2));
     KCHECK();
   };
-  if (hn[4]) {
+  if (hn[HUGE]) {
     if (!s2) {
       HIPCK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
       HIPCK(hipEventCreateWithFlags(&ev2, hipEventDisableTiming));
     }
-    big.resize(hn[4]);
-    amgd_d2h(big.data(), lists + 4 * L, (size_t)hn[4] * 4);
+    big.resize(hn[HUGE]);
+    amgd_d2h(big.data(), lists + HUGE * L, (size_t)hn[HUGE] * 4);
     std::vector<uint64_t> ro(rn + 1), qo(rn + 1);
     amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
     amgd_d2h(qo.data(), qoff, (size_t)(rn + 1) * 8);
@@ -658,20 +899,44 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   }
   // tiers by support size: the LDS triangle sized to the tier keeps small supports at
   // high occupancy (nz <= 32: 4 KB per wavefront)
-  if (hn[0])
-    k_qfactor_lds<QF_T0><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
+  static int t2blk = -1;
+  if (t2blk < 0) t2blk = getenv("AMGD_QF_T2BLK") ? atoi(getenv("AMGD_QF_T2BLK")) : 3;
+  if (hn[0] && (t2blk & 4))
+    k_qfactor_blk<QF_T0, 8, 64><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
         lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[1])
-    k_qfactor_lds<QF_T1><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
+  else if (hn[0])
+    k_qfactor_lds<QF_T0, 64><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
+        lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (hn[1] && (t2blk & 2))
+    k_qfactor_blk<QF_T1, 8, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
         lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[2])
-    k_qfactor_lds<QF_T2><<<(int)std::min<unsigned>(hn[2], 65536u), 64, 0, s>>>(
+  else if (hn[1])
+    k_qfactor_lds<QF_T1, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
+        lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (hn[2] && (t2blk & 1))
+    k_qfactor_blk<QF_T2, 8, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
         lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[3])
-    k_qfactor_mid<<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
-        lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  else if (hn[2])
+    k_qfactor_lds<QF_T2, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
+        lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  if (qf_blocked()) {
+    if (hn[3])
+      k_qfactor_blk<256, 8><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
+          lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+    if (hn[4])
+      k_qfactor_blk<512, 8><<<(int)std::min<unsigned>(hn[4], 8192u), 256, 0, s>>>(
+          lists + 4 * L, hn[4], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+    if (hn[5])
+      k_qfactor_blk<QF_T3, 4><<<(int)std::min<unsigned>(hn[5], 8192u), 256, 0, s>>>(
+          lists + 5 * L, hn[5], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  } else {
+    for (int q = 3; q < 6; q++)
+      if (hn[q])
+        k_qfactor_mid<<<(int)std::min<unsigned>(hn[q], 8192u), 256, 0, s>>>(
+            lists + q * L, hn[q], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  }
   KCHECK();
-  if (hn[4]) {                    // the library stream waits for the side stream
+  if (hn[HUGE]) {                 // the library stream waits for the side stream
     bool redo = false;
     for (size_t q = 0; q < big.size(); q++) {
       if (!bigstat[q]) continue;
@@ -691,8 +956,8 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   }
   if (sglog) {
     amgd_sync();
-    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u/%u (huge nz %u) Q %lu  %.2f ms\n",
-            rn, (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], hn[4],
+    fprintf(stderr, "qfactor cols %u nnz %lu tiers %u/%u/%u/%u/%u/%u/%u (huge nz %u) Q %lu  %.2f ms\n",
+            rn, (unsigned long)Wt->nnz, hn[0], hn[1], hn[2], hn[3], hn[4], hn[5], hn[6],
             bignz.empty() ? 0u : bignz[0], (unsigned long)tot, (amgd_wtime() - t_start) * 1e3);
   }
   amgd_free(lists); amgd_free(cnt);

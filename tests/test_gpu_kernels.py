@@ -286,7 +286,7 @@ def _qfactor_case(structure):
     rng = np.random.default_rng(21)
     ro, cols = [0], []
     if structure == "tiers":
-        sizes = [1, 5, 31, 32, 33, 40, 64, 65, 100, 128, 129, 300, 1024, 1025, 1400]
+        sizes = [1, 5, 31, 32, 33, 40, 64, 65, 100, 128, 129, 256, 257, 300, 512, 513, 1024, 1025, 1400]
         for nz in sizes:
             lo = int(rng.integers(0, m ** 3 - 3 * nz))
             c = np.sort(rng.choice(np.arange(lo, lo + 3 * nz), size=nz, replace=False))
