@@ -87,6 +87,7 @@ def lib() -> C.CDLL:
         L.amgd_test_dot.restype = C.c_double
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
+        L.amgd_test_spgemm_win.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
@@ -257,6 +258,12 @@ def lmop_stats(reset: bool = True) -> dict:
     out = (C.c_uint64 * 4)()
     lib().amgd_test_lmop_stats(out, int(reset))
     return {"fast": out[0], "general": out[1], "dirty_prefix": out[2], "misses": out[3]}
+
+
+def spgemm_win(w: int) -> None:
+    """wide output rows: 0 = LDS hash kernels, 4096 / 8192 / 16384 = dense-accumulator column
+    windows whatever the column count, -1 = automatic (environment / default)"""
+    lib().amgd_test_spgemm_win(int(w))
 
 
 def spgemm_flat(on: bool) -> None:

@@ -173,6 +173,9 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
     amgd_coarsen_mask2(g, m, mask, x, n);
     amgd_mat_max_gather(St, vf, x, amax, m);       /* m = mat_max(S,vf,mask.*id) */
     amgd_coarsen_mask3(m, mask, vc, vf, vfd, n, anyvc);
+    if (getenv("AMGD_CLOG") && (it % 10 == 1))
+      fprintf(stderr, "coarsen n %u sweep %d active %lu\n", n, it,
+              (unsigned long)amgd_u8_count(vf, n));
   }
   dcsr_free(&S); dcsr_free(&St);
   amgd_free(vf); amgd_free(mask); amgd_free(vfd); amgd_free(g); amgd_free(w1); amgd_free(w2);
@@ -477,7 +480,8 @@ static dcsr *find_support(const dcsr *R, double goal) {
   }
   double *ones = dones(ns);
   dcsr *Sk = amgd_coo2csr(ns, si, sj, ones, nf, nc, 1);
-  if (verbose()) printf("    find_support: %d sweeps, %lu entries\n", it, (unsigned long)ns);
+  if (verbose()) printf("    find_support: %d sweeps, %lu entries (R %u x %u, nnz %lu)\n", it,
+                       (unsigned long)ns, nf, nc, (unsigned long)R->nnz);
   amgd_free(ones);
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);

@@ -1006,31 +1006,56 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
       wav[t] = av;
       __syncthreads();
       const int ne = (int)min((uint64_t)NT, a1 - wb);
-      for (int e = 0; e < ne; e++) {
-        const uint32_t L = wlen[e];
-        if (L == 0) continue;                        // uniform
-        const uint64_t b0 = wbs[e];
-        const double a = wav[e];
-        for (uint32_t j0 = 0; j0 < L; j0 += 2 * NT) {
-          const uint32_t ja = j0 + t, jb = j0 + NT + t;
-          uint32_t ca = 0, cb = 0;
-          double pa = 0.0, pb = 0.0;
-          if (ja < L) { ca = bcol[b0 + ja]; if (MODE) pa = ba[b0 + ja] * a; }
-          if (jb < L) { cb = bcol[b0 + jb]; if (MODE) pb = ba[b0 + jb] * a; }
-          if (ja < L) {
-            const uint32_t sl = sg_insert<LG>(hk, ca, &nfill, MODE == 0);
-            if (MODE) hv[sl] = hv[sl] + pa;
-            else if (sl == EMPTY_KEY) ovf = 1;
-          }
-          if (jb < L) {
-            const uint32_t sl = sg_insert<LG>(hk, cb, &nfill, MODE == 0);
-            if (MODE) hv[sl] = hv[sl] + pb;
-            else if (sl == EMPTY_KEY) ovf = 1;
-          }
-          if (MODE == 0 && (ovf || nfill > cap)) break;   // racy LDS read: early exit only
+      // chunks (layer e, offset j0) of up to 2*NT products, empty layers skipped; the
+      // next chunk's (column, product) loads are issued before the current chunk is
+      // inserted, so the HBM latency of layer k+1 overlaps the LDS work and barrier of k
+      int e = 0;
+      uint32_t j0 = 0;
+      while (e < ne && wlen[e] == 0) e++;
+      uint32_t ca = 0, cb = 0;
+      double pa = 0.0, pb = 0.0;
+      bool va = false, vb = false;
+      // raw B values are carried; the product is formed at insert time (forming it
+      // in fetch would wait for the load right there)
+      auto fetch = [&](int ee, uint32_t jj, uint32_t &xa_, uint32_t &xb_, double &ya, double &yb,
+                       bool &fa, bool &fb) {
+        const uint32_t L = wlen[ee];
+        const uint64_t b0 = wbs[ee];
+        const uint32_t ja = jj + t, jb = jj + NT + t;
+        fa = ja < L;
+        fb = jb < L;
+        if (fa) { xa_ = bcol[b0 + ja]; if (MODE) ya = ba[b0 + ja]; }
+        if (fb) { xb_ = bcol[b0 + jb]; if (MODE) yb = ba[b0 + jb]; }
+      };
+      if (e < ne) fetch(e, 0, ca, cb, pa, pb, va, vb);
+      while (e < ne) {
+        int e2 = e;
+        uint32_t j2 = j0 + 2 * NT;
+        if (j2 >= wlen[e]) {
+          e2 = e + 1;
+          j2 = 0;
+          while (e2 < ne && wlen[e2] == 0) e2++;
         }
-        if (MODE == 1) __syncthreads();              // layer k before layer k+1
-        else if (ovf || nfill > cap) break;
+        uint32_t na = 0, nb = 0;
+        double qa = 0.0, qb = 0.0;
+        bool fa = false, fb = false;
+        if (e2 < ne) fetch(e2, j2, na, nb, qa, qb, fa, fb);
+        const double a = MODE ? wav[e] : 0.0;
+        if (va) {
+          const uint32_t sl = sg_insert<LG>(hk, ca, &nfill, MODE == 0);
+          if (MODE) hv[sl] = hv[sl] + pa * a;
+          else if (sl == EMPTY_KEY) ovf = 1;
+        }
+        if (vb) {
+          const uint32_t sl = sg_insert<LG>(hk, cb, &nfill, MODE == 0);
+          if (MODE) hv[sl] = hv[sl] + pb * a;
+          else if (sl == EMPTY_KEY) ovf = 1;
+        }
+        if (MODE == 0 && (ovf || nfill > cap)) break;   // racy LDS read: early exit only
+        if (MODE == 1 && e2 != e) __syncthreads();      // layer k before layer k+1
+        e = e2;
+        j0 = j2;
+        ca = na; cb = nb; pa = qa; pb = qb; va = fa; vb = fb;
       }
       __syncthreads();
       if (MODE == 0 && (ovf || nfill > cap)) break;
@@ -1042,6 +1067,150 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
       continue;
     }
     sg_emit<NT, S>(hk, hv, wtot, wlen, t, xro[i], xcol, xa, &cnt[i]);
+  }
+}
+
+// Wide output rows (thousands of distinct columns): a dense LDS accumulator over a
+// column window [wb, wb+W) instead of a hash table.  The row's column range is
+// covered window by window; in each window the A entries are taken in ascending k
+// (layers) and all threads cover the part of that B row inside the window (B rows
+// are sorted, so it is the next run after a per-layer cursor); one barrier per layer
+// orders layer k before layer k+1, so every output is summed in the reference's
+// order.  No probing, no CAS, and the window is emitted in column order (no sort).
+// The next layer's loads are issued before the current layer's adds.
+template <int W, int RAP = 0>
+__global__ __launch_bounds__(256) void k_sg_win(const uint32_t *rows, uint32_t nrows,
+                                                const uint64_t *aro, const uint32_t *acol,
+                                                const double *aa, const uint64_t *bro,
+                                                const uint32_t *bcol, const double *ba,
+                                                uint64_t *cnt2, const uint64_t *xro,
+                                                uint32_t *xcol, double *xa) {
+  constexpr int NT = 256, SPT = W / NT;
+  __shared__ double acc[W];
+  __shared__ uint8_t tch[W];
+  __shared__ uint64_t lbs[NT];
+  __shared__ uint32_t llen[NT], lcur[NT];
+  __shared__ double lav[NT];
+  __shared__ uint32_t wtot[NT / 64 + 1];
+  __shared__ uint32_t s_min, s_max;
+  const int t = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t i = rows[r];
+    const uint64_t a0 = aro[i], a1 = aro[i + 1];
+    const uint64_t ob = xro[i];
+    const bool multi = a1 - a0 > (uint64_t)NT;
+    if (t == 0) { s_min = 0xffffffffu; s_max = 0; }
+    __syncthreads();
+    for (uint64_t ka = a0 + t; ka < a1; ka += NT) {     // column range of the row
+      const uint32_t k = acol[ka];
+      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
+      const uint64_t b0 = bro[k], b1 = bro[k + 1];
+      if (b0 < b1) {
+        atomicMin(&s_min, bcol[b0]);
+        atomicMax(&s_max, bcol[b1 - 1]);
+      }
+    }
+    __syncthreads();
+    const uint32_t cmin = s_min, cmax = s_max;
+    uint32_t nout = 0;
+    for (uint64_t wbl = cmin; wbl <= (uint64_t)cmax && cmin <= cmax; wbl += W) {
+      const uint32_t wb = (uint32_t)wbl;
+      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + W - 1);   // inclusive
+      for (int q = t; q < W; q += NT) { acc[q] = 0.0; tch[q] = 0; }
+      for (uint64_t c0 = a0; c0 < a1; c0 += NT) {
+        const int ne = (int)min((uint64_t)NT, a1 - c0);
+        if (multi || wb == cmin) {                      // layer table of this chunk
+          if (t < ne) {
+            const uint64_t ka = c0 + t;
+            const uint32_t k = acol[ka];
+            uint32_t len = 0;
+            uint64_t b0 = 0;
+            if (!(ka + 1 < a1 && acol[ka + 1] == k)) {   // duplicate columns: the last one wins
+              b0 = bro[k];
+              len = (uint32_t)(bro[k + 1] - b0);
+            }
+            uint32_t cur = 0;
+            if (wb != cmin) {                           // lower_bound(wb) in the B row
+              uint32_t lo = 0, hi = len;
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (bcol[b0 + mid] < wb) lo = mid + 1;
+                else hi = mid;
+              }
+              cur = lo;
+            }
+            lbs[t] = b0;
+            llen[t] = len;
+            lav[t] = aa[ka];
+            lcur[t] = cur;
+          }
+        }
+        __syncthreads();
+        auto nextl = [&](int e) {
+          e++;
+          while (e < ne && lcur[e] >= llen[e]) e++;
+          return e;
+        };
+        int e = nextl(-1);
+        uint32_t off = 0, col = 0xffffffffu;
+        double val = 0.0;
+        if (e < ne) {
+          off = lcur[e];
+          const uint32_t j = off + t;
+          if (j < llen[e]) { col = bcol[lbs[e] + j]; val = ba[lbs[e] + j]; }
+        }
+        while (e < ne) {
+          const int e2 = nextl(e);
+          uint32_t ncol = 0xffffffffu;
+          double nval = 0.0;
+          if (e2 < ne) {
+            const uint32_t j = lcur[e2] + t;
+            if (j < llen[e2]) { ncol = bcol[lbs[e2] + j]; nval = ba[lbs[e2] + j]; }
+          }
+          const bool in = col <= we;
+          if (in) {
+            const uint32_t q = col - wb;
+            acc[q] = acc[q] + val * lav[e];
+            tch[q] = 1;
+          }
+          const uint32_t n = (uint32_t)__syncthreads_count(in);   // layer k before k+1
+          off += n;
+          if (n == (uint32_t)NT) {                     // more of this layer in the window
+            const uint32_t j = off + t;
+            col = 0xffffffffu;
+            if (j < llen[e]) { col = bcol[lbs[e] + j]; val = ba[lbs[e] + j]; }
+            continue;
+          }
+          if (t == 0) lcur[e] = off;
+          e = e2;
+          if (e < ne) off = lcur[e];
+          col = ncol;
+          val = nval;
+        }
+        __syncthreads();
+      }
+      // emit the window in column order: each thread a run of SPT slots
+      uint32_t c = 0;
+      for (int q = 0; q < SPT; q++) {
+        const int sl = t * SPT + q;
+        c += (tch[sl] && acc[sl] != 0.0) ? 1u : 0u;
+      }
+      const uint32_t inc = block_incl_scan<NT>(c, wtot);
+      uint64_t o = ob + nout + (inc - c);
+      for (int q = 0; q < SPT; q++) {
+        const int sl = t * SPT + q;
+        if (tch[sl] && acc[sl] != 0.0) {
+          xcol[o] = wb + (uint32_t)sl;
+          xa[o] = acc[sl];
+          o++;
+        }
+      }
+      nout += wtot[0] + (NT / 64 > 1 ? wtot[1] : 0) + (NT / 64 > 2 ? wtot[2] : 0) +
+              (NT / 64 > 3 ? wtot[3] : 0);
+      __syncthreads();
+    }
+    if (t == 0) cnt2[i] = nout;
+    __syncthreads();
   }
 }
 
@@ -1123,12 +1292,85 @@ static bool sg_force_flat() {
   return g_sg_flat == 1;
 }
 extern "C" void amgd_spgemm_force_flat(int on) { g_sg_flat = on ? 1 : 0; }
+static int g_sg_win_forced = 0; // tests: the window applies whatever the column count
+static int g_sg_win = -1;       // AMGD_SG_WIN: window of the dense-accumulator kernel (0: off)
+static int sg_win() {
+  if (g_sg_win < 0) {
+    const char *e = getenv("AMGD_SG_WIN");
+    g_sg_win = e ? atoi(e) : 2048;
+    if (g_sg_win != 0 && g_sg_win != 1024 && g_sg_win != 2048 && g_sg_win != 4096 && g_sg_win != 8192 && g_sg_win != 16384) g_sg_win = 2048;
+  }
+  return g_sg_win;
+}
+extern "C" void amgd_spgemm_set_win(int w) {
+  g_sg_win = w < 0 ? -1 : w;
+  g_sg_win_forced = w > 0;
+}
+// the windowed kernel pays one barrier per layer per window: it wins while the output
+// rows span few windows (narrow column spaces), the hash kernels beyond
+static uint32_t sg_win_p0() {
+  static long v = -1;
+  if (v < 0) { const char *e = getenv("AMGD_SG_WIN_P0"); v = e ? atol(e) : 48; }
+  return (uint32_t)v;
+}
 static int g_sg_slot = -1;
 static uint64_t g_sg_bytes = 0;
 extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
 extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; }
 extern "C" uint64_t amgd_spgemm_bytes(void) { return g_sg_bytes; }
 
+// SGLOG: rows with >= 1024 outputs binned by column span (<=4K, 8K, 16K, 32K, 64K, more)
+__global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn,
+                            unsigned long long *h) {
+  GRID_STRIDE(i, rn) {
+    const uint64_t a = ro[i], b = ro[i + 1];
+    if (b - a < 1024) continue;
+    const uint32_t sp = col[b - 1] - col[a] + 1;
+    int q = 0;
+    while (q < 5 && sp > (4096u << q)) q++;
+    atomicAdd(&h[q], 1ull);
+  }
+}
+// wide rows -> windowed (dense accumulator) or hash kernels.  The windowed kernel
+// pays a barrier per layer per window: it is chosen when a layer brings enough
+// products into a window, i.e. products * min(W, span) / (layers * span) >= p0,
+// span = the row's output column range (from the first/last column of its B rows).
+__global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *aro,
+                            const uint32_t *acol, const uint64_t *bro, const uint32_t *bcol,
+                            const uint64_t *ub, uint32_t W, uint32_t p0, uint32_t *wl,
+                            uint32_t *hl, unsigned *cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t iters = (n + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {   // uniform trip count (wave_append)
+    const uint64_t r = c0 + it * stride;
+    const bool valid = r < n;
+    bool w = false;
+    uint32_t i = 0;
+    if (valid) {
+      i = list[r];
+      const uint64_t a0 = aro[i], a1 = aro[i + 1];
+      uint32_t mn = 0xffffffffu, mx = 0;
+      for (uint64_t ka = a0; ka < a1; ka++) {
+        const uint32_t k = acol[ka];
+        const uint64_t b0 = bro[k], b1 = bro[k + 1];
+        if (b0 < b1) {
+          mn = min(mn, bcol[b0]);
+          mx = max(mx, bcol[b1 - 1]);
+        }
+      }
+      if (mn <= mx) {
+        const double span = (double)(mx - mn) + 1.0;
+        const double ppwl = (double)ub[i] * fmin((double)W, span) / ((double)(a1 - a0) * span);
+        w = ppwl >= (double)p0;
+      }
+    }
+    const unsigned p = wave_append(&cnt[0], valid && w);
+    if (valid && w) wl[p] = i;
+    const unsigned q = wave_append(&cnt[1], valid && !w);
+    if (valid && !w) hl[q] = i;
+  }
+}
 extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   if (A->cn != B->rn) {
     fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
@@ -1220,6 +1462,67 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
   }
   const bool rap = g_sg_slot >= 0;
+  const int win = kseq ? sg_win() : 0;
+  // wide bins (3: block hash, 4: dense slab) split into windowed / hash rows
+  uint32_t *wlists = nullptr;
+  unsigned wn[4] = {0, 0, 0, 0};
+  if (win && (hn[3] || hn[4])) {
+    wlists = (uint32_t *)amgd_alloc(2 * L * 4 + 16);
+    unsigned *wc = (unsigned *)amgd_alloc(32);
+    HIPCK(hipMemsetAsync(wc, 0, 32, s));
+    const uint32_t p0 = g_sg_win_forced ? 0u : sg_win_p0();
+    for (int q = 0; q < 2; q++) {
+      const unsigned nb = hn[3 + q];
+      if (!nb) continue;
+      uint32_t *src = lists + (3 + q) * L;
+      // windowed rows -> wlists[q]; hash rows compacted into the (copied) bin list
+      uint32_t *tmp = (uint32_t *)amgd_alloc((size_t)nb * 4 + 4);
+      HIPCK(hipMemcpyAsync(tmp, src, (size_t)nb * 4, hipMemcpyDeviceToDevice, s));
+      k_win_split<<<grid_for(nb), 256, 0, s>>>(tmp, nb, A->ro, A->col, B->ro, B->col, ub,
+                                               (uint32_t)win, p0, wlists + q * L, src, wc + 2 * q);
+      KCHECK();
+      amgd_free(tmp);
+    }
+    amgd_d2h(wn, wc, 16);
+    amgd_free(wc);
+    hn[3] = wn[1];
+    hn[4] = wn[3];
+  }
+#define SG_WIN(nr, rows_)                                                                       \
+  if (nr) {                                                                                     \
+    const unsigned nrw = (nr);                                                                  \
+    const int g = (int)std::min<unsigned>(nrw, 16384u);                                         \
+    if (win == 1024 && rap)                                                                     \
+      k_sg_win<1024, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 1024)                                                                       \
+      k_sg_win<1024, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 2048 && rap)                                                                \
+      k_sg_win<2048, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 2048)                                                                       \
+      k_sg_win<2048, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 4096 && rap)                                                                \
+      k_sg_win<4096, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 4096)                                                                       \
+      k_sg_win<4096, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 8192 && rap)                                                                \
+      k_sg_win<8192, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (win == 8192)                                                                       \
+      k_sg_win<8192, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
+                                          B->a, cnt2, cnt, tcol, ta);                           \
+    else if (rap)                                                                               \
+      k_sg_win<16384, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
+                                           B->a, cnt2, cnt, tcol, ta);                          \
+    else                                                                                        \
+      k_sg_win<16384, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
+                                           B->a, cnt2, cnt, tcol, ta);                          \
+  }
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
@@ -1237,6 +1540,10 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     SG_NUM(k_sg_row, 256, 13, 3, 8192u)
   }
 #undef SG_NUM
+  if (win) {
+    SG_WIN(wn[0], wlists)
+    SG_WIN(wn[2], wlists + L)
+  }
   if (hn[4]) {
     if (rap)
       k_spgemm_long<1, 1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,
@@ -1245,6 +1552,7 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
       k_spgemm_long<1, 0><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,
                                                B->a, B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);
   }
+#undef SG_WIN
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
   uint64_t nz = amgd_scan_u64(cnt2, rn);
@@ -1263,6 +1571,7 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     amgd_free(cnt); amgd_free(tcol); amgd_free(ta);
   }
   amgd_free(ub); amgd_free(lists); amgd_free(counts);
+  if (wlists) amgd_free(wlists);
   if (slab_v) { amgd_free(slab_v); amgd_free(slab_s); }
   if (sglog) {
     uint64_t prods = 0;
@@ -1274,10 +1583,19 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
     }
     amgd_sync();
     double ms = (amgd_wtime() - t_start) * 1e3;
-    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  %s  sym %u/%u num %u/%u/%u/%u dense %u  %.2f ms\n",
+    if (rn) {
+      unsigned long long *h = (unsigned long long *)amgd_alloc(64), hh[6];
+      amgd_memset(h, 0, 48);
+      k_span_hist<<<grid_for(rn), 256, 0, s>>>(X->ro, X->col, rn, h);
+      amgd_d2h(hh, h, 48);
+      amgd_free(h);
+      fprintf(stderr, "spgemm span hist (rows >= 1024 out): %llu %llu %llu %llu %llu %llu\n", hh[0],
+              hh[1], hh[2], hh[3], hh[4], hh[5]);
+    }
+    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  %s  sym %u/%u num %u/%u/%u/%u dense %u win %u  %.2f ms\n",
             rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz,
-            (unsigned long)prods, prods / (ms * 1e6), kseq ? (wide ? "kseq-w" : "kseq") : "flat",
-            hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], ms);
+            (unsigned long)prods, prods / (ms * 1e6), kseq ? (wide ? (win ? "kseq-w+win" : "kseq-w") : (win ? "kseq+win" : "kseq")) : "flat",
+            hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], wn[0] + wn[2], ms);
   }
   return X;
 }

@@ -153,3 +153,6 @@ API void amgd_test_qf_stats(uint64_t *out) {
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
 extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
+/* window of the dense-accumulator numeric kernel for wide rows: 0 (hash kernels), 8192, 16384 */
+extern void amgd_spgemm_set_win(int w);
+API void amgd_test_spgemm_win(int w) { amgd_spgemm_set_win(w); }

@@ -38,11 +38,15 @@ def test_spgemm_dense_overflow_rows():
     assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
 
 
-@pytest.mark.parametrize("case", ["narrow", "wide", "dense_rows", "dups_cancel"])
-def test_spgemm_kseq_long_b_rows(case):
+@pytest.mark.parametrize("win", [0, 4096, 8192, 16384])
+@pytest.mark.parametrize("case", ["narrow", "wide", "dense_rows", "dups_cancel", "wide_span"])
+def test_spgemm_kseq_long_b_rows(case, win):
     """k-sequential kernels (mean B row >= 64): every numeric bin incl. the dense slab,
-    duplicate columns in A rows (last one wins) and exact cancellation"""
-    rng = np.random.default_rng({"narrow": 31, "wide": 32, "dense_rows": 33, "dups_cancel": 34}[case])
+    duplicate columns in A rows (last one wins) and exact cancellation; wide rows by the
+    LDS hash (win 0) or the dense-accumulator column windows (several windows per row,
+    A rows longer than one layer table)"""
+    rng = np.random.default_rng({"narrow": 31, "wide": 32, "dense_rows": 33, "dups_cancel": 34,
+                                 "wide_span": 35}[case])
     if case == "narrow":        # mean B row ~100: wave-sized blocks for the small bins
         A = refops.rand_csr(rng, 400, 300, 0.02)
         B = refops.rand_csr(rng, 300, 3000, 0.035)
@@ -52,6 +56,9 @@ def test_spgemm_kseq_long_b_rows(case):
     elif case == "dense_rows":  # > 4096 distinct columns in some rows
         A = refops.rand_csr(rng, 20, 200, 0.3)
         B = refops.rand_csr(rng, 200, 9000, 0.05)
+    elif case == "wide_span":   # ~300-entry A rows, outputs spanning 40000 columns
+        A = refops.rand_csr(rng, 12, 600, 0.5, ints=True)
+        B = refops.rand_csr(rng, 600, 40000, 0.007, ints=True)
     else:
         A = refops.rand_csr(rng, 150, 120, 0.05, ints=True)
         B = refops.rand_csr(rng, 120, 400, 0.3, ints=True)
@@ -68,7 +75,11 @@ def test_spgemm_kseq_long_b_rows(case):
     assert B.a.size >= 64 * B.rn
     R = refops.spgemm(A, B)
     oa.spgemm_flat(False)
-    X = oa.test_csr_op(0, A, B)
+    oa.spgemm_win(win)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_win(-1)
     oa.spgemm_flat(True)
     try:
         Y = oa.test_csr_op(0, A, B)
