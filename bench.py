@@ -12,7 +12,8 @@ value   : whole-job rows/s = (ranks x rows) / max-over-ranks seconds per step.
           replicas only"), so scaling is "weak".
 roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
           and AfP = Af W; instantiated with RAP=1 so rocprof lists them apart;
-          k_sg_kseq for long B-operand rows, k_sg_row for short ones),
+          k_sg_kseq for long B-operand rows, k_sg_row for short ones, k_sg_win
+          for wide output rows),
           event-timed live on the library stream; algorithmic bytes = 12 B per
           nnz of each operand and result + 8 B per row (DESIGN.md);
           tools/rap_from_prof.py sums the same kernels from a rocprofv3 summary.
@@ -194,7 +195,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": args.traffic,
-                         "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_spgemm_long<1,1>: numeric "
+                         "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",
                          "algorithmic_bytes_per_setup": rap_bytes / args.steps,

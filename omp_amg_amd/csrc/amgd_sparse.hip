@@ -441,6 +441,14 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
   if (M->rn == 0) return;
+  static int mode = -1;
+  if (mode < 0) mode = getenv("AMGD_SPMV_MODE") ? atoi(getenv("AMGD_SPMV_MODE")) : 0;
+  if (mode == 1) {
+    int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
+    k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+    KCHECK();
+    return;
+  }
   if (M->nnz >= 32ull * M->rn && M->rn >= SL_MIN_ROWS) {
     int g = (int)std::min<uint64_t>(((uint64_t)M->rn + 255) / 256, 16384);
     k_spmv_lane<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z, alpha,
