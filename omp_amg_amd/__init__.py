@@ -88,6 +88,7 @@ def lib() -> C.CDLL:
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
+        L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
@@ -264,6 +265,12 @@ def spgemm_win(w: int) -> None:
     """wide output rows: 0 = LDS hash kernels, 4096 / 8192 / 16384 = dense-accumulator column
     windows whatever the column count, -1 = automatic (environment / default)"""
     lib().amgd_test_spgemm_win(int(w))
+
+
+def spgemm_wsym(w: int) -> None:
+    """symbolic pass of rows with many products: 0 = LDS hash, 32768 / 65536 = byte-map
+    column windows, -1 = automatic (environment / default)"""
+    lib().amgd_test_spgemm_wsym(int(w))
 
 
 def spgemm_flat(on: bool) -> None:

@@ -1316,6 +1316,18 @@ extern "C" void amgd_spgemm_set_win(int w) {
 }
 // the windowed kernel pays one barrier per layer per window: it wins while the output
 // rows span few windows (narrow column spaces), the hash kernels beyond
+static int g_sg_wsym = -1;      // AMGD_SG_WSYM: byte-map window of the symbolic kernel (0: hash)
+static int sg_wsym() {
+  if (g_sg_wsym < 0) {
+    const char *e = getenv("AMGD_SG_WSYM");
+    g_sg_wsym = e ? atoi(e) : 32768;
+    if (g_sg_wsym != 0 && g_sg_wsym != 8192 && g_sg_wsym != 16384 && g_sg_wsym != 32768 &&
+        g_sg_wsym != 65536)
+      g_sg_wsym = 32768;
+  }
+  return g_sg_wsym;
+}
+extern "C" void amgd_spgemm_set_wsym(int w) { g_sg_wsym = w; }
 static uint32_t sg_win_p0() {
   static long v = -1;
   if (v < 0) { const char *e = getenv("AMGD_SG_WIN_P0"); v = e ? atol(e) : 48; }
@@ -1339,6 +1351,84 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
     atomicAdd(&h[q], 1ull);
   }
 }
+// Symbolic pass for rows with many products: distinct columns counted with an LDS
+// byte map over a column window [wb, wb+SW) instead of a hash table (no probing, no
+// CAS; counting needs no order).  Each thread walks its own layers (B rows, sorted)
+// from a cursor while the columns stay inside the window; windows cover the row's
+// column range [cmin, cmax].  No capacity limit: every row gets its exact count.
+template <int SW>
+__global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t nrows,
+                                                 const uint64_t *aro, const uint32_t *acol,
+                                                 const uint64_t *bro, const uint32_t *bcol,
+                                                 uint64_t *cnt) {
+  constexpr int NT = 256, MAXL = 1024;
+  __shared__ uint32_t map[SW / 4];
+  __shared__ uint64_t lbs[MAXL];
+  __shared__ uint32_t lend[MAXL], lcur[MAXL];
+  __shared__ uint32_t s_min, s_max;
+  __shared__ unsigned long long s_tot;
+  uint8_t *mb = (uint8_t *)map;
+  const int t = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t i = rows[r];
+    const uint64_t a0 = aro[i], a1 = aro[i + 1];
+    if (a1 - a0 > (uint64_t)MAXL) {          // more layers than the table: dense-slab recount
+      if (t == 0) cnt[i] = OVERFLOW_MARK;
+      continue;
+    }
+    const uint32_t nl = (uint32_t)(a1 - a0);
+    if (t == 0) { s_min = 0xffffffffu; s_max = 0; s_tot = 0; }
+    __syncthreads();
+    for (uint32_t e = t; e < nl; e += NT) {
+      const uint32_t k = acol[a0 + e];
+      const uint64_t b0 = bro[k], b1 = bro[k + 1];
+      lbs[e] = b0;
+      lend[e] = (uint32_t)(b1 - b0);
+      lcur[e] = 0;
+      if (b0 < b1) {
+        atomicMin(&s_min, bcol[b0]);
+        atomicMax(&s_max, bcol[b1 - 1]);
+      }
+    }
+    __syncthreads();
+    const uint32_t cmin = s_min, cmax = s_max;
+    uint64_t tot = 0;
+    for (uint64_t wbl = cmin; cmin <= cmax && wbl <= (uint64_t)cmax; wbl += SW) {
+      const uint32_t wb = (uint32_t)wbl;
+      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + SW - 1);
+      for (int q = t; q < SW / 4; q += NT) map[q] = 0;
+      __syncthreads();
+      for (uint32_t e = t; e < nl; e += NT) {
+        const uint64_t b0 = lbs[e];
+        const uint32_t L = lend[e];
+        uint32_t c = lcur[e];
+        while (c < L) {
+          uint32_t cc[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) cc[u] = (c + u < L) ? bcol[b0 + c + u] : 0xffffffffu;
+          int u = 0;
+          for (; u < 4; u++) {
+            if (cc[u] > we) break;
+            mb[cc[u] - wb] = 1;
+          }
+          c += u;
+          if (u < 4) break;
+        }
+        lcur[e] = c;
+      }
+      __syncthreads();
+      uint32_t n = 0;
+      for (int q = t; q < SW / 4; q += NT) n += __popc(map[q] & 0x01010101u);
+      atomicAdd(&s_tot, (unsigned long long)n);
+      __syncthreads();
+      tot = s_tot;
+      __syncthreads();
+    }
+    if (t == 0) cnt[i] = tot;
+    __syncthreads();
+  }
+}
+
 // wide rows -> windowed (dense accumulator) or hash kernels.  The windowed kernel
 // pays a barrier per layer per window: it is chosen when a layer brings enough
 // products into a window, i.e. products * min(W, span) / (layers * span) >= p0,
@@ -1420,7 +1510,20 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
   if (hc[1]) {
-    if (kseq)
+    const int wsym = kseq ? sg_wsym() : 0;
+    if (wsym == 8192)
+      k_sg_wsym<8192><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
+    else if (wsym == 16384)
+      k_sg_wsym<16384><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
+    else if (wsym == 32768)
+      k_sg_wsym<32768><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
+    else if (wsym == 65536)
+      k_sg_wsym<65536><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
+    else if (kseq)
       k_sg_kseq<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
           nullptr);

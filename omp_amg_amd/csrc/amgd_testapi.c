@@ -156,3 +156,6 @@ API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
 /* window of the dense-accumulator numeric kernel for wide rows: 0 (hash kernels), 8192, 16384 */
 extern void amgd_spgemm_set_win(int w);
 API void amgd_test_spgemm_win(int w) { amgd_spgemm_set_win(w); }
+/* symbolic pass of rows with many products: 0 (LDS hash), 32768 / 65536 (byte-map windows) */
+extern void amgd_spgemm_set_wsym(int w);
+API void amgd_test_spgemm_wsym(int w) { amgd_spgemm_set_wsym(w); }

@@ -89,6 +89,34 @@ def test_spgemm_kseq_long_b_rows(case, win):
     assert refops.same(Y, R)
 
 
+@pytest.mark.parametrize("wsym", [0, 32768, 65536])
+@pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows"])
+def test_spgemm_symbolic_windows(case, wsym):
+    """symbolic pass of rows with many products: LDS hash (0) or byte-map column windows
+    (several windows per row; A rows past the layer table fall back to the slab recount)"""
+    rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54}[case])
+    if case == "wide":
+        A = refops.rand_csr(rng, 200, 150, 0.04)
+        B = refops.rand_csr(rng, 150, 6000, 0.1)
+    elif case == "dense_rows":
+        A = refops.rand_csr(rng, 20, 200, 0.3)
+        B = refops.rand_csr(rng, 200, 9000, 0.05)
+    elif case == "wide_span":
+        A = refops.rand_csr(rng, 12, 600, 0.5, ints=True)
+        B = refops.rand_csr(rng, 600, 200000, 0.0015, ints=True)
+    else:                       # 1100-1300 entries per A row
+        A = refops.rand_csr(rng, 4, 1400, 0.85)
+        B = refops.rand_csr(rng, 1400, 3000, 0.03)
+    assert B.a.size >= 64 * B.rn
+    R = refops.spgemm(A, B)
+    oa.spgemm_wsym(wsym)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_wsym(-1)
+    assert refops.same(X, R)
+
+
 def test_spgemm_empty_rows():
     rng = np.random.default_rng(3)
     A = refops.rand_csr(rng, 50, 40, 0.02)
