@@ -1159,21 +1159,34 @@ __global__ __launch_bounds__(256) void k_sg_win(const uint32_t *rows, uint32_t n
           while (e < ne && lcur[e] >= llen[e]) e++;
           return e;
         };
+        // three-stage pipeline over layers: the columns of layer e+2 and the values of
+        // layer e+1 (only where its column falls in the window) are in flight while
+        // layer e is added; out-of-window entries cost a 4-byte column read only
         int e = nextl(-1);
         uint32_t off = 0, col = 0xffffffffu;
         double val = 0.0;
         if (e < ne) {
           off = lcur[e];
           const uint32_t j = off + t;
-          if (j < llen[e]) { col = bcol[lbs[e] + j]; val = ba[lbs[e] + j]; }
+          if (j < llen[e]) {
+            col = bcol[lbs[e] + j];
+            if (col <= we) val = ba[lbs[e] + j];
+          }
+        }
+        int e2 = e < ne ? nextl(e) : ne;
+        uint32_t col2 = 0xffffffffu;
+        if (e2 < ne) {
+          const uint32_t j = lcur[e2] + t;
+          if (j < llen[e2]) col2 = bcol[lbs[e2] + j];
         }
         while (e < ne) {
-          const int e2 = nextl(e);
-          uint32_t ncol = 0xffffffffu;
-          double nval = 0.0;
-          if (e2 < ne) {
-            const uint32_t j = lcur[e2] + t;
-            if (j < llen[e2]) { ncol = bcol[lbs[e2] + j]; nval = ba[lbs[e2] + j]; }
+          const int e3 = e2 < ne ? nextl(e2) : ne;
+          double val2 = 0.0;
+          if (e2 < ne && col2 <= we) val2 = ba[lbs[e2] + lcur[e2] + t];
+          uint32_t col3 = 0xffffffffu;
+          if (e3 < ne) {
+            const uint32_t j = lcur[e3] + t;
+            if (j < llen[e3]) col3 = bcol[lbs[e3] + j];
           }
           const bool in = col <= we;
           if (in) {
@@ -1186,14 +1199,19 @@ __global__ __launch_bounds__(256) void k_sg_win(const uint32_t *rows, uint32_t n
           if (n == (uint32_t)NT) {                     // more of this layer in the window
             const uint32_t j = off + t;
             col = 0xffffffffu;
-            if (j < llen[e]) { col = bcol[lbs[e] + j]; val = ba[lbs[e] + j]; }
-            continue;
+            if (j < llen[e]) {
+              col = bcol[lbs[e] + j];
+              if (col <= we) val = ba[lbs[e] + j];
+            }
+            continue;                                  // (stages e2/e3 are reissued)
           }
           if (t == 0) lcur[e] = off;
           e = e2;
           if (e < ne) off = lcur[e];
-          col = ncol;
-          val = nval;
+          col = col2;
+          val = val2;
+          e2 = e3;
+          col2 = col3;
         }
         __syncthreads();
       }
