@@ -298,6 +298,47 @@ __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t
 }
 // long rows: one wavefront per row; the 64 lanes load and multiply a chunk
 // (coalesced) into LDS, lane 0 adds the chunk in order -- same sum, same order.
+// The next chunk's loads are issued before lane 0's adds (double buffering), and
+// lane 0 reads its chunk 8 products at a time.
+__device__ __forceinline__ double wave_row_sum(const uint32_t *col, const double *a,
+                                               const double *x, uint64_t k0, uint64_t k1,
+                                               double *buf, int lane) {
+  double t = 0;
+  uint64_t k = k0 + lane;
+  double p = 0.0;
+  if (k < k1) p = x ? a[k] * x[col[k]] : a[k];
+  for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
+    buf[lane] = p;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t kn = c0 + 64 + lane;
+    uint32_t cn = 0;
+    double an = 0.0;
+    if (kn < k1) {
+      an = a[kn];
+      if (x) cn = col[kn];
+    }
+    if (lane == 0) {
+      const int m = (int)min((uint64_t)64, k1 - c0);
+      int q = 0;
+      for (; q + 8 <= m; q += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = buf[q + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) t += v[u];
+      }
+      for (; q < m; q++) t += buf[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    p = 0.0;
+    if (kn < k1) p = x ? an * x[cn] : an;
+  }
+  return t;
+}
 __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t rn, const double *x,
                                                    double *z, double alpha, const double *y,
@@ -305,26 +346,7 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
   __shared__ double buf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < rn; i += (uint64_t)gridDim.x * 4) {
-    uint64_t k0 = ro[i], k1 = ro[i + 1];
-    double t = 0;
-    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
-      uint64_t k = c0 + lane;
-      if (k < k1) buf[w][lane] = x ? a[k] * x[col[k]] : a[k];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      if (lane == 0) {
-        int m = (int)min((uint64_t)64, k1 - c0);
-        int q = 0;
-        for (; q + 8 <= m; q += 8) {
-          double v0 = buf[w][q], v1 = buf[w][q + 1], v2 = buf[w][q + 2], v3 = buf[w][q + 3];
-          double v4 = buf[w][q + 4], v5 = buf[w][q + 5], v6 = buf[w][q + 6], v7 = buf[w][q + 7];
-          t += v0; t += v1; t += v2; t += v3; t += v4; t += v5; t += v6; t += v7;
-        }
-        for (; q < m; q++) t += buf[w][q];
-      }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
+    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
@@ -405,22 +427,7 @@ __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, cons
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
     const uint32_t i = list[r];
-    const uint64_t k0 = ro[i], k1 = ro[i + 1];
-    double t = 0;
-    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
-      const uint64_t k = c0 + lane;
-      if (k < k1) buf[w][lane] = x ? a[k] * x[col[k]] : a[k];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane == 0) {
-        const int m = (int)min((uint64_t)64, k1 - c0);
-        for (int q = 0; q < m; q++) t += buf[w][q];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) z[i] = t;
   }
 }
