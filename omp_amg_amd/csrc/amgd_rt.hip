@@ -752,16 +752,27 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
     uint64_t c = cb;
     while (c < ce) {
       if (tid == 0) {
+        // runs of chunks guessed in one binade e are walked on the integer grid of
+        // that binade (S stays strictly inside (2^52, 2^53), so t = S * 2^(e-52)
+        // is exact and lies in binade e): the double is formed once per run
         double t = s;
         uint64_t q = c;
-        for (; q < ce; q++) {
+        while (q < ce) {
           const SpecRec r = rb[q - cb];
           if (r.flag || !(fabs(t) >= 2.2250738585072014e-308) || ilogb(t) != r.e) break;
-          long long S0 = (long long)ldexp(t, 52 - r.e);
-          bool ok = S0 > 0 ? (S0 + r.mn > LO && S0 + r.mx < HI)
-                           : (S0 + r.mx < -LO && S0 + r.mn > -HI);
-          if (!ok) break;
-          t = ldexp((double)(S0 + r.M), r.e - 52);
+          const int e = r.e;
+          long long S = (long long)ldexp(t, 52 - e);
+          const uint64_t q0 = q;
+          for (; q < ce; q++) {
+            const SpecRec rr = rb[q - cb];
+            if (rr.flag || rr.e != e) break;
+            const bool ok = S > 0 ? (S + rr.mn > LO && S + rr.mx < HI)
+                                  : (S + rr.mx < -LO && S + rr.mn > -HI);
+            if (!ok) break;
+            S += rr.M;
+          }
+          t = ldexp((double)S, e - 52);
+          if (q == q0) break;             // no progress: the chunk is added exactly below
         }
         s_sh = t;
         cnext = q;
