@@ -183,9 +183,6 @@ extern "C" dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *v
 // perm_out (optional) maps CSC position -> CSR position.
 // ---------------------------------------------------------------------------
 __global__ void k_iota_u64(uint64_t *p, uint64_t n) { GRID_STRIDE(i, n) p[i] = i; }
-__global__ void k_col_count(const uint32_t *col, uint64_t nz, uint64_t *cnt) {
-  GRID_STRIDE(k, nz) atomicAdd((unsigned long long *)&cnt[col[k]], 1ull);
-}
 __global__ void k_tr_fill(const uint64_t *perm, const uint32_t *row, const double *a, uint64_t nz,
                           uint32_t *tcol, double *ta) {
   GRID_STRIDE(t, nz) {
@@ -194,14 +191,40 @@ __global__ void k_tr_fill(const uint64_t *perm, const uint32_t *row, const doubl
     ta[t] = a[p];
   }
 }
+// row offsets of the transpose from the sorted column keys: ro[c] = #keys < c, i.e.
+// every c in (keys[t-1], keys[t]] starts at t (no atomics, no scan)
+// (runs of more than RO_GAP empty columns are queued and filled block-wide)
+#define RO_GAP 64
+__global__ void k_ro_from_sorted(const uint32_t *keys, uint64_t nz, uint32_t cn, uint64_t *ro,
+                                 unsigned *ngap, uint64_t *gaps) {
+  GRID_STRIDE(t, nz + 1) {
+    const uint64_t lo = t == 0 ? 0 : (uint64_t)keys[t - 1] + 1;
+    const uint64_t hi = t == nz ? (uint64_t)cn : (uint64_t)keys[t];
+    if (hi + 1 > lo + RO_GAP) {
+      const unsigned g = atomicAdd(ngap, 1u);
+      gaps[3 * (uint64_t)g] = lo;
+      gaps[3 * (uint64_t)g + 1] = hi;
+      gaps[3 * (uint64_t)g + 2] = t;
+      continue;
+    }
+    for (uint64_t c = lo; c <= hi; c++) ro[c] = t;
+  }
+}
+__global__ void k_ro_gaps(const unsigned *ngap, const uint64_t *gaps, uint64_t *ro) {
+  const unsigned n = *ngap;
+  for (unsigned g = blockIdx.x; g < n; g += gridDim.x) {
+    const uint64_t lo = gaps[3 * (uint64_t)g], hi = gaps[3 * (uint64_t)g + 1],
+                   t = gaps[3 * (uint64_t)g + 2];
+    for (uint64_t c = lo + threadIdx.x; c <= hi; c += blockDim.x) ro[c] = t;
+  }
+}
 extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   hipStream_t s = amgd_s();
   uint64_t nz = A->nnz;
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->cn + 1) * 8);
-  HIPCK(hipMemsetAsync(cnt, 0, ((size_t)A->cn + 1) * 8, s));
   uint64_t *perm = (uint64_t *)amgd_alloc(nz * 8 + 8);
+  if (!nz) HIPCK(hipMemsetAsync(cnt, 0, ((size_t)A->cn + 1) * 8, s));
   if (nz) {
-    k_col_count<<<grid_for(nz), 256, 0, s>>>(A->col, nz, cnt);
     uint64_t *iota = (uint64_t *)amgd_alloc(nz * 8 + 8);
     uint32_t *kout = (uint32_t *)amgd_alloc(nz * 4 + 4);
     k_iota_u64<<<grid_for(nz), 256, 0, s>>>(iota, nz);
@@ -210,9 +233,20 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
     HIPCK(rocprim::radix_sort_pairs(nullptr, tb, A->col, kout, iota, perm, (size_t)nz, 0, eb, s));
     void *tmp = amgd_alloc(tb + 16);
     HIPCK(rocprim::radix_sort_pairs(tmp, tb, A->col, kout, iota, perm, (size_t)nz, 0, eb, s));
+    {
+      // a run of > RO_GAP empty columns needs > RO_GAP columns: at most cn / RO_GAP + 1 runs
+      const uint64_t maxg = (uint64_t)A->cn / RO_GAP + 2;
+      uint64_t *gaps = (uint64_t *)amgd_alloc(maxg * 24 + 16);
+      unsigned *ngap = (unsigned *)amgd_alloc(16);
+      HIPCK(hipMemsetAsync(ngap, 0, 4, s));
+      k_ro_from_sorted<<<grid_for(nz + 1), 256, 0, s>>>(kout, nz, A->cn, cnt, ngap, gaps);
+      k_ro_gaps<<<1024, 256, 0, s>>>(ngap, gaps, cnt);
+      KCHECK();
+      amgd_free(gaps);
+      amgd_free(ngap);
+    }
     amgd_free(tmp); amgd_free(iota); amgd_free(kout);
   }
-  amgd_scan_u64(cnt, A->cn);
   dcsr *T = (dcsr *)malloc(sizeof(dcsr));
   T->rn = A->cn; T->cn = A->rn; T->nnz = nz; T->ro = cnt;
   T->col = (uint32_t *)amgd_alloc(nz * 4 + 4);

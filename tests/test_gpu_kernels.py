@@ -132,6 +132,15 @@ def test_transpose(seed):
     assert refops.same(oa.test_csr_op(1, A), refops.transpose(A))
 
 
+@pytest.mark.parametrize("rn,cn,density", [(40, 20000, 0.0005), (3, 5000, 0.001), (30, 700, 0.0)])
+def test_transpose_empty_column_runs(rn, cn, density):
+    # row offsets come from the sorted column keys; runs of > 64 empty columns
+    # (leading, trailing, interior) take the queued block-wide fill
+    rng = np.random.default_rng(rn)
+    A = refops.rand_csr(rng, rn, cn, density)
+    assert refops.same(oa.test_csr_op(1, A), refops.transpose(A))
+
+
 def test_mpm_and_mxmpoint():
     rng = np.random.default_rng(5)
     A = refops.rand_csr(rng, 200, 150, 0.05, ints=True)
