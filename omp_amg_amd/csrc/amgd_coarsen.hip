@@ -1,0 +1,232 @@
+// amgd_coarsen.hip -- incremental coarsening sweeps (amg_setup.c:2737-2874).
+//
+// Every quantity of a coarsening sweep is local: row i of g, w1, w2, w, the
+// strength masks and both mat_max results depends only on vf within a fixed
+// number of hops of i in S's graph (g 1, w1 2, w2 4, w/mask1 4, Amax 1, m1 and
+// mask2 5, m2 and mask3 6).  vf changes only at the points a sweep turns into C
+// points (D0), so the next sweep's values differ from the last sweep's only
+// within 6 hops of D0; everywhere else the persistent per-stage buffers already
+// hold exactly what a full recomputation would produce.  A sweep therefore
+//   1. grows D0 hop by hop (S and S^T neighbours, first visit claimed with an
+//      atomicMax on a per-sweep stamp) into one list whose prefixes are the rows
+//      within 1..6 hops,
+//   2. recomputes each stage over the prefix of its radius only, with the same
+//      per-row arithmetic (left-to-right sums from +0.0, order-free maxima) as
+//      the full kernels, and
+//   3. writes the new C points as the next sweep's D0 list.
+// When the 6-hop set is large the sweep runs the full kernels instead (same
+// buffers, same values), so the C/F sets are bit-identical either way.
+#include <float.h>
+#include "amgd.h"
+#include "amgd_dev.h"
+
+#define CS_HOPS 6
+
+// one BFS hop: frontier = front[cum(r-2) .. cum(r-1)), new nodes appended at cum(r-1)+
+__global__ __launch_bounds__(256) void k_cs_hop(const uint64_t *sro, const uint32_t *scol,
+                                                const uint64_t *tro, const uint32_t *tcol,
+                                                uint32_t *front, uint32_t *cnt, int r,
+                                                uint32_t *stamp, uint32_t base, uint32_t limit) {
+  uint32_t lo = 0;
+  for (int q = 0; q < r - 1; q++) lo += cnt[q];
+  const uint32_t hi = lo + cnt[r - 1];
+  if (hi > limit) return;                      // the host falls back to a full sweep
+  const int lane = threadIdx.x & 63;
+  const uint64_t wid = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t b = lo + wid * 64; b < hi; b += nw * 64) {
+    const uint64_t idx = b + lane;
+    const bool own = idx < hi;
+    const uint32_t j = own ? front[idx] : 0u;
+    const uint64_t s0 = own ? sro[j] : 0, s1 = own ? sro[j + 1] : 0;
+    const uint64_t t0 = own ? tro[j] : 0, t1 = own ? tro[j + 1] : 0;
+    const uint32_t ls = (uint32_t)(s1 - s0), len = ls + (uint32_t)(t1 - t0);
+    uint32_t mx = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
+    for (uint32_t e = 0; e < mx; e++) {
+      bool claim = false;
+      uint32_t i = 0;
+      if (e < len) {
+        i = e < ls ? scol[s0 + e] : tcol[t0 + (e - ls)];
+        claim = atomicMax(&stamp[i], base) < base;
+      }
+      const unsigned pos = wave_append(&cnt[r], claim);
+      if (claim) front[hi + pos] = i;
+    }
+  }
+}
+
+extern "C" int amgd_cs_grow(const dcsr *S, const dcsr *St, uint32_t *front, uint32_t *cnt_d,
+                            uint32_t *stamp, uint32_t base, uint32_t limit, uint32_t *cum) {
+  hipStream_t s = amgd_s();
+  const int g = grid_for((uint64_t)S->rn, 256, 4096);
+  for (int r = 1; r <= CS_HOPS; r++)
+    k_cs_hop<<<g, 256, 0, s>>>(S->ro, S->col, St->ro, St->col, front, cnt_d, r, stamp, base, limit);
+  KCHECK();
+  uint32_t c[8];
+  amgd_d2h(c, cnt_d, sizeof(c));
+  uint32_t t = 0, cu[CS_HOPS + 1];
+  for (int r = 0; r <= CS_HOPS; r++) {
+    t += c[r];
+    cu[r] = t;
+    if (t > limit) return 0;                   // cum untouched: the caller's full sizes
+  }
+  for (int r = 0; r <= CS_HOPS; r++) cum[r] = cu[r];
+  return 1;
+}
+
+#define LIST_ROWS(r, i, list, n)                                                                \
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < (uint64_t)(n);         \
+       r += (uint64_t)gridDim.x * blockDim.x)                                                   \
+    for (uint32_t i = list[r], once_ = 1; once_; once_ = 0)
+
+// z_i = (S x)_i * vf_i, left-to-right from +0.0: the arithmetic of k_spmv with
+// alpha = 0, beta = 1 and a row mask
+__global__ void k_cs_spmv(const uint64_t *ro, const uint32_t *col, const double *a,
+                          const uint32_t *list, uint32_t n, const double *x, double *z,
+                          const uint8_t *f) {
+  LIST_ROWS(r, i, list, n) {
+    double t = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++) {
+      const double p = a[k] * x[col[k]];
+      t += p;
+    }
+    double v = 1.0 * t;
+    v = v * (f[i] ? 1.0 : 0.0);
+    z[i] = v;
+  }
+}
+// w = (1./w1).*w2, w(w1==0) = 0; mask1 = w > ctol^2; x1 = g.*mask1  (k_coarsen_w + k_mask1)
+__global__ void k_cs_w_mask1(const uint32_t *list, uint32_t n, const double *w1, const double *w2,
+                             double *w, double ctol2, const double *g, uint8_t *ma, double *x1) {
+  LIST_ROWS(r, i, list, n) {
+    double t = 1. / w1[i];
+    t = t * w2[i];
+    const double wi = w1[i] == 0 ? 0. : t;
+    w[i] = wi;
+    const uint8_t m = wi > ctol2 ? 1 : 0;
+    ma[i] = m;
+    x1[i] = g[i] * (m ? 1. : 0.);
+  }
+}
+__global__ void k_cs_amax(const uint64_t *ro, const uint32_t *col, const double *a,
+                          const uint32_t *list, uint32_t n, const uint8_t *f, double tol,
+                          double *amax) {
+  LIST_ROWS(r, i, list, n) {
+    double m = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++) {
+      const double v = fabs(a[k]);
+      if (f[col[k]] != 0 && v > m) m = v;
+    }
+    amax[i] = m * tol;
+  }
+}
+__global__ void k_cs_gather(const uint64_t *tro, const uint32_t *tcol, const double *ta,
+                            const uint32_t *list, uint32_t n, const uint8_t *f, const double *x,
+                            const double *amax, double *y) {
+  LIST_ROWS(r, k, list, n) {
+    double m = -DBL_MAX;
+    if (f[k] != 0)
+      for (uint64_t t = tro[k]; t < tro[k + 1]; t++) {
+        const uint32_t i = tcol[t];
+        if (fabs(ta[t]) < amax[i]) continue;
+        const double xi = x[i];
+        if (xi > m) m = xi;
+      }
+    y[k] = m;
+  }
+}
+// mask2 = mask1 & (g - m1 >= 0); x2 = mask2 .* id   (k_mask2 without overwriting g)
+template <bool LIST>
+__global__ void k_cs_mask2(const uint32_t *list, uint32_t n, const double *g, const double *m1,
+                           const uint8_t *ma, uint8_t *mb, double *x2) {
+  GRID_STRIDE(r, n) {
+    const uint32_t i = LIST ? list[r] : (uint32_t)r;
+    const double gi = g[i] - m1[i];
+    const uint8_t mk = (ma[i] && gi >= 0.) ? 1 : 0;
+    mb[i] = mk;
+    x2[i] = (mk ? 1. : 0.) * ((double)i + 1.0);
+  }
+}
+// mask3 = mask2 & (id - m2 > 0); vc |= mask3; vf ^= mask3; new C points -> next D0
+template <bool LIST>
+__global__ void k_cs_mask3(const uint32_t *list, uint32_t n, const double *m2, const uint8_t *mb,
+                           uint8_t *vc, uint8_t *vf, double *vfd, uint32_t *anyvc,
+                           uint32_t *d0, uint32_t *d0cnt, uint32_t *stamp, uint32_t next_base) {
+  // wave-uniform trip count (wave_append needs every lane)
+  for (uint64_t rb = (uint64_t)blockIdx.x * blockDim.x; rb < (uint64_t)n;
+       rb += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = rb + threadIdx.x;
+    bool mk = false;
+    uint32_t i = 0;
+    if (r < n) {
+      i = LIST ? list[r] : (uint32_t)r;
+      const double gi = ((double)i + 1.0) - m2[i];
+      mk = mb[i] && gi > 0.;
+      if (mk) {
+        vc[i] = 1;
+        *anyvc = 1;
+        const uint8_t fv = vf[i] ? 0 : 1;
+        vf[i] = fv;
+        vfd[i] = fv ? 1. : 0.;
+        stamp[i] = next_base;
+      }
+    }
+    const unsigned pos = wave_append(d0cnt, mk);
+    if (mk) d0[pos] = i;
+  }
+}
+
+static inline int lgrid(uint32_t n) { return grid_for(n, 256, 8192); }
+
+extern "C" void amgd_cs_spmv(const dcsr *S, const uint32_t *list, uint32_t n, const double *x,
+                             double *z, const uint8_t *f) {
+  if (!list) { amgd_spmv(S, x, z, 0.0, NULL, 1.0, f); return; }
+  if (n) k_cs_spmv<<<lgrid(n), 256, 0, amgd_s()>>>(S->ro, S->col, S->a, list, n, x, z, f);
+  KCHECK();
+}
+extern "C" void amgd_cs_w_mask1(const uint32_t *list, uint32_t n, const double *w1,
+                                const double *w2, double *w, double ctol2, const double *g,
+                                uint8_t *ma, double *x1) {
+  if (!list) {
+    amgd_coarsen_w(w1, w2, w, n);
+    amgd_coarsen_mask1(w, ctol2, g, ma, x1, n);
+    return;
+  }
+  if (n) k_cs_w_mask1<<<lgrid(n), 256, 0, amgd_s()>>>(list, n, w1, w2, w, ctol2, g, ma, x1);
+  KCHECK();
+}
+extern "C" void amgd_cs_amax(const dcsr *S, const uint32_t *list, uint32_t n, const uint8_t *f,
+                             double tol, double *amax) {
+  if (!list) { amgd_mat_amax(S, f, tol, amax); return; }
+  if (n) k_cs_amax<<<lgrid(n), 256, 0, amgd_s()>>>(S->ro, S->col, S->a, list, n, f, tol, amax);
+  KCHECK();
+}
+extern "C" void amgd_cs_gather(const dcsr *St, const uint32_t *list, uint32_t n, const uint8_t *f,
+                               const double *x, const double *amax, double *y) {
+  if (!list) { amgd_mat_max_gather(St, f, x, amax, y); return; }
+  if (n)
+    k_cs_gather<<<lgrid(n), 256, 0, amgd_s()>>>(St->ro, St->col, St->a, list, n, f, x, amax, y);
+  KCHECK();
+}
+extern "C" void amgd_cs_mask2(const uint32_t *list, uint32_t n, const double *g, const double *m1,
+                              const uint8_t *ma, uint8_t *mb, double *x2) {
+  if (!n) return;
+  if (list) k_cs_mask2<true><<<lgrid(n), 256, 0, amgd_s()>>>(list, n, g, m1, ma, mb, x2);
+  else k_cs_mask2<false><<<lgrid(n), 256, 0, amgd_s()>>>(list, n, g, m1, ma, mb, x2);
+  KCHECK();
+}
+extern "C" void amgd_cs_mask3(const uint32_t *list, uint32_t n, const double *m2,
+                              const uint8_t *mb, uint8_t *vc, uint8_t *vf, double *vfd,
+                              uint32_t *anyvc, uint32_t *d0, uint32_t *d0cnt, uint32_t *stamp,
+                              uint32_t next_base) {
+  if (!n) return;
+  if (list)
+    k_cs_mask3<true><<<lgrid(n), 256, 0, amgd_s()>>>(list, n, m2, mb, vc, vf, vfd, anyvc, d0,
+                                                     d0cnt, stamp, next_base);
+  else
+    k_cs_mask3<false><<<lgrid(n), 256, 0, amgd_s()>>>(list, n, m2, mb, vc, vf, vfd, anyvc, d0,
+                                                      d0cnt, stamp, next_base);
+  KCHECK();
+}

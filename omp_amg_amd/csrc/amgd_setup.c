@@ -137,26 +137,51 @@ static dcsr *strength(const dcsr *A) {
   return S;
 }
 
+/* The sweep loop keeps one buffer per stage (g, w1, w2a, w2, w, mask1, x1, Amax,
+   m1, mask2, x2, m2) so that, after the first sweep, each stage is recomputed
+   only on the rows within its dependency radius of the previous sweep's new C
+   points (amgd_coarsen.hip); the other rows already hold the values a full
+   sweep would produce.  Large dirty sets, long-row graphs and small levels run
+   the full kernels into the same buffers.  AMGD_CS_INC=0 forces full sweeps. */
 static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
   uint32_t n = A->cn;
   dcsr *S = strength(A);
   dcsr *St = amgd_transpose(S, NULL);
-  uint8_t *vf = (uint8_t *)amgd_alloc(n + 1), *mask = (uint8_t *)amgd_alloc(n + 1);
-  double *vfd = dones(n), *g = dalloc(n), *w1 = dalloc(n), *w2 = dalloc(n), *tmp = dalloc(n);
-  double *w = dalloc(n), *x = dalloc(n), *m = dalloc(n), *amax = dalloc(n);
+  uint8_t *vf = (uint8_t *)amgd_alloc(n + 1), *ma = (uint8_t *)amgd_alloc(n + 1);
+  uint8_t *mb = (uint8_t *)amgd_alloc(n + 1);
+  double *vfd = dones(n), *g = dalloc(n), *w1 = dalloc(n), *w2a = dalloc(n), *w2 = dalloc(n);
+  double *w = dalloc(n), *x1 = dalloc(n), *x2 = dalloc(n), *m1 = dalloc(n), *m2 = dalloc(n);
+  double *amax = dalloc(n);
   uint32_t *anyvc = (uint32_t *)amgd_alloc(4);
+  uint32_t *front[2], *cnt[2], *stamp = (uint32_t *)amgd_alloc(4ull * n + 4);
+  for (int q = 0; q < 2; q++) {
+    front[q] = (uint32_t *)amgd_alloc(4ull * n + 4);
+    cnt[q] = (uint32_t *)amgd_alloc(64);
+  }
+  const char *e1 = getenv("AMGD_CS_INC"), *e2 = getenv("AMGD_CS_MIN_ROWS");
+  const uint64_t min_rows = e2 && *e2 ? strtoull(e2, NULL, 10) : 65536;
+  const int inc = !(e1 && *e1 && atoi(e1) == 0) && n >= min_rows &&
+                  S->nnz + St->nnz <= 64ull * n;
+  const uint32_t limit = n / 4;
   amgd_memset(vc, 0, n);
   amgd_memset(vf, 1, n);
   amgd_memset(anyvc, 0, 4);
-  int it = 0;
+  amgd_memset(stamp, 0, 4ull * n);
+  amgd_memset(cnt[0], 0, 64);
+  int it = 0, cur = 0;
   for (;;) {
     it++;
-    amgd_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);      /* g  = vf.*(S*vf)   */
-    amgd_spmv(S, g, w1, 0.0, NULL, 1.0, vf);       /* w1 = vf.*(S*g)    */
-    amgd_spmv(S, w1, w2, 0.0, NULL, 1.0, vf);      /* w2 = vf.*(S*w1)   */
-    amgd_spmv(S, w2, tmp, 0.0, NULL, 1.0, vf);     /* w2 = vf.*(S*w2)   */
-    SWAPD(w2, tmp);
-    amgd_coarsen_w(w1, w2, w, n);                  /* w = (1./w1).*w2   */
+    const uint32_t *L = NULL;
+    uint32_t nr[8];
+    for (int r = 0; r < 8; r++) nr[r] = n;
+    if (inc && it > 1 && amgd_cs_grow(S, St, front[cur], cnt[cur], stamp, (uint32_t)it, limit, nr))
+      L = front[cur];
+    amgd_cs_spmv(S, L, nr[1], vfd, g, vf);          /* g   = vf.*(S*vf)  */
+    amgd_cs_spmv(S, L, nr[2], g, w1, vf);           /* w1  = vf.*(S*g)   */
+    amgd_cs_spmv(S, L, nr[3], w1, w2a, vf);         /* w2a = vf.*(S*w1)  */
+    amgd_cs_spmv(S, L, nr[4], w2a, w2, vf);         /* w2  = vf.*(S*w2a) */
+    /* w = (1./w1).*w2; mask1 = w > ctol^2; x1 = mask1.*g */
+    amgd_cs_w_mask1(L, nr[4], w1, w2, w, ctol * ctol, g, ma, x1);
     uint64_t mi = 0;
     double w1m = amgd_max_first(w1, n, &mi), wm = amgd_max_first(w, n, NULL);
     double b = (w1m < wm) ? sqrt(w1m) : sqrt(wm);
@@ -167,19 +192,24 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
       if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
       break;
     }
-    amgd_coarsen_mask1(w, ctol * ctol, g, mask, x, n);
-    amgd_mat_amax(S, vf, 0.1, amax);               /* Amax: same (S, vf) for both calls */
-    amgd_mat_max_gather(St, vf, x, amax, m);       /* m = mat_max(S,vf,mask.*g)  */
-    amgd_coarsen_mask2(g, m, mask, x, n);
-    amgd_mat_max_gather(St, vf, x, amax, m);       /* m = mat_max(S,vf,mask.*id) */
-    amgd_coarsen_mask3(m, mask, vc, vf, vfd, n, anyvc);
+    amgd_cs_amax(S, L, nr[1], vf, 0.1, amax);      /* Amax: same (S, vf) for both calls */
+    amgd_cs_gather(St, L, nr[5], vf, x1, amax, m1); /* m1 = mat_max(S,vf,mask.*g)  */
+    amgd_cs_mask2(L, nr[5], g, m1, ma, mb, x2);     /* mask2 = mask1 & (g-m1>=0)   */
+    amgd_cs_gather(St, L, nr[6], vf, x2, amax, m2); /* m2 = mat_max(S,vf,mask.*id) */
+    const int nx = cur ^ 1;
+    amgd_memset(cnt[nx], 0, 64);
+    amgd_cs_mask3(L, nr[6], m2, mb, vc, vf, vfd, anyvc, front[nx], cnt[nx], stamp,
+                  (uint32_t)it + 1);
+    cur = nx;
     if (getenv("AMGD_CLOG") && (it % 10 == 1))
-      fprintf(stderr, "coarsen n %u sweep %d active %lu\n", n, it,
-              (unsigned long)amgd_u8_count(vf, n));
+      fprintf(stderr, "coarsen n %u sweep %d active %lu rows %u\n", n, it,
+              (unsigned long)amgd_u8_count(vf, n), L ? nr[6] : n);
   }
   dcsr_free(&S); dcsr_free(&St);
-  amgd_free(vf); amgd_free(mask); amgd_free(vfd); amgd_free(g); amgd_free(w1); amgd_free(w2);
-  amgd_free(tmp); amgd_free(w); amgd_free(x); amgd_free(m); amgd_free(amax); amgd_free(anyvc);
+  amgd_free(vf); amgd_free(ma); amgd_free(mb); amgd_free(vfd); amgd_free(g); amgd_free(w1);
+  amgd_free(w2a); amgd_free(w2); amgd_free(w); amgd_free(x1); amgd_free(x2); amgd_free(m1);
+  amgd_free(m2); amgd_free(amax); amgd_free(anyvc); amgd_free(stamp);
+  for (int q = 0; q < 2; q++) { amgd_free(front[q]); amgd_free(cnt[q]); }
 }
 
 /* ------------------------------------------------------------------------ */

@@ -92,3 +92,44 @@ def test_export_files_match_oracle(oracle_lib, tmp_path):
         g, o = outs["gpu"][f], outs["oracle"][f]
         assert g.shape == o.shape, f
         np.testing.assert_allclose(g, o, rtol=1e-9, atol=1e-12, err_msg=f)
+
+
+# incremental coarsening sweeps (amgd_coarsen.hip): forced on at every size, the
+# hierarchy must stay bit-identical to the reference's / the oracle's
+@pytest.mark.parametrize("case", golden_cases())
+def test_gpu_incremental_coarsen_bitexact_fixture(case, monkeypatch):
+    monkeypatch.setenv("AMGD_CS_MIN_ROWS", "0")
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("gen", [
+    ("p7_20", lambda: problems.poisson3d(20)),
+    ("aniso_16", lambda: problems.poisson3d(16, eps=1e-3)),
+    ("p27_12", lambda: problems.poisson3d(12, 27)),
+    ("sem_e3_N4", lambda: problems.sem_laplacian(3, 3, 3, 4, seed=2, jitter=0.3)),
+], ids=lambda g: g[0])
+def test_gpu_incremental_coarsen_vs_oracle(oracle_lib, gen, monkeypatch):
+    monkeypatch.setenv("AMGD_CS_MIN_ROWS", "0")
+    Ai, Aj, Av = gen[1]()
+    ref = abi.run_setup(oracle_lib, Ai, Aj, Av)
+    h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    bad = parity.compare(ref, h, exact=False, rtol=RTOL)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("m,stencil,min_rows", [(48, 7, None), (18, 27, "0")])
+def test_gpu_incremental_coarsen_matches_full_sweeps(m, stencil, min_rows, monkeypatch):
+    """default (incremental) vs AMGD_CS_INC=0 (every sweep over all rows):
+    identical hierarchies, bit for bit (48^3 is above the default threshold)"""
+    Ai, Aj, Av = problems.poisson3d(m, stencil)
+    if min_rows is not None:
+        monkeypatch.setenv("AMGD_CS_MIN_ROWS", min_rows)
+    h_inc = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    monkeypatch.setenv("AMGD_CS_INC", "0")
+    h_full = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    bad = parity.compare(h_full, h_inc, exact=True)
+    assert not bad, bad
