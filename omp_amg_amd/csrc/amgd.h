@@ -136,23 +136,39 @@ void amgd_mat_max_gather(const dcsr *St, const uint8_t *f, const double *x, cons
 void amgd_coarsen_mask2(double *g, const double *m, uint8_t *mask, double *x, uint32_t n);
 void amgd_coarsen_mask3(const double *m, uint8_t *mask, uint8_t *vc, uint8_t *vf, double *vfd,
                         uint32_t n, uint32_t *anyvc);
-/* incremental sweeps: stages over the rows within r hops of the last sweep's new
-   C points (list = that row list, n its length) or over all n rows (list = NULL) */
+/* incremental sweeps (amgd_coarsen.hip): a stage of radius R runs on the rows
+   within R hops of the last sweep's new C points -- the prefix cum[R] of the BFS
+   list (list mode) or the rows i with fs[i] - fb <= R (filter mode); rows = NULL
+   runs the full kernels */
+typedef struct {
+  const uint32_t *list;   /* BFS rows in hop order (list mode) or NULL */
+  uint32_t cum[8];        /* rows within r hops */
+  const uint32_t *fs;     /* row stamps (filter mode) */
+  uint32_t fb;            /* 8 * sweep */
+} amgd_csrows;
 int amgd_cs_grow(const dcsr *S, const dcsr *St, uint32_t *front, uint32_t *cnt_d,
-                 uint32_t *stamp, uint32_t base, uint32_t limit, uint32_t *cum);
-void amgd_cs_spmv(const dcsr *S, const uint32_t *list, uint32_t n, const double *x, double *z,
-                  const uint8_t *f);
-void amgd_cs_w_mask1(const uint32_t *list, uint32_t n, const double *w1, const double *w2,
-                     double *w, double ctol2, const double *g, uint8_t *ma, double *x1);
-void amgd_cs_amax(const dcsr *S, const uint32_t *list, uint32_t n, const uint8_t *f, double tol,
-                  double *amax);
-void amgd_cs_gather(const dcsr *St, const uint32_t *list, uint32_t n, const uint8_t *f,
-                    const double *x, const double *amax, double *y);
-void amgd_cs_mask2(const uint32_t *list, uint32_t n, const double *g, const double *m1,
-                   const uint8_t *ma, uint8_t *mb, double *x2);
-void amgd_cs_mask3(const uint32_t *list, uint32_t n, const double *m2, const uint8_t *mb,
-                   uint8_t *vc, uint8_t *vf, double *vfd, uint32_t *anyvc, uint32_t *d0,
-                   uint32_t *d0cnt, uint32_t *stamp, uint32_t next_base);
+                 uint32_t *stamp, uint32_t base8, uint32_t limit, uint32_t *cum);
+void amgd_spmv_filt(const dcsr *M, const double *x, double *z, const uint8_t *f,
+                    const uint32_t *fs, uint32_t fb, uint32_t fr);
+void amgd_mat_amax_filt(const dcsr *S, const uint8_t *f, double tol, double *amax,
+                        const uint32_t *fs, uint32_t fb, uint32_t fr);
+void amgd_mat_max_gather_filt(const dcsr *St, const uint8_t *f, const double *x,
+                              const double *amax, double *y, const uint32_t *fs, uint32_t fb,
+                              uint32_t fr);
+void amgd_cs_spmv(const dcsr *S, const double *x, double *z, const uint8_t *f,
+                  const amgd_csrows *rows, uint32_t R);
+void amgd_cs_w_mask1(uint32_t n, const double *w1, const double *w2, double *w, double ctol2,
+                     const double *g, uint8_t *ma, double *x1, const amgd_csrows *rows,
+                     uint32_t R);
+void amgd_cs_amax(const dcsr *S, const uint8_t *f, double tol, double *amax,
+                  const amgd_csrows *rows, uint32_t R);
+void amgd_cs_gather(const dcsr *St, const uint8_t *f, const double *x, const double *amax,
+                    double *y, const amgd_csrows *rows, uint32_t R);
+void amgd_cs_mask2(uint32_t n, const double *g, const double *m1, const uint8_t *ma, uint8_t *mb,
+                   double *x2, const amgd_csrows *rows, uint32_t R);
+void amgd_cs_mask3(uint32_t n, const double *m2, const uint8_t *mb, uint8_t *vc, uint8_t *vf,
+                   double *vfd, uint32_t *anyvc, uint32_t *d0, uint32_t *d0cnt, uint32_t *stamp,
+                   uint32_t next_base8, const amgd_csrows *rows, uint32_t R);
 
 /* ---------------- interpolation (amgd_interp.hip) ---------------- */
 dcsr *amgd_min_skel(const dcsr *R);

@@ -163,6 +163,9 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
   const int inc = !(e1 && *e1 && atoi(e1) == 0) && n >= min_rows &&
                   S->nnz + St->nnz <= 64ull * n;
   const uint32_t limit = n / 4;
+  /* very short rows: one thread per listed row (list mode) beats the block filter */
+  const char *e3 = getenv("AMGD_CS_LIST_NNZ");
+  const int list_mode = S->nnz <= (uint64_t)(e3 && *e3 ? atoi(e3) : 12) * n;
   amgd_memset(vc, 0, n);
   amgd_memset(vf, 1, n);
   amgd_memset(anyvc, 0, 4);
@@ -171,17 +174,21 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
   int it = 0, cur = 0;
   for (;;) {
     it++;
-    const uint32_t *L = NULL;
-    uint32_t nr[8];
-    for (int r = 0; r < 8; r++) nr[r] = n;
-    if (inc && it > 1 && amgd_cs_grow(S, St, front[cur], cnt[cur], stamp, (uint32_t)it, limit, nr))
-      L = front[cur];
-    amgd_cs_spmv(S, L, nr[1], vfd, g, vf);          /* g   = vf.*(S*vf)  */
-    amgd_cs_spmv(S, L, nr[2], g, w1, vf);           /* w1  = vf.*(S*g)   */
-    amgd_cs_spmv(S, L, nr[3], w1, w2a, vf);         /* w2a = vf.*(S*w1)  */
-    amgd_cs_spmv(S, L, nr[4], w2a, w2, vf);         /* w2  = vf.*(S*w2a) */
+    /* rows within r hops of the last sweep's new C points */
+    amgd_csrows rows_, *rows = NULL;
+    if (inc && it > 1 &&
+        amgd_cs_grow(S, St, front[cur], cnt[cur], stamp, 8u * it, limit, rows_.cum)) {
+      rows_.list = list_mode ? front[cur] : NULL;
+      rows_.fs = stamp;
+      rows_.fb = 8u * it;
+      rows = &rows_;
+    }
+    amgd_cs_spmv(S, vfd, g, vf, rows, 1);          /* g   = vf.*(S*vf)  */
+    amgd_cs_spmv(S, g, w1, vf, rows, 2);           /* w1  = vf.*(S*g)   */
+    amgd_cs_spmv(S, w1, w2a, vf, rows, 3);         /* w2a = vf.*(S*w1)  */
+    amgd_cs_spmv(S, w2a, w2, vf, rows, 4);         /* w2  = vf.*(S*w2a) */
     /* w = (1./w1).*w2; mask1 = w > ctol^2; x1 = mask1.*g */
-    amgd_cs_w_mask1(L, nr[4], w1, w2, w, ctol * ctol, g, ma, x1);
+    amgd_cs_w_mask1(n, w1, w2, w, ctol * ctol, g, ma, x1, rows, 4);
     uint64_t mi = 0;
     double w1m = amgd_max_first(w1, n, &mi), wm = amgd_max_first(w, n, NULL);
     double b = (w1m < wm) ? sqrt(w1m) : sqrt(wm);
@@ -192,18 +199,17 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
       if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
       break;
     }
-    amgd_cs_amax(S, L, nr[1], vf, 0.1, amax);      /* Amax: same (S, vf) for both calls */
-    amgd_cs_gather(St, L, nr[5], vf, x1, amax, m1); /* m1 = mat_max(S,vf,mask.*g)  */
-    amgd_cs_mask2(L, nr[5], g, m1, ma, mb, x2);     /* mask2 = mask1 & (g-m1>=0)   */
-    amgd_cs_gather(St, L, nr[6], vf, x2, amax, m2); /* m2 = mat_max(S,vf,mask.*id) */
+    amgd_cs_amax(S, vf, 0.1, amax, rows, 1);        /* Amax: same (S, vf) for both calls */
+    amgd_cs_gather(St, vf, x1, amax, m1, rows, 5);  /* m1 = mat_max(S,vf,mask.*g)  */
+    amgd_cs_mask2(n, g, m1, ma, mb, x2, rows, 5);   /* mask2 = mask1 & (g-m1>=0)   */
+    amgd_cs_gather(St, vf, x2, amax, m2, rows, 6);  /* m2 = mat_max(S,vf,mask.*id) */
     const int nx = cur ^ 1;
     amgd_memset(cnt[nx], 0, 64);
-    amgd_cs_mask3(L, nr[6], m2, mb, vc, vf, vfd, anyvc, front[nx], cnt[nx], stamp,
-                  (uint32_t)it + 1);
+    amgd_cs_mask3(n, m2, mb, vc, vf, vfd, anyvc, front[nx], cnt[nx], stamp, 8u * it + 8, rows, 6);
     cur = nx;
     if (getenv("AMGD_CLOG") && (it % 10 == 1))
       fprintf(stderr, "coarsen n %u sweep %d active %lu rows %u\n", n, it,
-              (unsigned long)amgd_u8_count(vf, n), L ? nr[6] : n);
+              (unsigned long)amgd_u8_count(vf, n), rows ? rows->cum[6] : n);
   }
   dcsr_free(&S); dcsr_free(&St);
   amgd_free(vf); amgd_free(ma); amgd_free(mb); amgd_free(vfd); amgd_free(g); amgd_free(w1);

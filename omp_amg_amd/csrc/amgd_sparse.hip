@@ -303,15 +303,21 @@ extern "C" dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask) {
 __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t *col,
                                               const double *a, uint32_t rn, const double *x,
                                               double *z, double alpha, const double *y,
-                                              double beta, const uint8_t *f) {
+                                              double beta, const uint8_t *f,
+                                              const uint32_t *fs = nullptr, uint32_t fb = 0,
+                                              uint32_t fr = 0) {
   __shared__ double pv[SPMV_CH];
   const int tid = threadIdx.x;
   for (uint64_t r0 = (uint64_t)blockIdx.x * SPMV_ROWS; r0 < rn;
        r0 += (uint64_t)gridDim.x * SPMV_ROWS) {
     const uint64_t r1 = min((uint64_t)rn, r0 + SPMV_ROWS);
-    const uint64_t b0 = ro[r0], b1 = ro[r1];
     const uint64_t i = r0 + tid;
     const bool own = i < r1;
+    // row filter (incremental coarsening): a block with no row within fr hops
+    // of the last sweep's changes skips; the others recompute every row
+    // (identical arithmetic, so clean rows are rewritten with their own values)
+    if (fs && !__syncthreads_or(own && fs[i] - fb <= fr)) continue;
+    const uint64_t b0 = ro[r0], b1 = ro[r1];
     const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
     double t = 0;
     for (uint64_t c0 = b0; c0 < b1; c0 += SPMV_CH) {
@@ -501,6 +507,16 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
     int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
     k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   }
+  KCHECK();
+}
+// rows-filtered SpMV (k_spmv arithmetic at any row length): z_i = (M x)_i * f_i on
+// the 256-row blocks holding a row i with fs[i] - fb <= fr
+extern "C" void amgd_spmv_filt(const dcsr *M, const double *x, double *z, const uint8_t *f,
+                               const uint32_t *fs, uint32_t fb, uint32_t fr) {
+  if (M->rn == 0) return;
+  int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
+  k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, 0.0, nullptr, 1.0, f, fs, fb,
+                                  fr);
   KCHECK();
 }
 // z = M^T x: rows of Mt are columns of M with rows ascending -> ordered gather

@@ -158,11 +158,13 @@ extern "C" void amgd_coarsen_mask1(const double *w, double ctol2, const double *
 template <int G>
 __global__ __launch_bounds__(256) void k_amax_g(const uint64_t *ro, const uint32_t *col,
                                                 const double *a, uint32_t rn, const uint8_t *f,
-                                                double tol, double *amax) {
+                                                double tol, double *amax,
+                                                const uint32_t *fs, uint32_t fb, uint32_t fr) {
   const uint32_t sub = threadIdx.x & (G - 1);
   const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
   for (uint64_t i = g0; i < rn; i += gs) {
+    if (fs && fs[i] - fb > fr) continue;        // row filter (group-uniform)
     double m = 0;
     for (uint64_t k = ro[i] + sub; k < ro[i + 1]; k += G) {
       double v = fabs(a[k]);
@@ -177,11 +179,14 @@ template <int G>
 __global__ __launch_bounds__(256) void k_matmax_gather_g(const uint64_t *tro, const uint32_t *tcol,
                                                          const double *ta, uint32_t n,
                                                          const uint8_t *f, const double *x,
-                                                         const double *amax, double *y) {
+                                                         const double *amax, double *y,
+                                                         const uint32_t *fs, uint32_t fb,
+                                                         uint32_t fr) {
   const uint32_t sub = threadIdx.x & (G - 1);
   const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
   for (uint64_t k = g0; k < n; k += gs) {
+    if (fs && fs[k] - fb > fr) continue;        // row filter (group-uniform)
     double m = -DBL_MAX;
     if (f[k] != 0)
       for (uint64_t t = tro[k] + sub; t < tro[k + 1]; t += G) {
@@ -217,14 +222,32 @@ static int lanes_for(uint64_t nnz, uint64_t rn) {
 extern "C" void amgd_mat_amax(const dcsr *S, const uint8_t *f, double tol, double *amax) {
   if (!S->rn) return;
   int G = lanes_for(S->nnz, S->rn);
-  MM_DISPATCH(k_amax_g, G, S->rn, S->ro, S->col, S->a, S->rn, f, tol, amax);
+  MM_DISPATCH(k_amax_g, G, S->rn, S->ro, S->col, S->a, S->rn, f, tol, amax, nullptr, 0u, 0u);
+  KCHECK();
+}
+// the same two launches restricted to rows i with fs[i] - fb <= fr
+extern "C" void amgd_mat_amax_filt(const dcsr *S, const uint8_t *f, double tol, double *amax,
+                                   const uint32_t *fs, uint32_t fb, uint32_t fr) {
+  if (!S->rn) return;
+  int G = lanes_for(S->nnz, S->rn);
+  MM_DISPATCH(k_amax_g, G, S->rn, S->ro, S->col, S->a, S->rn, f, tol, amax, fs, fb, fr);
+  KCHECK();
+}
+extern "C" void amgd_mat_max_gather_filt(const dcsr *St, const uint8_t *f, const double *x,
+                                         const double *amax, double *y, const uint32_t *fs,
+                                         uint32_t fb, uint32_t fr) {
+  if (!St->rn) return;
+  int G = lanes_for(St->nnz, St->rn);
+  MM_DISPATCH(k_matmax_gather_g, G, St->rn, St->ro, St->col, St->a, St->rn, f, x, amax, y, fs, fb,
+              fr);
   KCHECK();
 }
 extern "C" void amgd_mat_max_gather(const dcsr *St, const uint8_t *f, const double *x,
                                     const double *amax, double *y) {
   if (!St->rn) return;
   int G = lanes_for(St->nnz, St->rn);
-  MM_DISPATCH(k_matmax_gather_g, G, St->rn, St->ro, St->col, St->a, St->rn, f, x, amax, y);
+  MM_DISPATCH(k_matmax_gather_g, G, St->rn, St->ro, St->col, St->a, St->rn, f, x, amax, y,
+              nullptr, 0u, 0u);
   KCHECK();
 }
 extern "C" void amgd_mat_max(const dcsr *S, const dcsr *St, const uint8_t *f, const double *x,

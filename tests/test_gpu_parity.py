@@ -121,13 +121,18 @@ def test_gpu_incremental_coarsen_vs_oracle(oracle_lib, gen, monkeypatch):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("m,stencil,min_rows", [(48, 7, None), (18, 27, "0")])
-def test_gpu_incremental_coarsen_matches_full_sweeps(m, stencil, min_rows, monkeypatch):
+@pytest.mark.parametrize("m,stencil,min_rows,list_nnz", [
+    (48, 7, None, None), (48, 7, None, "0"), (18, 27, "0", None), (18, 27, "0", "1000")])
+def test_gpu_incremental_coarsen_matches_full_sweeps(m, stencil, min_rows, list_nnz,
+                                                     monkeypatch):
     """default (incremental) vs AMGD_CS_INC=0 (every sweep over all rows):
-    identical hierarchies, bit for bit (48^3 is above the default threshold)"""
+    identical hierarchies, bit for bit (48^3 is above the default threshold);
+    list_nnz "0" forces the block-filter mode, "1000" the row-list mode"""
     Ai, Aj, Av = problems.poisson3d(m, stencil)
     if min_rows is not None:
         monkeypatch.setenv("AMGD_CS_MIN_ROWS", min_rows)
+    if list_nnz is not None:
+        monkeypatch.setenv("AMGD_CS_LIST_NNZ", list_nnz)
     h_inc = abi.run_setup(oa.lib(), Ai, Aj, Av)
     monkeypatch.setenv("AMGD_CS_INC", "0")
     h_full = abi.run_setup(oa.lib(), Ai, Aj, Av)
