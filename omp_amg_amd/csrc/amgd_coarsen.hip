@@ -8,7 +8,7 @@
 // within 6 hops of D0; everywhere else the persistent per-stage buffers already
 // hold exactly what a full recomputation would produce.  A sweep therefore
 //   1. grows D0 hop by hop (S and S^T neighbours; the first visit claims a row
-//      with a CAS of its stamp to 8*sweep + hop),
+//      with a CAS of its stamp to 8*sweep + hop; LDS-aggregated appends),
 //   2. recomputes each stage on the rows within its radius, either
 //      * list mode (very short rows, level 0 of a 7-point grid): the BFS list is
 //        in hop order, so the rows within r hops are its prefix; one thread per
@@ -35,39 +35,47 @@
     for (uint32_t i = LIST ? list[r_] : (uint32_t)r_, once_ = 1; once_; once_ = 0)              \
       if (LIST || DIRTY(i))
 
-// one BFS hop: frontier = front[cum(r-2) .. cum(r-1)), new rows appended at cum(r-1)+
+// one BFS hop: frontier = front[cum(r-2) .. cum(r-1)), new rows appended at cum(r-1)+.
+// A thread walks one frontier row's S and S^T neighbours; claimed rows are
+// gathered in LDS and appended with one global atomic per block and chunk.
+#define HOP_CAP 4096
+__device__ __forceinline__ void cs_claim(uint32_t i, uint32_t *stamp, uint32_t key,
+                                         uint32_t base8, uint32_t *buf, uint32_t *nb,
+                                         uint32_t *front, uint32_t hi, uint32_t *cntr) {
+  const uint32_t old = stamp[i];
+  if (old >= base8 || atomicCAS(&stamp[i], old, key) != old) return;
+  const uint32_t p = atomicAdd(nb, 1u);
+  if (p < HOP_CAP) buf[p] = i;
+  else front[hi + atomicAdd(cntr, 1u)] = i;      // LDS buffer full: direct append
+}
 __global__ __launch_bounds__(256) void k_cs_hop(const uint64_t *sro, const uint32_t *scol,
                                                 const uint64_t *tro, const uint32_t *tcol,
                                                 uint32_t *front, uint32_t *cnt, int r,
                                                 uint32_t *stamp, uint32_t base8, uint32_t limit) {
+  __shared__ uint32_t buf[HOP_CAP];
+  __shared__ uint32_t nb, gbase;
   uint32_t lo = 0;
   for (int q = 0; q < r - 1; q++) lo += cnt[q];
   const uint32_t hi = lo + cnt[r - 1];
   if (hi > limit) return;                      // the host falls back to a full sweep
-  const int lane = threadIdx.x & 63;
-  const uint64_t wid = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t b = lo + wid * 64; b < hi; b += nw * 64) {
-    const uint64_t idx = b + lane;
-    const bool own = idx < hi;
-    const uint32_t j = own ? front[idx] : 0u;
-    const uint64_t s0 = own ? sro[j] : 0, s1 = own ? sro[j + 1] : 0;
-    const uint64_t t0 = own ? tro[j] : 0, t1 = own ? tro[j + 1] : 0;
-    const uint32_t ls = (uint32_t)(s1 - s0), len = ls + (uint32_t)(t1 - t0);
-    uint32_t mx = len;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
-    for (uint32_t e = 0; e < mx; e++) {
-      bool claim = false;
-      uint32_t i = 0;
-      if (e < len) {
-        i = e < ls ? scol[s0 + e] : tcol[t0 + (e - ls)];
-        const uint32_t old = stamp[i];
-        if (old < base8) claim = atomicCAS(&stamp[i], old, base8 + (uint32_t)r) == old;
-      }
-      const unsigned pos = wave_append(&cnt[r], claim);
-      if (claim) front[hi + pos] = i;
+  const uint32_t key = base8 + (uint32_t)r;
+  for (uint64_t c = lo + (uint64_t)blockIdx.x * 256; c < hi; c += (uint64_t)gridDim.x * 256) {
+    if (threadIdx.x == 0) nb = 0;
+    __syncthreads();
+    const uint64_t idx = c + threadIdx.x;
+    if (idx < hi) {
+      const uint32_t j = front[idx];
+      for (uint64_t k = sro[j]; k < sro[j + 1]; k++)
+        cs_claim(scol[k], stamp, key, base8, buf, &nb, front, hi, &cnt[r]);
+      for (uint64_t k = tro[j]; k < tro[j + 1]; k++)
+        cs_claim(tcol[k], stamp, key, base8, buf, &nb, front, hi, &cnt[r]);
     }
+    __syncthreads();
+    const uint32_t m = nb < HOP_CAP ? nb : HOP_CAP;
+    if (threadIdx.x == 0) gbase = m ? atomicAdd(&cnt[r], m) : 0u;
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < m; t += 256) front[hi + gbase + t] = buf[t];
+    __syncthreads();
   }
 }
 

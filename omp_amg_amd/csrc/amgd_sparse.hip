@@ -429,21 +429,41 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double t = 0;
     const uint32_t sub = lane & (SL_SEG - 1), grp = lane >> 4;
-    for (uint32_t off = 0; off < mx; off += SL_SEG) {
-#pragma unroll 4
-      for (int q = 0; q < 16; q++) {
-        const int rr = q * 4 + grp;
-        const uint32_t e = off + sub;
-        double v = 0.0;
-        if (e < rlen[w][rr]) {
-          const uint64_t k = rk0[w][rr] + e;
-          v = x ? a[k] * x[col[k]] : a[k];
-        }
-        buf[w][rr][sub] = v;
+    // round `off`'s products sit in v[]; the next round's (a, col) loads are
+    // issued before the lanes add the current round, so HBM latency overlaps
+    // the ordered adds (the sums and their order are unchanged)
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const int rr = q * 4 + grp;
+      v[q] = 0.0;
+      if (sub < rlen[w][rr]) {
+        const uint64_t k = rk0[w][rr] + sub;
+        v[q] = x ? a[k] * x[col[k]] : a[k];
       }
+    }
+    for (uint32_t off = 0; off < mx; off += SL_SEG) {
+#pragma unroll
+      for (int q = 0; q < 16; q++) buf[w][q * 4 + grp][sub] = v[q];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t en = off + SL_SEG + sub;
+      double an[16];
+      uint32_t cn[16];
+      bool hv[16];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int rr = q * 4 + grp;
+        hv[q] = en < rlen[w][rr];
+        an[q] = 0.0;
+        cn[q] = 0;
+        if (hv[q]) {
+          const uint64_t k = rk0[w][rr] + en;
+          an[q] = a[k];
+          if (x) cn[q] = col[k];
+        }
+      }
       if (off < len) {
         const uint32_t m = min((uint32_t)SL_SEG, len - off);
         for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
@@ -451,6 +471,8 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < 16; q++) v[q] = hv[q] ? (x ? an[q] * x[cn[q]] : an[q]) : 0.0;
     }
     if (own) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
