@@ -675,12 +675,14 @@ extern "C" void amgd_rowsum_sq_inv(const dcsr *A, double *s) {
 // mxmpoint (amg_setup.c:1807): X = A.*B on the intersection (zeros kept).
 // Count pass + scan + fill pass, one thread per row.
 // ---------------------------------------------------------------------------
+#define MPM_LONG 64   // rows with na + nb >= MPM_LONG and no repeated column: k_mpm_wave
 template <bool FILL>
 __global__ void k_mpm(const uint64_t *aro, const uint32_t *acol, const double *aa,
                       const uint64_t *bro, const uint32_t *bcol, const double *ba, uint32_t rn,
                       double alpha, double beta, uint64_t *cnt, const uint64_t *xro,
-                      uint32_t *xcol, double *xa) {
+                      uint32_t *xcol, double *xa, const uint8_t *longrow = nullptr) {
   GRID_STRIDE(i, rn) {
+    if (longrow && longrow[i]) continue;
     uint64_t ja = aro[i], ea = aro[i + 1], jb = bro[i], eb = bro[i + 1];
     uint64_t o = FILL ? xro[i] : 0, c = 0;
     while (ja < ea || jb < eb) {
@@ -713,6 +715,109 @@ __global__ void k_mpm(const uint64_t *aro, const uint32_t *acol, const double *a
     if (!FILL) cnt[i] = c;
   }
 }
+// Long rows: one wavefront per row, every entry placed by rank instead of a
+// sequential merge.  With strictly increasing columns in both rows, A entry p
+// (column c) lands at p + #B<c - #matched<c - #dropped<c and an unmatched B entry
+// q at q + #A<c - (same two counts); #B<c / #A<c come from a binary search in
+// the other row, the matched / dropped counts from wave prefix sums over the
+// row's own entries (a matched pair is dropped when alpha*a + beta*b == 0, the
+// sequential merge's test).  Values are the merge's own expressions.  A row with
+// a repeated column is flagged and left to the sequential merge.
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *c, uint32_t n, uint32_t key) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (c[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(256) void k_mpm_flag(const uint64_t *aro, const uint32_t *acol,
+                                                  const uint64_t *bro, const uint32_t *bcol,
+                                                  uint32_t rn, uint8_t *longrow) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; i < rn;
+       i += (uint64_t)gridDim.x * 4) {
+    const uint64_t ka = aro[i], na = aro[i + 1] - ka, kb = bro[i], nb = bro[i + 1] - kb;
+    if (na + nb < MPM_LONG) {
+      if (lane == 0) longrow[i] = 0;
+      continue;
+    }
+    bool dup = false;
+    for (uint64_t p = lane; p + 1 < na; p += 64) dup |= acol[ka + p] >= acol[ka + p + 1];
+    for (uint64_t q = lane; q + 1 < nb; q += 64) dup |= bcol[kb + q] >= bcol[kb + q + 1];
+    const bool anyd = __ballot(dup) != 0;
+    if (lane == 0) longrow[i] = anyd ? 0 : 1;
+  }
+}
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uint32_t *acol,
+                                                  const double *aa, const uint64_t *bro,
+                                                  const uint32_t *bcol, const double *ba,
+                                                  uint32_t rn, double alpha, double beta,
+                                                  const uint8_t *longrow, uint64_t *cnt,
+                                                  const uint64_t *xro, uint32_t *xcol,
+                                                  double *xa) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; i < rn;
+       i += (uint64_t)gridDim.x * 4) {
+    if (!longrow[i]) continue;
+    const uint64_t ka = aro[i], kb = bro[i];
+    const uint32_t na = (uint32_t)(aro[i + 1] - ka), nb = (uint32_t)(bro[i + 1] - kb);
+    const uint64_t o = FILL ? xro[i] : 0;
+    uint32_t cm = 0, cd = 0;                      // matched / dropped so far (A side)
+    for (uint32_t p0 = 0; p0 < na; p0 += 64) {
+      const uint32_t p = p0 + lane;
+      bool has = p < na, m = false, d = false;
+      uint32_t c = 0, bs = 0;
+      double v = 0.0;
+      if (has) {
+        c = acol[ka + p];
+        bs = lower_bound_u32(bcol + kb, nb, c);
+        m = bs < nb && bcol[kb + bs] == c;
+        if (m) {
+          v = alpha * aa[ka + p] + beta * ba[kb + bs];
+          d = !(v != 0.0);
+        } else if (FILL) {
+          v = alpha * aa[ka + p];
+        }
+      }
+      const uint64_t bm = __ballot(m), bd = __ballot(d);
+      if (FILL && has && !d) {
+        const uint64_t pos = (uint64_t)p + bs - (cm + __popcll(bm & lt)) - (cd + __popcll(bd & lt));
+        xcol[o + pos] = c;
+        xa[o + pos] = v;
+      }
+      cm += __popcll(bm);
+      cd += __popcll(bd);
+    }
+    if (!FILL) {
+      if (lane == 0) cnt[i] = (uint64_t)na + nb - cm - cd;
+      continue;
+    }
+    uint32_t bmc = 0, bdc = 0;                    // matched / dropped so far (B side)
+    for (uint32_t q0 = 0; q0 < nb; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      bool has = q < nb, m = false, d = false;
+      uint32_t c = 0, as = 0;
+      if (has) {
+        c = bcol[kb + q];
+        as = lower_bound_u32(acol + ka, na, c);
+        m = as < na && acol[ka + as] == c;
+        if (m) d = !((alpha * aa[ka + as] + beta * ba[kb + q]) != 0.0);
+      }
+      const uint64_t bm = __ballot(m), bd = __ballot(d);
+      if (has && !m) {
+        const uint64_t pos =
+            (uint64_t)q + as - (bmc + __popcll(bm & lt)) - (bdc + __popcll(bd & lt));
+        xcol[o + pos] = c;
+        xa[o + pos] = beta * ba[kb + q];
+      }
+      bmc += __popcll(bm);
+      bdc += __popcll(bd);
+    }
+  }
+}
 extern "C" dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *B) {
   if (A->rn != B->rn || A->cn != B->cn) {
     fprintf(stderr, "omp_amg_amd: mpm dimension mismatch (%u x %u vs %u x %u)\n", A->rn, A->cn,
@@ -720,20 +825,36 @@ extern "C" dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *
     abort();
   }
   hipStream_t s = amgd_s();
+  static int wave = -1;
+  if (wave < 0) wave = getenv("AMGD_MPM_WAVE") ? atoi(getenv("AMGD_MPM_WAVE")) : 1;
+  // the wave kernel pays for rows averaging >= MPM_LONG / 4 entries
+  const bool use_w = wave && A->rn && (A->nnz + B->nnz) >= (uint64_t)A->rn * (MPM_LONG / 4);
+  uint8_t *lr = nullptr;
+  const int gw = (int)std::min<uint64_t>(((uint64_t)A->rn + 3) / 4, 65536);
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
+  if (use_w) {
+    lr = (uint8_t *)amgd_alloc((size_t)A->rn + 1);
+    k_mpm_flag<<<gw, 256, 0, s>>>(A->ro, A->col, B->ro, B->col, A->rn, lr);
+    k_mpm_wave<false><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn, alpha,
+                                         beta, lr, cnt, nullptr, nullptr, nullptr);
+  }
   if (A->rn)
     k_mpm<false><<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn,
-                                                  alpha, beta, cnt, nullptr, nullptr, nullptr);
+                                                  alpha, beta, cnt, nullptr, nullptr, nullptr, lr);
   KCHECK();
   uint64_t nz = amgd_scan_u64(cnt, A->rn);
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
   X->a = (double *)amgd_alloc(nz * 8 + 8);
+  if (use_w)
+    k_mpm_wave<true><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn, alpha,
+                                        beta, lr, nullptr, X->ro, X->col, X->a);
   if (A->rn)
     k_mpm<true><<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn,
-                                                 alpha, beta, nullptr, X->ro, X->col, X->a);
+                                                 alpha, beta, nullptr, X->ro, X->col, X->a, lr);
   KCHECK();
+  if (lr) amgd_free(lr);
   return X;
 }
 

@@ -397,3 +397,29 @@ def test_expand_pick(case):
         X.a[::5] = 0.0
     assert oa.test_csr_op(6, X).nnz == refops.expand_pick(X).nnz
     assert refops.same(oa.test_csr_op(6, X), refops.expand_pick(X))
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_mpm_long_rows_rank_placement(seed):
+    """rows of >= 64 merged entries take the wave-per-row rank placement:
+    disjoint, overlapping and cancelling (exact-zero dropped) entries, short rows
+    mixed in, and a row with a repeated column (left to the sequential merge)"""
+    rng = np.random.default_rng(seed)
+    A = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
+    C = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
+    # B: A's pattern, half the values equal (A - B cancels there), plus C's entries
+    a2 = A.a.copy()
+    flip = rng.random(len(a2)) < 0.5
+    a2[flip] += 1.0
+    B = refops.Csr(A.rn, A.cn, A.row_off.copy(), A.col.copy(), a2)
+    BC = refops.mpm(1.0, B, 1.0, C)
+    for (x, al, y, be) in [(A, 1.0, C, 1.0), (A, 1.0, A, -1.0), (A, 1.0, BC, -1.0),
+                           (BC, 2.0, A, 0.5)]:
+        assert refops.same(oa.test_csr_op(2, x, y, al, be), refops.mpm(al, x, be, y))
+    # a repeated column in one long row
+    col = A.col.copy()
+    s, e = A.row_off[7], A.row_off[8]
+    if e - s >= 2:
+        col[s + 1] = col[s]
+    D = refops.Csr(A.rn, A.cn, A.row_off.copy(), col, A.a.copy())
+    assert refops.same(oa.test_csr_op(2, D, C, 1.0, -1.0), refops.mpm(1.0, D, -1.0, C))
