@@ -183,10 +183,14 @@ extern "C" dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *v
 // perm_out (optional) maps CSC position -> CSR position.
 // ---------------------------------------------------------------------------
 __global__ void k_iota_u64(uint64_t *p, uint64_t n) { GRID_STRIDE(i, n) p[i] = i; }
-__global__ void k_tr_fill(const uint64_t *perm, const uint32_t *row, const double *a, uint64_t nz,
+__global__ void k_iota_u32(uint32_t *p, uint64_t n) { GRID_STRIDE(i, n) p[i] = (uint32_t)i; }
+// P = u64 (perm handed back to the caller) or u32 (nnz < 2^32, perm internal:
+// a third less radix-sort traffic and a narrower perm read here)
+template <typename P>
+__global__ void k_tr_fill(const P *perm, const uint32_t *row, const double *a, uint64_t nz,
                           uint32_t *tcol, double *ta) {
   GRID_STRIDE(t, nz) {
-    uint64_t p = perm[t];
+    const uint64_t p = perm[t];
     tcol[t] = row[p];
     ta[t] = a[p];
   }
@@ -221,18 +225,31 @@ __global__ void k_ro_gaps(const unsigned *ngap, const uint64_t *gaps, uint64_t *
 extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   hipStream_t s = amgd_s();
   uint64_t nz = A->nnz;
+  const bool narrow = !perm_out && nz < (1ull << 32);
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->cn + 1) * 8);
-  uint64_t *perm = (uint64_t *)amgd_alloc(nz * 8 + 8);
+  void *perm = amgd_alloc(nz * (narrow ? 4 : 8) + 8);
   if (!nz) HIPCK(hipMemsetAsync(cnt, 0, ((size_t)A->cn + 1) * 8, s));
   if (nz) {
-    uint64_t *iota = (uint64_t *)amgd_alloc(nz * 8 + 8);
+    void *iota = amgd_alloc(nz * (narrow ? 4 : 8) + 8);
     uint32_t *kout = (uint32_t *)amgd_alloc(nz * 4 + 4);
-    k_iota_u64<<<grid_for(nz), 256, 0, s>>>(iota, nz);
     size_t tb = 0;
     int eb = bits_for(A->cn);
-    HIPCK(rocprim::radix_sort_pairs(nullptr, tb, A->col, kout, iota, perm, (size_t)nz, 0, eb, s));
-    void *tmp = amgd_alloc(tb + 16);
-    HIPCK(rocprim::radix_sort_pairs(tmp, tb, A->col, kout, iota, perm, (size_t)nz, 0, eb, s));
+    void *tmp;
+    if (narrow) {
+      k_iota_u32<<<grid_for(nz), 256, 0, s>>>((uint32_t *)iota, nz);
+      HIPCK(rocprim::radix_sort_pairs(nullptr, tb, A->col, kout, (uint32_t *)iota,
+                                      (uint32_t *)perm, (size_t)nz, 0, eb, s));
+      tmp = amgd_alloc(tb + 16);
+      HIPCK(rocprim::radix_sort_pairs(tmp, tb, A->col, kout, (uint32_t *)iota, (uint32_t *)perm,
+                                      (size_t)nz, 0, eb, s));
+    } else {
+      k_iota_u64<<<grid_for(nz), 256, 0, s>>>((uint64_t *)iota, nz);
+      HIPCK(rocprim::radix_sort_pairs(nullptr, tb, A->col, kout, (uint64_t *)iota,
+                                      (uint64_t *)perm, (size_t)nz, 0, eb, s));
+      tmp = amgd_alloc(tb + 16);
+      HIPCK(rocprim::radix_sort_pairs(tmp, tb, A->col, kout, (uint64_t *)iota, (uint64_t *)perm,
+                                      (size_t)nz, 0, eb, s));
+    }
     {
       // a run of > RO_GAP empty columns needs > RO_GAP columns: at most cn / RO_GAP + 1 runs
       const uint64_t maxg = (uint64_t)A->cn / RO_GAP + 2;
@@ -254,11 +271,16 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   if (nz) {
     uint32_t *row = (uint32_t *)amgd_alloc(nz * 4 + 4);
     k_row_of_entry<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
-    k_tr_fill<<<grid_for(nz), 256, 0, s>>>(perm, row, A->a, nz, T->col, T->a);
+    if (narrow)
+      k_tr_fill<uint32_t><<<grid_for(nz), 256, 0, s>>>((const uint32_t *)perm, row, A->a, nz,
+                                                       T->col, T->a);
+    else
+      k_tr_fill<uint64_t><<<grid_for(nz), 256, 0, s>>>((const uint64_t *)perm, row, A->a, nz,
+                                                       T->col, T->a);
     KCHECK();
     amgd_free(row);
   }
-  if (perm_out) *perm_out = perm;
+  if (perm_out) *perm_out = (uint64_t *)perm;
   else amgd_free(perm);
   return T;
 }
