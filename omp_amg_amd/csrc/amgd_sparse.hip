@@ -488,7 +488,16 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
       }
       if (off < len) {
         const uint32_t m = min((uint32_t)SL_SEG, len - off);
-        for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+        if (m == SL_SEG) {
+          // full segment: all LDS reads issued before the ordered adds
+          double u[SL_SEG];
+#pragma unroll
+          for (int e = 0; e < SL_SEG; e++) u[e] = buf[w][lane][e];
+#pragma unroll
+          for (int e = 0; e < SL_SEG; e++) t += u[e];
+        } else {
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
