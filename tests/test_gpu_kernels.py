@@ -90,11 +90,12 @@ def test_spgemm_kseq_long_b_rows(case, win):
 
 
 @pytest.mark.parametrize("wsym", [0, 32768, 65536])
-@pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows"])
+@pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
 def test_spgemm_symbolic_windows(case, wsym):
     """symbolic pass of rows with many products: LDS hash (0) or byte-map column windows
     (several windows per row; A rows past the layer table fall back to the slab recount)"""
-    rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54}[case])
+    rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54,
+                                 "gapped": 55}[case])
     if case == "wide":
         A = refops.rand_csr(rng, 200, 150, 0.04)
         B = refops.rand_csr(rng, 150, 6000, 0.1)
@@ -104,6 +105,11 @@ def test_spgemm_symbolic_windows(case, wsym):
     elif case == "wide_span":
         A = refops.rand_csr(rng, 12, 600, 0.5, ints=True)
         B = refops.rand_csr(rng, 600, 200000, 0.0015, ints=True)
+    elif case == "gapped":      # column clusters far apart: windows with no column are skipped
+        A = refops.rand_csr(rng, 30, 300, 0.3, ints=True)
+        B = refops.rand_csr(rng, 300, 6000, 0.02, ints=True)
+        shift = np.array([0, 70000, 250000, 1000000])[B.col // 1500]
+        B = refops.Csr(B.rn, 1006000, B.row_off, B.col + shift, B.a)
     else:                       # 1100-1300 entries per A row
         A = refops.rand_csr(rng, 4, 1400, 0.85)
         B = refops.rand_csr(rng, 1400, 3000, 0.03)
