@@ -39,8 +39,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1)
-    p.add_argument("--warmup", type=int, default=0)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--budget-s", type=float, default=450.0,
+                   help="wall-time budget of the whole run (s): warmup and timed steps stop early "
+                        "when one more step would pass it; `steps`/`warmup` report what ran")
     p.add_argument("--m", type=int, default=256, help="grid edge (configs[1]: 256)")
     p.add_argument("--stencil", type=int, default=7)
     p.add_argument("--fast-dots", action="store_true",
@@ -49,6 +52,8 @@ def parse():
     p.add_argument("--cpu-m", type=int, default=20,
                    help="reference CPU sample grid edge (20: a size the reference terminates on)")
     p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--cpu-budget-s", type=float, default=45.0,
+                   help="cap on the total time of the CPU baseline (all child runs)")
     p.add_argument("--cpu-child", nargs=2, type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic", type=float, default=None,
                    help="RAP HBM bytes per launch from a rocprofv3 PMC pass (profiles/)")
@@ -72,7 +77,7 @@ def cpu_child(m, reps):
     print(json.dumps({"kind": kind, "secs": dt, "rows": m ** 3, "reps": reps, "levels": h.nlevels}))
 
 
-def cpu_baseline(m, reps):
+def cpu_baseline(m, reps, budget_s):
     """The reference's own serial setup (oracle/_ref/libref_amg.so, compiled from
     /root/reference by oracle/Makefile) on a bounded sample, in a child process:
     the reference crashes or never terminates on many inputs (DESIGN.md
@@ -83,12 +88,14 @@ def cpu_baseline(m, reps):
             or os.path.exists(os.path.join(ROOT, "oracle", "build", "liboracle.so"))):
         return None
     secs, done, fails, d = 0.0, 0, 0, None
+    deadline = time.time() + budget_s
     for _ in range(3 * reps):          # each rep in its own process: the reference's heap
-        if done == reps:               # overruns make it crash now and then on 7-point grids
+        left = deadline - time.time()  # overruns make it crash now and then on 7-point grids
+        if done == reps or left < 5:
             break
         try:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", str(m), "1"],
-                               capture_output=True, text=True, timeout=240)
+                               capture_output=True, text=True, timeout=left)
             d = json.loads(r.stdout.strip().splitlines()[-1])
             secs += d["secs"]
             done += 1
@@ -96,7 +103,8 @@ def cpu_baseline(m, reps):
             fails += 1
     if done == 0:
         return {"value": None, "unit": "rows/s", "cores": 1, "kind": "reference",
-                "sample": f"reference serial setup on 3D 7-point Poisson {m}^3 crashed {fails}x"}
+                "sample": f"reference serial setup on 3D 7-point Poisson {m}^3: no run finished within "
+                          f"{budget_s:.0f} s ({fails} crashed / timed out)"}
     d["reps"], d["secs"] = done, secs
     return {"value": d["rows"] * d["reps"] / d["secs"], "unit": "rows/s", "cores": 1, "kind": d["kind"],
             "sample": f"3D 7-point Poisson {m}^3 ({d['rows']} rows, {d['levels']} levels) x{d['reps']}, "
@@ -120,13 +128,19 @@ def heartbeat(period=30.0):
 
 def main():
     args = parse()
+    if args.steps < 1:
+        sys.exit("bench.py: --steps must be >= 1")
     if args.cpu_child:
         cpu_child(*args.cpu_child)
         return
+    t_start = time.time()
     hb = heartbeat()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; for N>1 launch under "
+                 f"python -m torch.distributed.run --nproc-per-node {args.gpus} ... bench.py --gpus {args.gpus}")
     dist = None
     if world > 1:
         import torch
@@ -149,16 +163,44 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
+    def agree(flag):
+        """all ranks take the same continue/stop decision (max over ranks)"""
+        if dist is None:
+            return flag
+        import torch
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return bool(t.item() > 0)
+
+    # Wall-time budget: the CPU baseline's cap is reserved up front; a warmup or
+    # timed step starts only if the estimate of one step still fits.  Warmup may
+    # use at most a quarter of what is left, and at least one timed step always runs.
+    reserve = 0.0 if (args.no_cpu_baseline or world > 1) else args.cpu_budget_s + 5.0
+    deadline = t_start + args.budget_s - reserve
+    t_step = 0.0
+    warm = 0
+    warm_deadline = time.time() + 0.25 * max(0.0, deadline - time.time())
+    while warm < args.warmup and (warm == 0 or not agree(time.time() + t_step > warm_deadline)):
+        t1 = time.perf_counter()
         ds.run(exact_dots=not args.fast_dots)
+        t_step = time.perf_counter() - t1
+        warm += 1
     barrier()
     rap_ms, rap_bytes, rap_nnz, st = 0.0, 0, 0, None
+    steps = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    while steps < args.steps:
+        if steps > 0 and agree(time.time() + t_step > deadline):
+            break
+        t1 = time.perf_counter()
         st = ds.run(exact_dots=not args.fast_dots)
+        t_step = time.perf_counter() - t1
+        steps += 1
         rap_ms += st["rap_kernel_ms"]
         rap_bytes += st["rap_bytes"]
         rap_nnz += st["rap_out_nnz"]
+        if rank == 0:
+            print(f"[bench] step {steps}: {t_step:.2f} s", file=sys.stderr, flush=True)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -166,8 +208,8 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ms_per_step = dt * 1e3 / args.steps
-    value = world * rows * args.steps / dt
+    ms_per_step = dt * 1e3 / steps
+    value = world * rows * steps / dt
 
     if rank == 0:
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
@@ -176,8 +218,11 @@ def main():
             "value": value,
             "unit": "rows/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
+            "steps": steps,
+            "warmup": warm,
+            "steps_requested": args.steps,
+            "warmup_requested": args.warmup,
+            "budget_s": args.budget_s,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
@@ -198,11 +243,11 @@ def main():
                          "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",
-                         "algorithmic_bytes_per_setup": rap_bytes / args.steps,
-                         "kernel_ms_per_setup": rap_ms / args.steps},
+                         "algorithmic_bytes_per_setup": rap_bytes / steps,
+                         "kernel_ms_per_setup": rap_ms / steps},
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps, args.cpu_budget_s)
         print(json.dumps(out), flush=True)
     ds.close()
     # (no amgd_shutdown here: the process exits and the driver reclaims everything;

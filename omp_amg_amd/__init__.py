@@ -79,6 +79,11 @@ def lib() -> C.CDLL:
                                     C.c_double, C.POINTER(HCsr)]
         L.amgd_test_spmv.argtypes = [C.POINTER(HCsr), C.c_void_p, C.c_double, C.c_void_p,
                                      C.c_double, C.c_void_p]
+        L.amgd_test_spmv_f.argtypes = [C.POINTER(HCsr), C.c_void_p, C.c_double, C.c_void_p,
+                                       C.c_double, C.c_void_p, C.c_void_p]
+        L.amgd_test_spmv_rows.argtypes = [C.POINTER(HCsr), C.c_void_p, C.c_uint32, C.c_void_p,
+                                          C.c_void_p]
+        L.amgd_test_spmv_sl_min.argtypes = [C.c_int64]
         L.amgd_test_build.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.POINTER(HCsr)]
         L.amgd_test_math.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -207,6 +212,43 @@ def test_spmv(A: abi.Csr, x, alpha=0.0, y=None, beta=1.0):
     lib().amgd_test_spmv(C.byref(ha), x.ctypes.data, alpha, None if yy is None else yy.ctypes.data,
                          beta, z.ctypes.data)
     return z
+
+
+def test_spmv_f(A: abi.Csr, x=None, alpha=0.0, y=None, beta=1.0, f=None):
+    """amgd_spmv with every option (x None: ordered row sums; f: u8 row mask)"""
+    init()
+    ha = _to_hcsr(A.row_off, A.col, A.a, A.rn, A.cn)
+    xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+    yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64)
+    ff = None if f is None else np.ascontiguousarray(f, dtype=np.uint8)
+    z = np.zeros(A.rn)
+    rc = lib().amgd_test_spmv_f(C.byref(ha), None if xx is None else xx.ctypes.data, alpha,
+                                None if yy is None else yy.ctypes.data, beta,
+                                None if ff is None else ff.ctypes.data, z.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("amgd_test_spmv_f failed")
+    return z
+
+
+def test_spmv_rows(A: abi.Csr, rows, x=None, z0=None):
+    """amgd_spmv_rows: products (x None: ordered sums) of the listed rows only; the
+    other entries of z keep z0"""
+    init()
+    ha = _to_hcsr(A.row_off, A.col, A.a, A.rn, A.cn)
+    rows = np.ascontiguousarray(rows, dtype=np.uint32)
+    xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+    z = np.zeros(A.rn) if z0 is None else np.array(z0, dtype=np.float64)
+    rc = lib().amgd_test_spmv_rows(C.byref(ha), rows.ctypes.data, len(rows),
+                                   None if xx is None else xx.ctypes.data, z.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("amgd_test_spmv_rows failed")
+    return z
+
+
+def spmv_sl_min(n: int) -> None:
+    """row count from which whole-matrix and listed-row SpMVs with long rows run lane-per-row
+    (0: always; -1: environment / default).  Same sums either way."""
+    lib().amgd_test_spmv_sl_min(int(n))
 
 
 def test_build(Ai, Aj, Av) -> abi.Csr:

@@ -510,6 +510,9 @@ static dcsr *find_support(const dcsr *R, double goal) {
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     ns += nsel;
+    if (getenv("AMGD_FSLOG"))
+      fprintf(stderr, "fs L%d nf %u nc %u nnz %lu it %d sel %u rem %u theta %g\n", g_lvl, nf, nc,
+              (unsigned long)R->nnz, it, nsel, nrem, theta);
     ph(PH_FS_SEL);
     if (nrem == 0) { g_ub++; break; }                    /* no progress: reference loops */
     if (ns + nc > cap) { g_ub++; break; }

@@ -423,7 +423,21 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
 // left-to-right sum and all 64 lanes add at once (k_spmv_wave leaves 63 idle).
 // LIST: the rows are list[0..n) instead of 0..n.
 #define SL_SEG 16
-#define SL_MIN_ROWS 65536   // >= 1024 wavefronts of 64 rows: enough to fill 256 CUs
+// Row-count thresholds from which the lane-per-row kernel runs (the sums are the
+// same either way; only speed differs):
+//  * listed rows (amgd_spmv_rows): 65536 = 1024 wavefronts of 64 rows, enough to
+//    fill 256 CUs;  AMGD_SL_LIST_MIN_ROWS overrides
+//  * whole matrices with long rows (amgd_spmv): 2^20 -- wave-per-row below that
+//    measured faster at 256^3 (setup 38.7 -> 38.3 s);  AMGD_SL_MIN_ROWS overrides
+// amgd_spmv_set_sl_min() (tests) forces both; -1 returns to the environment/default.
+static int64_t g_sl_forced = -1;
+static int64_t sl_env(const char *name, int64_t dflt) {
+  const char *e = getenv(name);
+  return e && *e ? atoll(e) : dflt;
+}
+static int64_t sl_min_whole() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_MIN_ROWS", 1 << 20); }
+static int64_t sl_min_list() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_LIST_MIN_ROWS", 65536); }
+extern "C" void amgd_spmv_set_sl_min(int64_t n) { g_sl_forced = n < 0 ? -1 : n; }
 template <bool LIST>
 __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
@@ -527,7 +541,7 @@ __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, cons
 extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x,
                                double *z) {
   if (!n) return;
-  if (n < SL_MIN_ROWS) {          // too few rows to fill the chip one row per lane
+  if ((int64_t)n < sl_min_list()) {          // too few rows to fill the chip one row per lane
     int g = (int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536);
     k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
     KCHECK();
@@ -549,10 +563,7 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
     KCHECK();
     return;
   }
-  static int64_t sl_min = -1;
-  // products of whole matrices: wave-per-row below 2^20 rows measured faster at 256^3
-  // (setup 38.7 -> 38.3 s; AMGD_SL_MIN_ROWS overrides, same sums either way)
-  if (sl_min < 0) sl_min = getenv("AMGD_SL_MIN_ROWS") ? atoll(getenv("AMGD_SL_MIN_ROWS")) : (1 << 20);
+  const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     int g = (int)std::min<uint64_t>(((uint64_t)M->rn + 255) / 256, 16384);
     k_spmv_lane<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z, alpha,

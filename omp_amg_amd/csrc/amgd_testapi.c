@@ -159,3 +159,44 @@ API void amgd_test_spgemm_win(int w) { amgd_spgemm_set_win(w); }
 /* symbolic pass of rows with many products: 0 (LDS hash), 32768 / 65536 (byte-map windows) */
 extern void amgd_spgemm_set_wsym(int w);
 API void amgd_test_spgemm_wsym(int w) { amgd_spgemm_set_wsym(w); }
+/* SpMV: row count from which the lane-per-row kernel runs, for whole-matrix and
+   listed-row products alike (0 = always, -1 = environment / default) */
+extern void amgd_spmv_set_sl_min(int64_t n);
+API void amgd_test_spmv_sl_min(int64_t n) { amgd_spmv_set_sl_min(n); }
+/* amgd_spmv with every option: x NULL = ordered row sums, y / f optional (f: u8 row mask) */
+API int amgd_test_spmv_f(const hcsr *HA, const double *x, double alpha, const double *y, double beta,
+                         const uint8_t *f, double *z) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA);
+  double *dx = NULL, *dy = NULL, *dz = (double *)amgd_alloc((size_t)HA->rn * 8 + 8);
+  uint8_t *df = NULL;
+  if (x) { dx = (double *)amgd_alloc((size_t)HA->cn * 8 + 8); amgd_h2d(dx, x, (size_t)HA->cn * 8); }
+  if (y) { dy = (double *)amgd_alloc((size_t)HA->rn * 8 + 8); amgd_h2d(dy, y, (size_t)HA->rn * 8); }
+  if (f) { df = (uint8_t *)amgd_alloc((size_t)HA->rn + 8); amgd_h2d(df, f, HA->rn); }
+  amgd_spmv(A, dx, dz, alpha, dy, beta, df);
+  amgd_d2h(z, dz, (size_t)HA->rn * 8);
+  if (dx) amgd_free(dx);
+  if (dy) amgd_free(dy);
+  if (df) amgd_free(df);
+  amgd_free(dz);
+  dcsr_free(&A);
+  return 0;
+}
+
+/* amgd_spmv_rows: z[list[r]] = (A x)[list[r]] (x NULL: row sums); other rows of z keep
+   their input values */
+API int amgd_test_spmv_rows(const hcsr *HA, const uint32_t *list, uint32_t n, const double *x, double *z) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA);
+  double *dx = NULL, *dz = (double *)amgd_alloc((size_t)HA->rn * 8 + 8);
+  uint32_t *dl = (uint32_t *)amgd_alloc((size_t)n * 4 + 8);
+  if (x) { dx = (double *)amgd_alloc((size_t)HA->cn * 8 + 8); amgd_h2d(dx, x, (size_t)HA->cn * 8); }
+  amgd_h2d(dz, z, (size_t)HA->rn * 8);
+  amgd_h2d(dl, list, (size_t)n * 4);
+  amgd_spmv_rows(A, dl, n, dx, dz);
+  amgd_d2h(z, dz, (size_t)HA->rn * 8);
+  if (dx) amgd_free(dx);
+  amgd_free(dz); amgd_free(dl);
+  dcsr_free(&A);
+  return 0;
+}

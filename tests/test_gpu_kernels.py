@@ -168,10 +168,9 @@ def test_spmv_ordered():
     assert np.array_equal(oa.test_spmv(L, xl), refops.spmv(L, xl))
 
 
-def test_spmv_lane_ragged():
-    """lane-per-row kernel (mean row >= 32): ragged rows, empty rows, rows shorter and
-    longer than its 16-entry rounds, 64-row groups that end mid-wave"""
-    rng = np.random.default_rng(23)
+def _ragged_long_rows(rng):
+    """mean row >= 32: ragged rows, empty rows, rows shorter and longer than the lane
+    kernel's 16-entry rounds; 1037 rows, so 64-row groups end mid-wave"""
     rn, cn = 1000 + 37, 3000
     ro, cols, vals = [0], [], []
     for i in range(rn):
@@ -183,10 +182,55 @@ def test_spmv_lane_ragged():
     L = refops.Csr(rn, cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64),
                    np.array(vals))
     assert L.a.size >= 32 * rn
+    return L
+
+
+def _rowsums(L):
+    return refops.spmv(L, np.ones(L.cn))          # a*1.0 == a: the ordered row sums
+
+
+@pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
+def test_spmv_long_rows_ragged(sl_min):
+    """long-row SpMV kernels on ragged rows: wave-per-row (default below 2^20 rows) and
+    lane-per-row (forced with the row threshold at 0), with and without y, the f row
+    mask and x = NULL (ordered row sums)"""
+    rng = np.random.default_rng(31)
+    L = _ragged_long_rows(np.random.default_rng(23))
+    rn, cn = L.rn, L.cn
     x = rng.standard_normal(cn)
     y = rng.standard_normal(rn)
-    assert np.array_equal(oa.test_spmv(L, x), refops.spmv(L, x))
-    assert np.array_equal(oa.test_spmv(L, x, 1.0, y, -1.0), refops.spmv(L, x, 1.0, y, -1.0))
+    f = (rng.random(rn) < 0.7).astype(np.uint8)
+    oa.spmv_sl_min(sl_min)
+    try:
+        assert np.array_equal(oa.test_spmv(L, x), refops.spmv(L, x))
+        assert np.array_equal(oa.test_spmv(L, x, 1.0, y, -1.0), refops.spmv(L, x, 1.0, y, -1.0))
+        assert np.array_equal(oa.test_spmv_f(L, x, 1.0, y, -1.0, f),
+                              refops.spmv(L, x, 1.0, y, -1.0) * (f != 0))
+        assert np.array_equal(oa.test_spmv_f(L, None), _rowsums(L))
+    finally:
+        oa.spmv_sl_min(-1)
+
+
+@pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
+def test_spmv_rows_listed(sl_min):
+    """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
+    threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
+    rng = np.random.default_rng(29)
+    L = _ragged_long_rows(np.random.default_rng(23))
+    x = rng.standard_normal(L.cn)
+    rows = np.sort(rng.choice(L.rn, size=700, replace=False)).astype(np.uint32)
+    rows = np.concatenate([rows[1::2], rows[::2]])               # unsorted list
+    z0 = np.full(L.rn, -7.25)
+    want = z0.copy()
+    want[rows] = refops.spmv(L, x)[rows]
+    want_s = z0.copy()
+    want_s[rows] = _rowsums(L)[rows]
+    oa.spmv_sl_min(sl_min)
+    try:
+        assert np.array_equal(oa.test_spmv_rows(L, rows, x, z0), want)
+        assert np.array_equal(oa.test_spmv_rows(L, rows, None, z0), want_s)
+    finally:
+        oa.spmv_sl_min(-1)
 
 
 def test_min_skel():

@@ -42,6 +42,21 @@ def test_gpu_bitexact_vs_reference_fixture(case):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("case", ["p27_8", "sem_e3_N2", "p7_14", "aniso_12"])
+def test_gpu_bitexact_lane_spmv_forced(case):
+    """every SpMV with long rows (whole-matrix and listed rows) through the lane-per-row
+    kernel, which by default runs only from 2^20 / 65536 rows: hierarchy still bit-exact"""
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    oa.spmv_sl_min(0)
+    try:
+        h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    finally:
+        oa.spmv_sl_min(-1)
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("gen", [
     ("p7_20", lambda: problems.poisson3d(20)),
     ("p7_24x20x16", lambda: problems.poisson3d(16, mx=24, my=20)),
