@@ -7,9 +7,12 @@ workload: BASELINE.json configs[1] -- 3D 7-point Poisson 256^3 CSR (16.7M rows,
           coarsening, Chebyshev/Lanczos smoother, energy-minimising interpolation,
           Galerkin RAP for every level) from a device-resident COO matrix to a
           hierarchy resident in HBM.  Inputs are uploaded before the timed region.
-value   : whole-job rows/s = (ranks x rows) / max-over-ranks seconds per step.
-          Round 1 runs one independent replica per GPU (DESIGN.md "Multi-GPU:
-          replicas only"), so scaling is "weak".
+value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup of
+          the same matrix row-sharded over the N GPUs (--mode shard, default): the
+          heavy row-independent kernels are split by work and completed by RCCL
+          allgatherv over xGMI, value = rows / max-over-ranks seconds, scaling
+          "strong"; --mode replicas runs N independent setups (value = N x rows /
+          max time, scaling "weak").
 roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
           and AfP = Af W; instantiated with RAP=1 so rocprof lists them apart;
           k_sg_kseq for long B-operand rows, k_sg_row for short ones, k_sg_win
@@ -44,6 +47,11 @@ def parse():
     p.add_argument("--budget-s", type=float, default=450.0,
                    help="wall-time budget of the whole run (s): warmup and timed steps stop early "
                         "when one more step would pass it; `steps`/`warmup` report what ran")
+    p.add_argument("--mode", choices=["shard", "replicas"], default="shard",
+                   help="N>1: one row-sharded setup (strong scaling) or N independent replicas")
+    p.add_argument("--transport", choices=["rccl", "host"], default="rccl",
+                   help="shard mode data path: RCCL over xGMI, or host-staged gloo (rehearsal "
+                        "of N ranks on fewer GPUs; ranks share devices round-robin)")
     p.add_argument("--m", type=int, default=256, help="grid edge (configs[1]: 256)")
     p.add_argument("--stencil", type=int, default=7)
     p.add_argument("--fast-dots", action="store_true",
@@ -142,16 +150,26 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; for N>1 launch under "
                  f"python -m torch.distributed.run --nproc-per-node {args.gpus} ... bench.py --gpus {args.gpus}")
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if args.transport == "host":
+            device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        # control plane (barriers, the stop decision, max-over-ranks time) on gloo;
+        # the data path is the library's own RCCL communicator on its stream
+        dist.init_process_group("gloo")
 
     import omp_amg_amd as oa
-    from omp_amg_amd import problems
+    from omp_amg_amd import problems, shard
 
-    oa.lib().amgd_init(local)
+    oa.lib().amgd_init(device)
+    sharded = world > 1 and args.mode == "shard"
+    if sharded and args.transport == "host":
+        shard.init_host(rank, world)
+    elif sharded:
+        shard.init_rccl(rank, world)
     Ai, Aj, Av = problems.poisson3d(args.m, args.stencil)
     rows = args.m ** 3
     ds = oa.DeviceSetup(Ai, Aj, Av)
@@ -160,6 +178,7 @@ def main():
     def barrier():
         if dist is not None:
             import torch
+            oa.lib().amgd_dev_sync()
             torch.cuda.synchronize()
             dist.barrier()
 
@@ -168,7 +187,7 @@ def main():
         if dist is None:
             return flag
         import torch
-        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device="cuda")
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return bool(t.item() > 0)
 
@@ -188,6 +207,8 @@ def main():
     barrier()
     rap_ms, rap_bytes, rap_nnz, st = 0.0, 0, 0, None
     steps = 0
+    if sharded:
+        shard.stats(reset=True)
     t0 = time.perf_counter()
     while steps < args.steps:
         if steps > 0 and agree(time.time() + t_step > deadline):
@@ -205,11 +226,13 @@ def main():
     dt = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt * 1e3 / steps
-    value = world * rows * steps / dt
+    copies = 1 if sharded else world
+    value = copies * rows * steps / dt
+    comm = shard.stats() if sharded else None
 
     if rank == 0:
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
@@ -225,16 +248,19 @@ def main():
             "budget_s": args.budget_s,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"3D {args.stencil}-point Poisson {args.m}^3 CSR, full AMG setup "
                                    f"(BASELINE configs[1])",
                        "rows": rows, "nnz": int(st["nnz0"]), "levels": int(st["nlevels"]),
-                       "parallelism": f"replicas x{world}",
+                       "parallelism": (f"rows sharded x{world} (replicated hierarchy, RCCL allgatherv over xGMI)"
+                                       if sharded and args.transport == "rccl" else
+                                       f"rows sharded x{world} (host-staged gloo rehearsal)" if sharded
+                                       else f"replicas x{world}"),
                        "global_dots": "tree" if args.fast_dots else "reference-order"},
-            "rap_spgemm_nnz_per_s": world * rap_nnz / (rap_ms * 1e-3) if rap_ms > 0 else None,
+            "rap_spgemm_nnz_per_s": copies * rap_nnz / (rap_ms * 1e-3) if rap_ms > 0 else None,
             "phases_ms": {k: round(st[k], 2) for k in ("t_build_ms", "t_coarsen_ms", "t_smoother_ms",
                                                           "t_interp_ms", "t_rap_ms")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -246,10 +272,15 @@ def main():
                          "algorithmic_bytes_per_setup": rap_bytes / steps,
                          "kernel_ms_per_setup": rap_ms / steps},
         }
+        if comm is not None:
+            out["comm_rank0_per_step"] = {"allgatherv_calls": comm["calls"] / steps,
+                                          "bytes": comm["bytes"] / steps, "ms": comm["ms"] / steps}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps, args.cpu_budget_s)
         print(json.dumps(out), flush=True)
     ds.close()
+    if sharded:
+        shard.free()
     # (no amgd_shutdown here: the process exits and the driver reclaims everything;
     # tearing the HIP stream down before exit crashes rocprofv3's own finalisation)
     hb.set()

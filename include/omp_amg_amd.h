@@ -49,11 +49,35 @@ int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj, con
 int amgd_hier_export(const amgd_hier *h, struct amg_setup_data *data);  /* D2H into the ABI struct */
 void amgd_hier_free(amgd_hier **h);
 void amgd_get_stats(amgd_stats *st);
+/* ---- multi-GPU: row-sharded setup over the GPUs of one node (DESIGN.md "Multi-GPU") ----
+   Every rank calls amgd_setup_device on the same matrix; the row-independent heavy
+   kernels (SpGEMMs, Q factors) are split by work across the ranks and completed by
+   an in-place allgatherv, so every rank ends with the same, bit-identical hierarchy.
+   No reference interface corresponds: the reference's setup is serial
+   (amg_setup.c:60); crs_setup's comm (crs.h:15) is where a caller passes its ranks. */
+int amgd_comm_rccl_uid(unsigned char uid[128]);     /* rank 0: fresh RCCL unique id */
+int amgd_comm_init_rccl(int rank, int size, const unsigned char uid[128]);
+/* host transport: bufs[b] is a device buffer whose range s holds bytes
+   [offs[b*(size+1)+s], offs[b*(size+1)+s+1]); rank `rank` fills its range, the callback
+   must leave every range filled on every rank.  Returns 0 on success. */
+typedef int (*amgd_allgatherv_fn)(void *user, int nbuf, void *const *bufs, const uint64_t *offs,
+                                  int rank, int size);
+int amgd_comm_init_host(int rank, int size, amgd_allgatherv_fn fn, void *user);
+int amgd_comm_init_sim(int nshards);   /* one process computes all shards in turn (tests) */
+void amgd_comm_free(void);             /* back to one GPU */
+int amgd_comm_size(void);
+int amgd_comm_rank(void);
+/* scale of the per-op minimum work below which an op runs unsharded (1 = default, 0 = always shard) */
+void amgd_comm_set_min_work(double scale);
+void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms);
+void amgd_comm_stats_reset(void);
+
 /* device scratch helpers for ctypes callers (bench/tests) */
 void *amgd_dev_alloc(size_t bytes);
 void amgd_dev_free(void *p);
 void amgd_dev_upload(void *d, const void *h, size_t n);
 void amgd_dev_download(void *h, const void *d, size_t n);
+void amgd_dev_sync(void);                        /* wait for the library stream */
 
 #ifdef __cplusplus
 }

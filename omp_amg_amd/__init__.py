@@ -7,6 +7,7 @@ Python here is only a ctypes mirror of that C ABI for tests and the bench:
   amg_setup(Ai, Aj, Av)      -> abi.Hierarchy     (reference amg_setup.h:5, host COO in)
   DeviceSetup                -> device-resident COO -> hierarchy in HBM (omp_amg_amd.h)
   stats()                    -> per-phase times of the last setup
+  shard.*                    -> multi-GPU row sharding (RCCL / host transport / one-process sim)
 
 The product path is the HIP library only: if it is missing or no GPU is
 visible these functions raise -- there is no CPU fallback.
@@ -97,6 +98,18 @@ def lib() -> C.CDLL:
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
+        L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
+        L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
+        L.amgd_comm_rccl_uid.restype = C.c_int
+        L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
+        L.amgd_comm_init_rccl.restype = C.c_int
+        L.amgd_comm_init_host.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.amgd_comm_init_host.restype = C.c_int
+        L.amgd_comm_init_sim.argtypes = [C.c_int]
+        L.amgd_comm_init_sim.restype = C.c_int
+        L.amgd_comm_set_min_work.argtypes = [C.c_double]
+        L.amgd_comm_stats.argtypes = [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -287,6 +300,12 @@ def qf_sparse(mode: int) -> None:
     """huge-support Q factor: 0 dense cooperative, 1 sparse first (default),
     2 sparse with a capacity too small to finish (exercises the dense fallback)"""
     lib().amgd_test_qf_sparse(int(mode))
+
+
+def qf_coop_lds(m: int) -> None:
+    """dense cooperative huge-support factor: supports up to m points stage s1/s2/qk in
+    LDS, larger ones read them from global memory (-1: default 8192)"""
+    lib().amgd_test_qf_coop_lds(int(m))
 
 
 def qf_stats() -> dict:

@@ -64,6 +64,17 @@ uint32_t amgd_scan_u32(uint32_t *counts, uint64_t n);
 /* compaction map for a u8 mask: map[i] = rank of i among set entries (or ~0) */
 uint32_t amgd_mask_rank(const uint8_t *mask, uint32_t n, uint32_t *map);
 
+/* ---------------- row sharding over GPUs (amgd_comm.hip) ---------------- */
+int amgd_nshards(void);                          /* 1: sharding off */
+void amgd_my_shards(int *first, int *last);      /* shard ranges this process computes */
+int amgd_shard_worth(uint64_t work, uint64_t min_work);
+/* contiguous ranges of equal work: split_h[0..N] from an exclusive prefix of n+1 entries */
+void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h);
+/* range s of buffer b = bytes [off[b*(N+1)+s], off[b*(N+1)+s+1]), completed on every rank */
+void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off);
+void amgd_allgather_u64(uint64_t *vals_h);       /* vals_h[s] of the own shards -> all */
+void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_t *out_h);
+
 /* ---------------- reductions (return host values, sync) ---------------- */
 void amgd_set_exact(int on);     /* 1: reference-order (sequential) dots -- default; 0: tree */
 int amgd_get_exact(void);

@@ -1,0 +1,263 @@
+// amgd_comm.hip -- row sharding of the heavy setup kernels over the GPUs of one node.
+//
+// Design (DESIGN.md "Multi-GPU"): every rank keeps the whole hierarchy of the level
+// being built in its own HBM (256^3 peaks at ~108 GB of 288 GB) and runs the
+// setup's control flow redundantly -- coarsening sweeps, reference-order dots,
+// Lanczos, the find_support loop -- so every host decision is taken identically
+// everywhere without a collective.  The work-heavy, row-independent kernels are
+// sharded: the Gustavson SpGEMMs (RAP, Af*W, the constraint pattern), the
+// per-coarse-point Q factors and their application.  Rows (or coarse points) are
+// split into contiguous ranges of equal WORK (products, nz^3, nz^2), each rank
+// computes its ranges straight into the global output buffer, and one in-place
+// allgatherv over xGMI completes it on every rank.  Each output row is computed
+// by the same kernel from the same inputs, so the assembled result is
+// bit-identical to the one-GPU result -- the parity contract does not change.
+//
+// Transports:
+//   RCCL  -- the node's xGMI mesh is point-to-point (a link to every peer), so the
+//            allgatherv is one ncclGroup of direct send/recv pairs with every peer
+//            on the library stream (all links busy at once), not a ring.  librccl
+//            is dlopen'ed from ROCm at amgd_comm_init_rccl so the library itself
+//            loads (and its symbols export) without it.
+//   host  -- a caller-supplied allgatherv callback (tests: gloo between processes
+//            sharing one GPU; RCCL refuses two ranks on one device).
+//   sim   -- one process computes every shard in turn (no communication): checks
+//            the range splitting and assembly on a single GPU.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "amgd.h"
+#include "amgd_dev.h"
+#include "omp_amg_amd.h"
+
+#define API __attribute__((visibility("default")))
+
+enum { COMM_NONE = 0, COMM_RCCL = 1, COMM_HOST = 2, COMM_SIM = 3 };
+static int g_kind = COMM_NONE, g_rank = 0, g_size = 1;
+static amgd_allgatherv_fn g_cb = nullptr;
+static void *g_user = nullptr;
+static double g_min_scale = 1.0;      // work thresholds x this (0: shard everything)
+static uint64_t g_bytes = 0, g_calls = 0;
+static double g_ms = 0;
+
+// ---- RCCL entry points (dlopen'ed) ----
+struct Rccl {
+  void *h = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+  ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+  ncclResult_t (*CommDestroy)(ncclComm_t);
+  ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*GroupStart)();
+  ncclResult_t (*GroupEnd)();
+  const char *(*GetErrorString)(ncclResult_t);
+};
+static Rccl R;
+static ncclComm_t g_nc = nullptr;
+
+static int rccl_load() {
+  if (R.h) return 0;
+  const char *names[] = {"/opt/rocm/lib/librccl.so.1", "librccl.so.1", "librccl.so"};
+  for (const char *n : names)
+    if ((R.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+  if (!R.h) {
+    fprintf(stderr, "omp_amg_amd: cannot load librccl: %s\n", dlerror());
+    return -1;
+  }
+#define SYM(f)                                                       \
+  *(void **)&R.f = dlsym(R.h, "nccl" #f);                            \
+  if (!R.f) {                                                        \
+    fprintf(stderr, "omp_amg_amd: librccl lacks nccl%s\n", #f);      \
+    return -1;                                                       \
+  }
+  SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(Send) SYM(Recv) SYM(GroupStart)
+  SYM(GroupEnd) SYM(GetErrorString)
+#undef SYM
+  return 0;
+}
+#define NCCK(x)                                                                         \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) {                                                            \
+      fprintf(stderr, "omp_amg_amd: %s failed at %s:%d: %s\n", #x, __FILE__, __LINE__, \
+              R.GetErrorString(r_));                                                    \
+      abort();                                                                          \
+    }                                                                                   \
+  } while (0)
+
+extern "C" API int amgd_comm_rccl_uid(unsigned char *uid) {
+  if (rccl_load()) return -1;
+  ncclUniqueId id;
+  if (R.GetUniqueId(&id) != ncclSuccess) return -2;
+  memcpy(uid, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+extern "C" API int amgd_comm_init_rccl(int rank, int size, const unsigned char *uid) {
+  amgd_comm_free();
+  if (size < 1 || rank < 0 || rank >= size) return -3;
+  if (rccl_load()) return -1;
+  amgd_s();                                   // HIP device / stream first
+  ncclUniqueId id;
+  memcpy(id.internal, uid, NCCL_UNIQUE_ID_BYTES);
+  if (R.CommInitRank(&g_nc, size, id, rank) != ncclSuccess) return -2;
+  g_kind = COMM_RCCL;
+  g_rank = rank;
+  g_size = size;
+  return 0;
+}
+
+extern "C" API int amgd_comm_init_host(int rank, int size, amgd_allgatherv_fn fn, void *user) {
+  amgd_comm_free();
+  if (size < 1 || rank < 0 || rank >= size || !fn) return -3;
+  g_kind = COMM_HOST;
+  g_rank = rank;
+  g_size = size;
+  g_cb = fn;
+  g_user = user;
+  return 0;
+}
+
+extern "C" API int amgd_comm_init_sim(int nshards) {
+  amgd_comm_free();
+  if (nshards < 1) return -3;
+  g_kind = nshards > 1 ? COMM_SIM : COMM_NONE;
+  g_size = nshards;
+  return 0;
+}
+
+extern "C" API void amgd_comm_free(void) {
+  if (g_kind == COMM_RCCL && g_nc) {
+    amgd_sync();
+    R.CommDestroy(g_nc);
+    g_nc = nullptr;
+  }
+  g_kind = COMM_NONE;
+  g_rank = 0;
+  g_size = 1;
+  g_cb = nullptr;
+  g_user = nullptr;
+}
+
+extern "C" API int amgd_comm_size(void) { return g_size; }
+extern "C" API int amgd_comm_rank(void) { return g_rank; }
+extern "C" API void amgd_comm_set_min_work(double scale) { g_min_scale = scale < 0 ? 1.0 : scale; }
+extern "C" API void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms) {
+  *calls = g_calls;
+  *bytes = g_bytes;
+  *ms = g_ms;
+}
+extern "C" API void amgd_comm_stats_reset(void) { g_calls = g_bytes = 0; g_ms = 0; }
+
+// ---- internal API (amgd.h) ----
+int amgd_nshards(void) { return g_kind == COMM_NONE ? 1 : g_size; }
+void amgd_my_shards(int *first, int *last) {
+  if (g_kind == COMM_SIM) { *first = 0; *last = g_size; }
+  else { *first = g_rank; *last = g_rank + 1; }
+}
+int amgd_shard_worth(uint64_t work, uint64_t min_work) {
+  if (amgd_nshards() <= 1) return 0;
+  static double env = -1;
+  if (env < 0) {
+    const char *e = getenv("AMGD_SHARD_MIN");
+    env = e && *e ? atof(e) : 1.0;
+  }
+  return (double)work >= (double)min_work * env * g_min_scale;
+}
+
+// Range s of the shards holds bytes [off[b*(N+1)+s], off[b*(N+1)+s+1]) of buffer b;
+// every rank holds its own ranges, after the call every rank holds all of them.
+void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off) {
+  const int N = g_size;
+  if (g_kind == COMM_NONE || g_kind == COMM_SIM || N == 1) return;
+  double t0 = amgd_wtime();
+  for (int b = 0; b < nbuf; b++) g_bytes += off[b * (N + 1) + N] - off[b * (N + 1)];
+  g_calls++;
+  if (g_kind == COMM_HOST) {
+    amgd_sync();
+    if (g_cb(g_user, nbuf, bufs, off, g_rank, N) != 0) {
+      fprintf(stderr, "omp_amg_amd: host allgatherv callback failed\n");
+      abort();
+    }
+  } else {
+    hipStream_t s = amgd_s();
+    NCCK(R.GroupStart());
+    for (int b = 0; b < nbuf; b++) {
+      const uint64_t *o = off + (size_t)b * (N + 1);
+      char *base = (char *)bufs[b];
+      const uint64_t mlen = o[g_rank + 1] - o[g_rank];
+      for (int p = 0; p < N; p++) {
+        if (p == g_rank) continue;
+        const uint64_t plen = o[p + 1] - o[p];
+        if (mlen) NCCK(R.Send(base + o[g_rank], mlen, ncclChar, p, g_nc, s));
+        if (plen) NCCK(R.Recv(base + o[p], plen, ncclChar, p, g_nc, s));
+      }
+    }
+    NCCK(R.GroupEnd());
+    amgd_sync();
+  }
+  g_ms += (amgd_wtime() - t0) * 1e3;
+}
+
+// split[s] = first item whose exclusive work prefix reaches s*total/N (s = 0..N):
+// contiguous ranges of equal work; prefix = exclusive scan, n+1 entries
+__global__ void k_shard_split(const uint64_t *prefix, uint32_t n, int N, uint32_t *split) {
+  const int s = threadIdx.x;
+  if (s > N) return;
+  const uint64_t total = prefix[n];
+  if (s == N) { split[s] = n; return; }
+  const unsigned __int128 t = (unsigned __int128)total * (unsigned)s;
+  const uint64_t target = (uint64_t)(t / (unsigned)N);
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (prefix[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  split[s] = s == 0 ? 0 : lo;
+}
+void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h) {
+  const int N = amgd_nshards();
+  uint32_t *d = (uint32_t *)amgd_alloc(4 * (N + 1) + 4);
+  k_shard_split<<<1, 64 * ((N + 64) / 64), 0, amgd_s()>>>(prefix, n, N, d);
+  KCHECK();
+  amgd_d2h(split_h, d, 4 * (size_t)(N + 1));
+  amgd_free(d);
+}
+
+// per-shard u64 values gathered to every rank (in-place on a device buffer)
+void amgd_allgather_u64(uint64_t *vals_h) {
+  const int N = amgd_nshards();
+  int f, l;
+  amgd_my_shards(&f, &l);
+  uint64_t *d = (uint64_t *)amgd_alloc(8 * (size_t)N + 8);
+  amgd_h2d(d + f, vals_h + f, 8 * (size_t)(l - f));
+  std::vector<uint64_t> off(N + 1);
+  for (int s = 0; s <= N; s++) off[s] = 8 * (uint64_t)s;
+  void *b = d;
+  amgd_allgatherv(1, &b, off.data());
+  amgd_d2h(vals_h, d, 8 * (size_t)N);
+  amgd_free(d);
+}
+
+// host values of a device u64 array at the given indices
+__global__ void k_gather_u64(const uint64_t *a, const uint32_t *idx, int n, uint64_t *o) {
+  const int t = threadIdx.x;
+  if (t < n) o[t] = a[idx[t]];
+}
+void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_t *out_h) {
+  uint32_t *di = (uint32_t *)amgd_alloc(4 * (size_t)n + 4);
+  uint64_t *dv = (uint64_t *)amgd_alloc(8 * (size_t)n + 8);
+  amgd_h2d(di, idx_h, 4 * (size_t)n);
+  k_gather_u64<<<1, 64 * ((n + 63) / 64), 0, amgd_s()>>>(a, di, n, dv);
+  KCHECK();
+  amgd_d2h(out_h, dv, 8 * (size_t)n);
+  amgd_free(di);
+  amgd_free(dv);
+}

@@ -461,14 +461,17 @@ __device__ __forceinline__ void grid_sync(unsigned *bar, unsigned nblocks, unsig
 // huge supports (nz <= QF_COOP_MAX): one support at a time over a cooperative
 // grid of 64-lane blocks; s1/s2/qk are global (shared by the blocks) and staged
 // through LDS where a block reads them serially
+// (LDS = false, supports past QF_COOP_MAX: the blocks read s1 / s2 / qk straight
+// from global memory instead of LDS copies -- same values, same order)
 #define QF_COOP_MAX 8192
+template <bool LDS>
 __global__ __launch_bounds__(64) void k_qfactor_coop(uint32_t c, const uint64_t *wro,
                                                      const uint32_t *wcol, const uint64_t *aro,
                                                      const uint32_t *acol, const double *aa,
                                                      const uint64_t *qoff, double *Q,
                                                      double *s1b, double *s2, double *qk,
                                                      unsigned *bar) {
-  extern __shared__ double xs[];      // 2 * nz doubles
+  extern __shared__ double xs[];      // 2 * nz doubles (LDS)
   __shared__ double sh_al;
   const uint32_t lane = threadIdx.x, G = gridDim.x;
   const uint32_t gt = blockIdx.x * 64 + lane, GT = G * 64;
@@ -482,7 +485,12 @@ __global__ __launch_bounds__(64) void k_qfactor_coop(uint32_t c, const uint64_t 
     if (k > 0) {                                   // finish row k-1 (every block computes al)
       const uint32_t kp = k - 1;
       const double *s1p = s1b + (uint64_t)(kp & 1) * nz;
-      for (uint32_t m = lane; m <= kp; m += 64) { xa[m] = s1p[m]; xb[m] = qk[m]; }
+      if (LDS) {
+        for (uint32_t m = lane; m <= kp; m += 64) { xa[m] = s1p[m]; xb[m] = qk[m]; }
+      } else {
+        xa = (double *)s1p;
+        xb = qk;
+      }
       __syncthreads();
       if (lane == 0) {
         double al = xa[kp];
@@ -500,11 +508,13 @@ __global__ __launch_bounds__(64) void k_qfactor_coop(uint32_t c, const uint64_t 
     const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
     for (uint32_t m = gt; m <= k; m += GT) s1[m] = row_lookup(acol, aa, a0, a1, Qj[m]);
     grid_sync(bar, G, gen);
-    for (uint32_t m = lane; m <= k; m += 64) xa[m] = s1[m];
+    if (LDS) for (uint32_t m = lane; m <= k; m += 64) xa[m] = s1[m];
+    else xa = s1;
     __syncthreads();
     for (uint32_t i = gt; i < k; i += GT) s2[i] = seq_dot_batched(U + tri(i), xa, i + 1);
     grid_sync(bar, G, gen);
-    for (uint32_t m = lane; m < k; m += 64) xa[m] = s2[m];
+    if (LDS) for (uint32_t m = lane; m < k; m += 64) xa[m] = s2[m];
+    else xa = s2;
     __syncthreads();
     for (uint32_t ib = gt - lane; ib < k; ib += GT) {
       const uint32_t i = ib + lane;
@@ -706,21 +716,23 @@ __global__ void k_qsize(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
 struct BinLim {
   uint32_t l[7];
 };
-__global__ void k_bin_nz(const uint64_t *wro, uint32_t rn, BinLim lim, int nb, uint32_t *lists,
-                         unsigned *cnt) {
+// (columns cb <= c < ce only: a shard's range)
+__global__ void k_bin_nz(const uint64_t *wro, uint32_t cb, uint32_t ce, BinLim lim, int nb,
+                         uint32_t *lists, unsigned *cnt, uint64_t lstride) {
+  const uint64_t n = ce - cb;
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t iters = (rn + stride - 1) / stride;
+  uint64_t iters = (n + stride - 1) / stride;
   for (uint64_t it = 0; it < iters; it++) {   // uniform trip count (wave_append)
-    uint64_t c = c0 + it * stride;
-    uint64_t nz = c < rn ? wro[c + 1] - wro[c] : 0;
+    uint64_t c = cb + c0 + it * stride;
+    uint64_t nz = c < ce ? wro[c + 1] - wro[c] : 0;
     int bin = nb - 1;
     for (int q = nb - 2; q >= 0; q--)
       if (nz <= lim.l[q]) bin = q;
     for (int q = 0; q < nb; q++) {
       bool take = nz != 0 && bin == q;
       unsigned p = wave_append(&cnt[q], take);
-      if (take) lists[(uint64_t)q * ((uint64_t)rn + 1) + p] = (uint32_t)c;
+      if (take) lists[(uint64_t)q * lstride + p] = (uint32_t)c;
     }
   }
 }
@@ -735,15 +747,15 @@ struct RowSplit {
   unsigned ns, nb;
   uint64_t maxnz;
 };
-static RowSplit split_rows(const dcsr *Wt, uint32_t cap) {
+static RowSplit split_rows(const dcsr *Wt, uint32_t cap, uint32_t cb, uint32_t ce) {
   RowSplit rs;
   const uint64_t L = (uint64_t)Wt->rn + 1;
   rs.sl = (uint32_t *)amgd_alloc(2 * L * 4);
   rs.bl = rs.sl + L;
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
-  if (Wt->rn) {
-    k_bin_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, BinLim{{cap}}, 2, rs.sl, cnt);
+  if (ce > cb) {
+    k_bin_nz<<<grid_for(ce - cb), 256, 0, amgd_s()>>>(Wt->ro, cb, ce, BinLim{{cap}}, 2, rs.sl, cnt, L);
     k_max_nz<<<grid_for(Wt->rn), 256, 0, amgd_s()>>>(Wt->ro, Wt->rn, (unsigned long long *)(cnt + 4));
   }
   unsigned h[8];
@@ -774,6 +786,8 @@ static int qf_blocked() {
   }
   return b;
 }
+static uint32_t g_coop_lds_max = QF_COOP_MAX;   // tests: smaller forces the global-memory variant
+extern "C" void amgd_qfactor_set_coop_lds(int m) { g_coop_lds_max = m < 0 ? QF_COOP_MAX : (uint32_t)m; }
 static unsigned long g_qf_stats[2];   // huge supports factored sparse / sent to the dense kernel
 extern "C" void amgd_qfactor_set_sparse(int m) { g_qf_sparse = m; }
 extern "C" void amgd_qfactor_stats(unsigned long *st) {
@@ -785,8 +799,9 @@ extern "C" void amgd_qfactor_stats(unsigned long *st) {
 #define QF_T1 64
 #define QF_T2 128
 #define QF_T3 1024
-extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
-                                uint64_t *qtotal) {
+// the factors of the coarse points cb <= c < ce (all tiers), into Q at qoff
+static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, double *Q,
+                          uint32_t cb, uint32_t ce, uint64_t tot) {
   hipStream_t s = amgd_s();
   static int sglog = -1;
   if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
@@ -794,19 +809,16 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   if (sglog) { amgd_sync(); t_start = amgd_wtime(); }
   const uint32_t rn = Wt->rn;
   const uint64_t L = (uint64_t)rn + 1;
-  uint64_t *qoff = (uint64_t *)amgd_alloc(L * 8);
-  if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
-  uint64_t tot = amgd_scan_u64(qoff, rn);
-  double *Q = (double *)amgd_alloc(tot * 8 + 8);
   // bins: LDS 32 / 64 / 128, blocked 256 / 512 / 1024, huge
   constexpr int NB = 7, HUGE = 6;
   uint32_t *lists = (uint32_t *)amgd_alloc(NB * L * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
   unsigned hn[NB] = {0, 0, 0, 0, 0, 0, 0};
-  if (rn) {
-    k_bin_nz<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, BinLim{{QF_T0, QF_T1, QF_T2, 256, 512, QF_T3}},
-                                         NB, lists, cnt);
+  if (ce > cb) {
+    k_bin_nz<<<grid_for(ce - cb), 256, 0, s>>>(Wt->ro, cb, ce,
+                                              BinLim{{QF_T0, QF_T1, QF_T2, 256, 512, QF_T3}}, NB,
+                                              lists, cnt, L);
     KCHECK();
     amgd_d2h(hn, cnt, NB * 4);
   }
@@ -833,12 +845,16 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
     void *args[] = {&c, &pwro, &pwcol, &paro, &pacol, &paa, &pqoff, &Q, &s1b, &s2v, &qk, &bar};
     static bool attr = false;
     if (!attr) {
-      HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop,
+      HIPCK(hipFuncSetAttribute((const void *)k_qfactor_coop<true>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 2 * QF_COOP_MAX * 8));
       attr = true;
     }
-    HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop, dim3(G), dim3(64), args,
-                                     (unsigned)(2 * (size_t)nz * 8), s2));
+    if (nz <= g_coop_lds_max)
+      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop<true>, dim3(G), dim3(64), args,
+                                       (unsigned)(2 * (size_t)nz * 8), s2));
+    else
+      HIPCK(hipLaunchCooperativeKernel((const void *)k_qfactor_coop<false>, dim3(G), dim3(64), args,
+                                       0u, s2));
     KCHECK();
   };
   if (hn[HUGE]) {
@@ -854,10 +870,6 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
     const int sp = qf_sparse_mode();
     for (uint32_t c : big) {
       uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
-      if (nz > QF_COOP_MAX) {
-        fprintf(stderr, "omp_amg_amd: support of %u points exceeds QF_COOP_MAX\n", nz);
-        abort();
-      }
       bignz.push_back(nz);
       if (!sp) {
         bigstat.push_back(nullptr);
@@ -961,6 +973,51 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
             bignz.empty() ? 0u : bignz[0], (unsigned long)tot, (amgd_wtime() - t_start) * 1e3);
   }
   amgd_free(lists); amgd_free(cnt);
+}
+
+// Q factors of every coarse point.  Sharded (amgd_comm.hip): coarse points split
+// into contiguous ranges of equal factor work (nz^3), each rank factors its
+// ranges into the global Q, one allgatherv of the Q segments completes it.
+__global__ void k_qcost(const uint64_t *wro, uint32_t rn, uint64_t *cost) {
+  GRID_STRIDE(c, rn) {
+    uint64_t nz = wro[c + 1] - wro[c];
+    cost[c] = nz * nz * nz + 1;
+  }
+}
+#define QF_SHARD_MIN (1ull << 30)   // factor work (sum nz^3) below which one GPU does all
+extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
+                                uint64_t *qtotal) {
+  hipStream_t s = amgd_s();
+  const uint32_t rn = Wt->rn;
+  const uint64_t L = (uint64_t)rn + 1;
+  uint64_t *qoff = (uint64_t *)amgd_alloc(L * 8);
+  if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
+  uint64_t tot = amgd_scan_u64(qoff, rn);
+  double *Q = (double *)amgd_alloc(tot * 8 + 8);
+  const int N = amgd_nshards();
+  uint64_t work = 0;
+  uint64_t *cost = nullptr;
+  if (N > 1 && rn >= (uint32_t)N) {
+    cost = (uint64_t *)amgd_alloc(L * 8);
+    k_qcost<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, cost);
+    KCHECK();
+    work = amgd_scan_u64(cost, rn);
+  }
+  if (!cost || !amgd_shard_worth(work, QF_SHARD_MIN)) {
+    qfactor_range(Wt, A, qoff, Q, 0, rn, tot);
+  } else {
+    std::vector<uint32_t> split(N + 1);
+    amgd_shard_split(cost, rn, split.data());
+    std::vector<uint64_t> qo(N + 1);
+    amgd_gather_u64_at(qoff, split.data(), N + 1, qo.data());
+    int f, l;
+    amgd_my_shards(&f, &l);
+    for (int q = f; q < l; q++) qfactor_range(Wt, A, qoff, Q, split[q], split[q + 1], tot);
+    for (auto &v : qo) v *= 8;
+    void *b = Q;
+    amgd_allgatherv(1, &b, qo.data());
+  }
+  if (cost) amgd_free(cost);
   *qoff_out = qoff;
   if (qtotal) *qtotal = tot;
   return Q;
@@ -1011,10 +1068,11 @@ __global__ __launch_bounds__(NT) void k_qapply(const uint32_t *rows, uint32_t nr
     __syncthreads();
   }
 }
-extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
-                            const double *u, const double *lambda, double *out) {
+static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
+                         const double *u, const double *lambda, double *out, uint32_t cb,
+                         uint32_t ce) {
   hipStream_t s = amgd_s();
-  RowSplit rs = split_rows(Wt, QF_LDS_NZ);
+  RowSplit rs = split_rows(Wt, QF_LDS_NZ, cb, ce);
   if (rs.ns) {
     int g = (int)std::min<unsigned>(rs.ns, 65536u);
     k_qapply<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
@@ -1030,6 +1088,43 @@ extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qof
   }
   KCHECK();
   free_split(rs);
+}
+// sharded like the factor: ranges of equal work (nz^2), allgatherv of the out segments
+__global__ void k_qacost(const uint64_t *wro, uint32_t rn, uint64_t *cost) {
+  GRID_STRIDE(c, rn) {
+    uint64_t nz = wro[c + 1] - wro[c];
+    cost[c] = nz * nz + 1;
+  }
+}
+#define QA_SHARD_MIN (1ull << 27)
+extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
+                            const double *u, const double *lambda, double *out) {
+  const int N = amgd_nshards();
+  const uint32_t rn = Wt->rn;
+  if (N <= 1 || rn < (uint32_t)N) {
+    qapply_range(Wt, Q, qoff, Bt, u, lambda, out, 0, rn);
+    return;
+  }
+  uint64_t *cost = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  k_qacost<<<grid_for(rn), 256, 0, amgd_s()>>>(Wt->ro, rn, cost);
+  KCHECK();
+  const uint64_t work = amgd_scan_u64(cost, rn);
+  if (!amgd_shard_worth(work, QA_SHARD_MIN)) {
+    amgd_free(cost);
+    qapply_range(Wt, Q, qoff, Bt, u, lambda, out, 0, rn);
+    return;
+  }
+  std::vector<uint32_t> split(N + 1);
+  amgd_shard_split(cost, rn, split.data());
+  amgd_free(cost);
+  std::vector<uint64_t> wo(N + 1);
+  amgd_gather_u64_at(Wt->ro, split.data(), N + 1, wo.data());
+  int f, l;
+  amgd_my_shards(&f, &l);
+  for (int q = f; q < l; q++) qapply_range(Wt, Q, qoff, Bt, u, lambda, out, split[q], split[q + 1]);
+  for (auto &v : wo) v *= 8;
+  void *b = out;
+  amgd_allgatherv(1, &b, wo.data());
 }
 
 // ---------------------------------------------------------------------------

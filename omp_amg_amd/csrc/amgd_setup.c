@@ -736,6 +736,7 @@ API const char *amgd_error(void) { return amgd_last_error(); }
 API void amgd_get_stats(amgd_stats *st) { *st = g_st; }
 API void *amgd_dev_alloc(size_t bytes) { return amgd_alloc(bytes); }
 API void amgd_dev_free(void *p) { amgd_free(p); }
+API void amgd_dev_sync(void) { amgd_sync(); }
 API void amgd_dev_upload(void *d, const void *h, size_t n) { amgd_h2d(d, h, n); }
 API void amgd_dev_download(void *h, const void *d, size_t n) { amgd_d2h(h, d, n); }
 

@@ -1733,7 +1733,7 @@ __global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *ar
     if (valid && !w) hl[q] = i;
   }
 }
-extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
+static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (A->cn != B->rn) {
     fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
     abort();
@@ -1972,6 +1972,79 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
             (unsigned long)prods, prods / (ms * 1e6), kseq ? (wide ? (win ? "kseq-w+win" : "kseq-w") : (win ? "kseq+win" : "kseq")) : "flat",
             hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], wn[0] + wn[2], ms);
   }
+  return X;
+}
+
+// ---------------------------------------------------------------------------
+// Row-sharded SpGEMM (amgd_comm.hip): rows of A split into contiguous ranges of
+// equal product count, each rank multiplies its ranges (a row view of A: the
+// kernels only read ro[i]..ro[i+1], so no copy), the shard results are laid
+// into the global CSR at their offsets and completed by one allgatherv of
+// (ro, col, a).  Same kernels on the same rows: bit-identical to one GPU.
+// ---------------------------------------------------------------------------
+__global__ void k_ro_shift(const uint64_t *src, uint32_t n, uint64_t base, uint64_t *dst) {
+  GRID_STRIDE(i, n) dst[i] = src[i] + base;
+}
+#define SG_SHARD_MIN (1ull << 22)   // products below which one GPU does the whole product
+extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
+  const int N = amgd_nshards();
+  if (N <= 1 || A->rn < (uint32_t)N || A->cn != B->rn) return spgemm_local(A, B);
+  const uint32_t rn = A->rn;
+  uint64_t *ub = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  k_spgemm_ub<<<grid_for(rn), 256, 0, amgd_s()>>>(A->ro, A->col, rn, B->ro, ub);
+  KCHECK();
+  const uint64_t prods = amgd_scan_u64(ub, rn);
+  if (!amgd_shard_worth(prods, SG_SHARD_MIN)) {
+    amgd_free(ub);
+    return spgemm_local(A, B);
+  }
+  std::vector<uint32_t> split(N + 1);
+  amgd_shard_split(ub, rn, split.data());
+  amgd_free(ub);
+  std::vector<uint64_t> aro(N + 1), nzs(N + 1, 0);
+  amgd_gather_u64_at(A->ro, split.data(), N + 1, aro.data());
+  int f, l;
+  amgd_my_shards(&f, &l);
+  std::vector<dcsr *> xs(N, nullptr);
+  for (int q = f; q < l; q++) {
+    dcsr v = *A;
+    v.rn = split[q + 1] - split[q];
+    v.ro = A->ro + split[q];
+    v.nnz = aro[q + 1] - aro[q];
+    xs[q] = spgemm_local(&v, B);
+    nzs[q] = xs[q]->nnz;
+  }
+  amgd_allgather_u64(nzs.data());
+  std::vector<uint64_t> base(N + 1, 0);
+  for (int q = 0; q < N; q++) base[q + 1] = base[q] + nzs[q];
+  const uint64_t nz = base[N];
+  dcsr *X = (dcsr *)malloc(sizeof(dcsr));
+  X->rn = rn;
+  X->cn = B->cn;
+  X->nnz = nz;
+  X->ro = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
+  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  hipStream_t s = amgd_s();
+  HIPCK(hipMemsetAsync(X->ro, 0, 8, s));
+  for (int q = f; q < l; q++) {
+    const uint32_t n = split[q + 1] - split[q];
+    if (n) k_ro_shift<<<grid_for(n), 256, 0, s>>>(xs[q]->ro + 1, n, base[q], X->ro + split[q] + 1);
+    if (nzs[q]) {
+      HIPCK(hipMemcpyAsync(X->col + base[q], xs[q]->col, nzs[q] * 4, hipMemcpyDeviceToDevice, s));
+      HIPCK(hipMemcpyAsync(X->a + base[q], xs[q]->a, nzs[q] * 8, hipMemcpyDeviceToDevice, s));
+    }
+    dcsr_free(&xs[q]);
+  }
+  KCHECK();
+  std::vector<uint64_t> off(3 * (N + 1));
+  for (int q = 0; q <= N; q++) {
+    off[q] = ((uint64_t)split[q] + 1) * 8;   // ro entries split[q]+1 .. split[q+1]
+    off[(N + 1) + q] = base[q] * 4;
+    off[2 * (N + 1) + q] = base[q] * 8;
+  }
+  void *bufs[3] = {X->ro, X->col, X->a};
+  amgd_allgatherv(3, bufs, off.data());
   return X;
 }
 

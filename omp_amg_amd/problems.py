@@ -151,24 +151,29 @@ def sem_laplacian(ex: int, ey: int, ez: int, N: int, seed: int = 0, jitter: floa
     li = np.arange(n1)
     lz, ly, lx = np.meshgrid(li, li, li, indexing="ij")
     lx, ly, lz = lx.ravel(), ly.ravel(), lz.ravel()
-    rows, cols, vals = [], [], []
-    for kz in range(ez):
-        for ky in range(ey):
-            for kx in range(ex):
-                s = 1.0 + jitter * (rng.random(3) - 0.5)
-                Ke = elem(*s)
-                g = (kx * N + lx) + gx * ((ky * N + ly) + gy * (kz * N + lz))
-                rows.append(np.repeat(g, n1 ** 3))
-                cols.append(np.tile(g, n1 ** 3))
-                vals.append(Ke.ravel())
-    r = np.concatenate(rows)
-    c = np.concatenate(cols)
-    v = np.concatenate(vals)
-    # assemble duplicates
+    # the element matrix of an affine hex is a sum of Kronecker products with the
+    # diagonal GLL mass, so most of its (N+1)^6 entries are exact zeros: keep only
+    # its structural pattern (identical for every element) before assembly
+    pat = np.flatnonzero(elem(1.0, 1.0, 1.0).ravel() != 0)
+    pr, pc = pat // n1 ** 3, pat % n1 ** 3
+    loc = lx + gx * (ly + gy * lz)                       # node offsets inside an element
+    kz, ky, kx = np.meshgrid(np.arange(ez), np.arange(ey), np.arange(ex), indexing="ij")
+    base = (kx.ravel() * N + gx * (ky.ravel() * N + gy * kz.ravel() * N)).astype(np.int64)
+    if jitter == 0.0:
+        ke = np.broadcast_to(elem(1.0, 1.0, 1.0).ravel()[pat], (len(base), len(pat)))
+    else:                                                # element order = the loop order kz, ky, kx
+        ke = np.stack([elem(*(1.0 + jitter * (rng.random(3) - 0.5))).ravel()[pat]
+                       for _ in range(len(base))])
+    r = (base[:, None] + loc[pr][None, :]).ravel()
+    c = (base[:, None] + loc[pc][None, :]).ravel()
+    v = np.ascontiguousarray(ke).ravel()
+    # assemble duplicates (summed in element order, like gs)
     ntot = gx * gy * gz
     key = r * ntot + c
+    del r, c
     order = np.argsort(key, kind="stable")
     key, v = key[order], v[order]
+    del order
     uk, start = np.unique(key, return_index=True)
     vs = np.add.reduceat(v, start)
     r, c = uk // ntot, uk % ntot

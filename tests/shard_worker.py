@@ -1,0 +1,48 @@
+"""One rank of the multi-process sharded-setup test (tests/test_gpu_shard.py).
+
+Launched N times on the same GPU with RANK / WORLD_SIZE / MASTER_PORT set: gloo
+group, host-staged allgatherv transport (RCCL refuses two ranks on one device),
+every op sharded (min work 0).  Checks the hierarchy bit for bit against the
+reference fixture and, for a generated problem, against the one-GPU run of the
+same process.  Prints one JSON line; exit code 0 = pass."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import omp_amg_amd as oa  # noqa: E402
+from omp_amg_amd import abi, parity, problems, shard  # noqa: E402
+
+
+def main():
+    rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    oa.init(0)
+    case = os.environ["SHARD_CASE"]
+    out = {"rank": rank, "case": case}
+    if case.startswith("gold:"):
+        z = np.load(os.path.join(os.path.dirname(__file__), "golden", case[5:] + ".npz"))
+        ref = parity.from_npz(z)
+        Ai, Aj, Av = z["in_Ai"], z["in_Aj"], z["in_Av"]
+    else:
+        m = int(case.split(":")[1])
+        Ai, Aj, Av = problems.poisson3d(m, 27 if case.startswith("p27") else 7)
+        ref = abi.run_setup(oa.lib(), Ai, Aj, Av)            # one GPU, before sharding
+    shard.init_host(rank, size)
+    shard.set_min_work(0.0)
+    shard.stats(reset=True)
+    h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    st = shard.stats()
+    shard.free()
+    bad = parity.compare(ref, h, exact=True)
+    out.update(calls=st["calls"], bytes=st["bytes"], bad=bad[:5], levels=h.nlevels)
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if not bad and st["calls"] > 0 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -404,20 +404,26 @@ def _qfactor_case(structure):
     return W, A
 
 
-@pytest.mark.parametrize("structure,mode", [("tiers", 1), ("tiers", 0), ("scattered", 1),
-                                            ("scattered", 2), ("scattered", 0)])
-def test_qfactor_tiers_bitexact(structure, mode):
+@pytest.mark.parametrize("structure,mode,coop_lds", [("tiers", 1, -1), ("tiers", 0, -1),
+                                                     ("scattered", 1, -1), ("scattered", 2, -1),
+                                                     ("scattered", 0, -1), ("scattered", 0, 0),
+                                                     ("scattered", 2, 1200)])
+def test_qfactor_tiers_bitexact(structure, mode, coop_lds):
     """Q factors for supports in every tier (LDS 32 / 64 / 128 / block / huge) against
     the oracle's restatement of interp's Q loop, bit for bit.  Huge supports run the
     sparse kernel (mode 1), the dense cooperative kernel (mode 0), or the sparse
-    kernel with a capacity too small to finish, which must hand over to the dense one"""
+    kernel with a capacity too small to finish, which must hand over to the dense one.
+    coop_lds: supports above it run the dense kernel's global-memory variant (the one
+    supports past 8192 points take)"""
     W, A = _qfactor_case(structure)
     oa.qf_sparse(mode)
+    oa.qf_coop_lds(coop_lds)
     oa.qf_stats()
     try:
         X = oa.test_csr_op(5, W, A)
     finally:
         oa.qf_sparse(1)
+        oa.qf_coop_lds(-1)
     st = oa.qf_stats()
     nhuge = int((np.diff(W.row_off) > 1024).sum())
     if mode == 0:
