@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
+        L.amgd_test_spmv_bn.argtypes = [C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
@@ -262,6 +263,12 @@ def spmv_sl_min(n: int) -> None:
     """row count from which whole-matrix and listed-row SpMVs with long rows run lane-per-row
     (0: always; -1: environment / default).  Same sums either way."""
     lib().amgd_test_spmv_sl_min(int(n))
+
+
+def spmv_bn(on: int) -> None:
+    """wave-per-row SpMV row sums: 1 = chunks added on the binade grid by all lanes
+    (default), 0 = lane 0 adds each chunk in turn, -1 = environment / default.  Same sums."""
+    lib().amgd_test_spmv_bn(int(on))
 
 
 def test_build(Ai, Aj, Av) -> abi.Csr:

@@ -401,6 +401,36 @@ __device__ __forceinline__ double wave_row_sum(const uint32_t *col, const double
   }
   return t;
 }
+// the same row sum with the chunk added on the binade grid by all 64 lanes
+// (wave_chunk_add); the next chunk's loads are issued before the current one is added
+__device__ __forceinline__ double wave_row_sum_bn(const uint32_t *col, const double *a,
+                                                  const double *x, uint64_t k0, uint64_t k1,
+                                                  int lane) {
+  double t = 0.0;
+  uint64_t k = k0 + lane;
+  double p = 0.0;
+  if (k < k1) p = x ? a[k] * x[col[k]] : a[k];
+  for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
+    const uint64_t kn = c0 + 64 + lane;
+    uint32_t cn = 0;
+    double an = 0.0;
+    if (kn < k1) {
+      an = a[kn];
+      if (x) cn = col[kn];
+    }
+    t = wave_chunk_add(t, p, (int)min((uint64_t)64, k1 - c0), lane);
+    p = 0.0;
+    if (kn < k1) p = x ? an * x[cn] : an;
+  }
+  return t;
+}
+static int g_spmv_bn = -1;        // 1: binade-parallel wave row sums (default), 0: lane-0 adds
+static bool spmv_bn() {
+  if (g_spmv_bn < 0) { const char *e = getenv("AMGD_SPMV_BN"); g_spmv_bn = e ? atoi(e) != 0 : 1; }
+  return g_spmv_bn == 1;
+}
+extern "C" void amgd_spmv_set_bn(int on) { g_spmv_bn = on < 0 ? -1 : (on ? 1 : 0); }
+template <bool BN>
 __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t rn, const double *x,
                                                    double *z, double alpha, const double *y,
@@ -408,7 +438,8 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
   __shared__ double buf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < rn; i += (uint64_t)gridDim.x * 4) {
-    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
+    const double t = BN ? wave_row_sum_bn(col, a, x, ro[i], ro[i + 1], lane)
+                        : wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
@@ -527,6 +558,7 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
   }
 }
 // ordered sums (x == nullptr) or products of the listed rows only
+template <bool BN>
 __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, const uint32_t *col,
                                                         const double *a, const uint32_t *list,
                                                         uint32_t n, const double *x, double *z) {
@@ -534,7 +566,8 @@ __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, cons
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
     const uint32_t i = list[r];
-    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
+    const double t = BN ? wave_row_sum_bn(col, a, x, ro[i], ro[i + 1], lane)
+                        : wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) z[i] = t;
   }
 }
@@ -543,7 +576,8 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
   if (!n) return;
   if ((int64_t)n < sl_min_list()) {          // too few rows to fill the chip one row per lane
     int g = (int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536);
-    k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
+    if (spmv_bn()) k_spmv_wave_list<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
+    else k_spmv_wave_list<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
     KCHECK();
     return;
   }
@@ -552,8 +586,27 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
                                              1.0, nullptr);
   KCHECK();
 }
+static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
+                      double beta, const uint8_t *f);
+// AMGD_MVLOG=1: one line per whole-matrix SpMV (rows, nnz, kernel, time, effective GB/s)
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
+  static int mvlog = -1;
+  if (mvlog < 0) mvlog = getenv("AMGD_MVLOG") != nullptr;
+  if (!mvlog) { spmv_impl(M, x, z, alpha, y, beta, f); return; }
+  amgd_sync();
+  const double t0 = amgd_wtime();
+  spmv_impl(M, x, z, alpha, y, beta, f);
+  amgd_sync();
+  const double ms = (amgd_wtime() - t0) * 1e3;
+  const int64_t slm = sl_min_whole();
+  const char *k = M->nnz >= 32ull * M->rn ? ((int64_t)M->rn >= slm ? "lane" : "wave") : "stream";
+  fprintf(stderr, "spmv %u x %u nnz %lu %s x%d %.3f ms %.0f GB/s\n", M->rn, M->cn,
+          (unsigned long)M->nnz, k, x ? 1 : 0, ms,
+          (12.0 * M->nnz + 16.0 * M->rn + (x ? 8.0 * M->nnz : 0.0)) / (ms * 1e6));
+}
+static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
+                      double beta, const uint8_t *f) {
   if (M->rn == 0) return;
   static int mode = -1;
   if (mode < 0) mode = getenv("AMGD_SPMV_MODE") ? atoi(getenv("AMGD_SPMV_MODE")) : 0;
@@ -570,7 +623,8 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
                                                 y, beta, f);
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
-    k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+    if (spmv_bn()) k_spmv_wave<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+    else k_spmv_wave<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   } else {
     int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
     k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);

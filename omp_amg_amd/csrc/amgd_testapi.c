@@ -151,6 +151,8 @@ API void amgd_test_qf_stats(uint64_t *out) {
 }
 
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
+extern void amgd_spmv_set_bn(int on);
+API void amgd_test_spmv_bn(int on) { amgd_spmv_set_bn(on); }
 extern void amgd_qfactor_set_coop_lds(int m);
 API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }
 extern void amgd_spgemm_force_flat(int on);

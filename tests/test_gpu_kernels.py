@@ -189,8 +189,80 @@ def _rowsums(L):
     return refops.spmv(L, np.ones(L.cn))          # a*1.0 == a: the ordered row sums
 
 
+@pytest.fixture(params=[1, 0], ids=["bn", "lane0"])
+def bn(request):
+    """wave-per-row row sums: binade-grid chunk adds (default) or lane 0's ordered adds"""
+    oa.spmv_bn(request.param)
+    yield request.param
+    oa.spmv_bn(-1)
+
+
+def _adversarial_rows(rng, rn=700):
+    """rows built to break a parallel ordered sum: monotone positive sums crossing many
+    binades, exact ties at the running sum's half-ulp, leading / interleaved zeros and
+    -0, cancellation to exact zero mid-row, subnormals, huge magnitudes, mixed signs
+    hovering around a binade edge, inf and nan"""
+    ro, cols, vals = [0], [], []
+    cn = 2000
+    kinds = ["pos", "ties", "zeros", "cancel", "sub", "huge", "hover", "mixed", "inf"]
+    for i in range(rn):
+        kind = kinds[i % len(kinds)]
+        L = int(rng.choice([1, 2, 63, 64, 65, 130, 257, 600]))
+        if kind == "pos":
+            v = np.abs(rng.standard_normal(L)) * 2.0 ** rng.integers(-3, 4, L)
+        elif kind == "ties":
+            v = np.where(rng.random(L) < 0.5, 2.0 ** -53, 1.0) * (1 + (rng.random(L) < 0.3))
+            v[0] = 1.0
+        elif kind == "zeros":
+            v = np.where(rng.random(L) < 0.6, 0.0, rng.standard_normal(L))
+            v[: L // 2] = -0.0
+        elif kind == "cancel":
+            h = rng.standard_normal((L + 1) // 2)
+            v = np.concatenate([h, -h])[:L]
+        elif kind == "sub":
+            v = rng.standard_normal(L) * 2.0 ** -1070
+        elif kind == "huge":
+            v = rng.standard_normal(L) * 2.0 ** rng.integers(900, 1020, L)
+        elif kind == "hover":
+            v = np.where(rng.random(L) < 0.5, 1.0, -1.0) * 2.0 ** -52
+            v[0] = 1.0
+        elif kind == "mixed":
+            v = rng.standard_normal(L) * 10.0 ** rng.integers(-12, 12, L)
+        else:
+            v = rng.standard_normal(L)
+            v[L // 2] = np.inf if i % 2 else np.nan
+        c = np.sort(rng.choice(cn, size=L, replace=False))
+        cols.extend(c.tolist())
+        vals.extend(v.tolist())
+        ro.append(len(cols))
+    return refops.Csr(rn, cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64),
+                      np.array(vals))
+
+
+def test_spmv_wave_adversarial_rows(bn):
+    """wave-per-row SpMV / row sums on adversarial rows, bit for bit against the
+    sequential loop (nan compared as nan)"""
+    A = _adversarial_rows(np.random.default_rng(77))
+    with np.errstate(all="ignore"):
+        want_s = _rowsums(A)
+        x = np.where(np.random.default_rng(3).random(A.cn) < 0.5, 1.0, 0.5)
+        want = refops.spmv(A, x)
+    oa.spmv_sl_min(1 << 40)                      # whole matrix: wave-per-row kernel
+    try:
+        got_s = oa.test_spmv_f(A, None)
+        got = oa.test_spmv(A, x)
+        rows = np.arange(A.rn, dtype=np.uint32)[::-1].copy()
+        got_l = oa.test_spmv_rows(A, rows, x, np.zeros(A.rn))
+    finally:
+        oa.spmv_sl_min(-1)
+    for g, w in ((got_s, want_s), (got, want), (got_l, want)):
+        assert np.array_equal(g.view(np.uint64), w.view(np.uint64)) or \
+            np.array_equal(np.isnan(g), np.isnan(w)) and np.array_equal(g[~np.isnan(g)].view(np.uint64),
+                                                                       w[~np.isnan(w)].view(np.uint64))
+
+
 @pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
-def test_spmv_long_rows_ragged(sl_min):
+def test_spmv_long_rows_ragged(sl_min, bn):
     """long-row SpMV kernels on ragged rows: wave-per-row (default below 2^20 rows) and
     lane-per-row (forced with the row threshold at 0), with and without y, the f row
     mask and x = NULL (ordered row sums)"""
@@ -212,7 +284,7 @@ def test_spmv_long_rows_ragged(sl_min):
 
 
 @pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
-def test_spmv_rows_listed(sl_min):
+def test_spmv_rows_listed(sl_min, bn):
     """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
     threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
     rng = np.random.default_rng(29)
