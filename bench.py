@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                    help="shard mode data path: RCCL over xGMI, or host-staged gloo (rehearsal "
                         "of N ranks on fewer GPUs; ranks share devices round-robin)")
-    p.add_argument("--m", type=int, default=256, help="grid edge (configs[1]: 256)")
+    p.add_argument("--edge", "--m", dest="m", type=int, default=256,
+                   help="grid edge (configs[1]: 256); spell it --edge under torch.distributed.run")
     p.add_argument("--stencil", type=int, default=7)
     p.add_argument("--fast-dots", action="store_true",
                    help="tree-ordered global dots instead of reference order (not parity-certified)")

@@ -99,7 +99,7 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
-        L.amgd_test_spmv_bn.argtypes = [C.c_int]
+        L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
@@ -261,14 +261,14 @@ def test_spmv_rows(A: abi.Csr, rows, x=None, z0=None):
 
 def spmv_sl_min(n: int) -> None:
     """row count from which whole-matrix and listed-row SpMVs with long rows run lane-per-row
-    (0: always; -1: environment / default).  Same sums either way."""
+    instead of wave-per-row (0: always, the default; -1: environment / default).  Same sums."""
     lib().amgd_test_spmv_sl_min(int(n))
 
 
-def spmv_bn(on: int) -> None:
-    """wave-per-row SpMV row sums: 1 = chunks added on the binade grid by all lanes
-    (default), 0 = lane 0 adds each chunk in turn, -1 = environment / default.  Same sums."""
-    lib().amgd_test_spmv_bn(int(on))
+def spmv_rw(rw: int) -> None:
+    """rows per wavefront of the lane-per-row SpMV kernel: 4, 16 or 64 (-1: by row count).
+    Same sums either way."""
+    lib().amgd_test_spmv_rw(int(rw))
 
 
 def test_build(Ai, Aj, Av) -> abi.Csr:

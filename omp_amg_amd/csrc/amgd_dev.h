@@ -27,63 +27,6 @@ __device__ __forceinline__ unsigned wave_append(unsigned *counter, bool pred) {
   base = __shfl(base, leader, 64);
   return pred ? base + (unsigned)__popcll(mask & lt) : 0xffffffffu;
 }
-// Ordered (left-to-right, from +0) sum of one row's products by a whole wavefront:
-// the 64 products of a chunk are added on the integer grid of the running sum's
-// binade while the running sum stays strictly inside it -- fl(s + p) = s + RN_u(p)
-// there, so the sequential sum is s + u * (inclusive integer scan); the first
-// product that leaves the binade (or is a tie, huge or non-finite) is added the
-// ordinary way and the walk continues from the next one.  Bit-identical to the
-// sequential loop (the argument of the reference-order dots, amgd_rt.hip).
-// Every lane passes its own product `p` of the chunk (lanes >= m: ignored) and
-// every lane returns the same updated sum.
-__device__ __forceinline__ long long wave_incl_scan_i64(long long v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    long long y = __shfl_up(v, o, 64);
-    if (lane >= o) v = (long long)((unsigned long long)v + (unsigned long long)y);
-  }
-  return v;
-}
-__device__ __forceinline__ double wave_chunk_add(double s, double p, int m, int lane) {
-  const long long LO = 1ll << 52, HI = 1ll << 53;
-  int j = 0;
-  while (j < m) {
-    const bool act = lane >= j && lane < m;
-    if (s == 0.0) {                          // +0 + (+-0) = +0: jump to the first nonzero
-      const unsigned long long nzm = __ballot(act && p != 0.0);
-      if (!nzm) break;
-      const int f = __ffsll((long long)nzm) - 1;
-      s = __shfl(p, f, 64);                  // +0 + p == p exactly
-      j = f + 1;
-      continue;
-    }
-    if (!(fabs(s) >= 2.2250738585072014e-308) || !(fabs(s) < 1.0e300)) {
-      for (int q = j; q < m; q++) s = s + __shfl(p, q, 64);   // subnormal / huge: one by one
-      break;
-    }
-    const int e = ilogb(s);
-    const long long S0 = (long long)ldexp(s, 52 - e);          // |S0| in [2^52, 2^53)
-    const double xq = ldexp(p, 52 - e);
-    const double r = rint(xq);
-    const bool bad = act && (!(fabs(xq) < 7.2e16) || fabs(r - xq) == 0.5);
-    const long long v = (act && !bad) ? (long long)r : 0ll;
-    const long long P = wave_incl_scan_i64(v, lane);
-    const long long run = (long long)((unsigned long long)S0 + (unsigned long long)P);
-    const bool inside = S0 > 0 ? (run > LO && run < HI) : (run < -LO && run > -HI);
-    const unsigned long long vm = __ballot(act && (bad || !inside));
-    if (!vm) {
-      const long long fin = __shfl(run, m - 1, 64);
-      s = ldexp((double)fin, e - 52);
-      break;
-    }
-    const int vl = __ffsll((long long)vm) - 1;                  // first violating product
-    const long long before = __shfl(run, vl > 0 ? vl - 1 : 0, 64);
-    const double sb = vl > j ? ldexp((double)before, e - 52) : s;
-    s = sb + __shfl(p, vl, 64);
-    j = vl + 1;
-  }
-  return s;
-}
 #define GRID_STRIDE(i, n) \
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)(n); \
        i += (uint64_t)gridDim.x * blockDim.x)

@@ -401,36 +401,6 @@ __device__ __forceinline__ double wave_row_sum(const uint32_t *col, const double
   }
   return t;
 }
-// the same row sum with the chunk added on the binade grid by all 64 lanes
-// (wave_chunk_add); the next chunk's loads are issued before the current one is added
-__device__ __forceinline__ double wave_row_sum_bn(const uint32_t *col, const double *a,
-                                                  const double *x, uint64_t k0, uint64_t k1,
-                                                  int lane) {
-  double t = 0.0;
-  uint64_t k = k0 + lane;
-  double p = 0.0;
-  if (k < k1) p = x ? a[k] * x[col[k]] : a[k];
-  for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
-    const uint64_t kn = c0 + 64 + lane;
-    uint32_t cn = 0;
-    double an = 0.0;
-    if (kn < k1) {
-      an = a[kn];
-      if (x) cn = col[kn];
-    }
-    t = wave_chunk_add(t, p, (int)min((uint64_t)64, k1 - c0), lane);
-    p = 0.0;
-    if (kn < k1) p = x ? an * x[cn] : an;
-  }
-  return t;
-}
-static int g_spmv_bn = -1;        // 1: binade-parallel wave row sums (default), 0: lane-0 adds
-static bool spmv_bn() {
-  if (g_spmv_bn < 0) { const char *e = getenv("AMGD_SPMV_BN"); g_spmv_bn = e ? atoi(e) != 0 : 1; }
-  return g_spmv_bn == 1;
-}
-extern "C" void amgd_spmv_set_bn(int on) { g_spmv_bn = on < 0 ? -1 : (on ? 1 : 0); }
-template <bool BN>
 __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t rn, const double *x,
                                                    double *z, double alpha, const double *y,
@@ -438,8 +408,7 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
   __shared__ double buf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < rn; i += (uint64_t)gridDim.x * 4) {
-    const double t = BN ? wave_row_sum_bn(col, a, x, ro[i], ro[i + 1], lane)
-                        : wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
+    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
@@ -447,47 +416,53 @@ __global__ __launch_bounds__(256) void k_spmv_wave(const uint64_t *ro, const uin
     }
   }
 }
-// long rows, one row per LANE: each wavefront owns 64 rows and walks them in
+// long rows, one row per LANE (RW = 64; fewer rows per wavefront below): each wavefront owns 64 rows and walks them in
 // rounds of 16 entries; a round is loaded cooperatively (each load instruction
 // covers four 16-entry row segments, 128 B each) into an LDS tile, and every lane
 // then adds its own row's 16 products in order.  The sum is the reference's
 // left-to-right sum and all 64 lanes add at once (k_spmv_wave leaves 63 idle).
 // LIST: the rows are list[0..n) instead of 0..n.
-#define SL_SEG 16
-// Row-count thresholds from which the lane-per-row kernel runs (the sums are the
-// same either way; only speed differs):
-//  * listed rows (amgd_spmv_rows): 65536 = 1024 wavefronts of 64 rows, enough to
-//    fill 256 CUs;  AMGD_SL_LIST_MIN_ROWS overrides
-//  * whole matrices with long rows (amgd_spmv): 2^20 -- wave-per-row below that
-//    measured faster at 256^3 (setup 38.7 -> 38.3 s);  AMGD_SL_MIN_ROWS overrides
+// Long rows (mean >= 32): the lane kernel from 4096 rows on, with RW = 4 / 16 / 64
+// rows per wavefront by row count (lane_rw); wave-per-row (lane 0 adds) below
+// AMGD_SL_MIN_ROWS / AMGD_SL_LIST_MIN_ROWS (default 4096).  Chosen from the
+// micro-benchmark on the 256^3 setup's matrix shapes (tools/spmv_bench.py,
+// profiles/r02/spmv_bench.txt).  The sums are the same either way.
 // amgd_spmv_set_sl_min() (tests) forces both; -1 returns to the environment/default.
 static int64_t g_sl_forced = -1;
 static int64_t sl_env(const char *name, int64_t dflt) {
   const char *e = getenv(name);
   return e && *e ? atoll(e) : dflt;
 }
-static int64_t sl_min_whole() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_MIN_ROWS", 1 << 20); }
-static int64_t sl_min_list() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_LIST_MIN_ROWS", 65536); }
+static int64_t sl_min_whole() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_MIN_ROWS", 4096); }
+static int64_t sl_min_list() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_LIST_MIN_ROWS", 4096); }
 extern "C" void amgd_spmv_set_sl_min(int64_t n) { g_sl_forced = n < 0 ? -1 : n; }
-template <bool LIST>
+// RW rows per wavefront (64: one row per lane; 16 / 4 for matrices with fewer, longer
+// rows -- more wavefronts in flight, the first RW lanes add): a round loads SEG =
+// 1024 / RW entries of each row, 16 per lane, lane L's q-th load taking flat entry
+// q*64 + L of the round (row = that / SEG): every load instruction covers whole row
+// segments of >= 128 B.
+template <bool LIST, int RW>
 __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
                                                    double beta, const uint8_t *f) {
-  __shared__ double buf[4][64][SL_SEG + 1];
-  __shared__ uint64_t rk0[4][64];
-  __shared__ uint32_t rlen[4][64];
+  constexpr int SEG = 1024 / RW;
+  __shared__ double buf[4][RW][SEG + 1];
+  __shared__ uint64_t rk0[4][RW];
+  __shared__ uint32_t rlen[4][RW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * 64; rb < n;
-       rb += (uint64_t)gridDim.x * 4 * 64) {
+  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n;
+       rb += (uint64_t)gridDim.x * 4 * RW) {
     const uint64_t r = rb + lane;
-    const bool own = r < n;
+    const bool own = lane < RW && r < n;
     const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
     const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
     const uint32_t len = (uint32_t)(k1 - k0);
-    rk0[w][lane] = k0;
-    rlen[w][lane] = len;
+    if (lane < RW) {
+      rk0[w][lane] = k0;
+      rlen[w][lane] = len;
+    }
     uint32_t mx = len;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
@@ -495,33 +470,35 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double t = 0;
-    const uint32_t sub = lane & (SL_SEG - 1), grp = lane >> 4;
     // round `off`'s products sit in v[]; the next round's (a, col) loads are
     // issued before the lanes add the current round, so HBM latency overlaps
     // the ordered adds (the sums and their order are unchanged)
     double v[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-      const int rr = q * 4 + grp;
+      const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
       v[q] = 0.0;
-      if (sub < rlen[w][rr]) {
+      if ((uint32_t)sub < rlen[w][rr]) {
         const uint64_t k = rk0[w][rr] + sub;
         v[q] = x ? a[k] * x[col[k]] : a[k];
       }
     }
-    for (uint32_t off = 0; off < mx; off += SL_SEG) {
+    for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
-      for (int q = 0; q < 16; q++) buf[w][q * 4 + grp][sub] = v[q];
+      for (int q = 0; q < 16; q++) {
+        const int fl = q * 64 + lane;
+        buf[w][fl / SEG][fl % SEG] = v[q];
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint32_t en = off + SL_SEG + sub;
       double an[16];
       uint32_t cn[16];
       bool hv[16];
 #pragma unroll
       for (int q = 0; q < 16; q++) {
-        const int rr = q * 4 + grp;
+        const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
+        const uint32_t en = off + SEG + sub;
         hv[q] = en < rlen[w][rr];
         an[q] = 0.0;
         cn[q] = 0;
@@ -531,15 +508,18 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
           if (x) cn[q] = col[k];
         }
       }
-      if (off < len) {
-        const uint32_t m = min((uint32_t)SL_SEG, len - off);
-        if (m == SL_SEG) {
-          // full segment: all LDS reads issued before the ordered adds
-          double u[SL_SEG];
+      if (lane < RW && off < len) {
+        const uint32_t m = min((uint32_t)SEG, len - off);
+        if (m == SEG) {
+          // full segment: LDS reads issued 16 ahead of the ordered adds
 #pragma unroll
-          for (int e = 0; e < SL_SEG; e++) u[e] = buf[w][lane][e];
+          for (int e0 = 0; e0 < SEG; e0 += 16) {
+            double u[16];
 #pragma unroll
-          for (int e = 0; e < SL_SEG; e++) t += u[e];
+            for (int e = 0; e < 16; e++) u[e] = buf[w][lane][e0 + e];
+#pragma unroll
+            for (int e = 0; e < 16; e++) t += u[e];
+          }
         } else {
           for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
         }
@@ -557,8 +537,29 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     }
   }
 }
+// rows per wavefront of the lane kernel for n rows (>= ~2048 wavefronts in flight)
+static int64_t g_rw_forced = -2;     // AMGD_SL_RW / amgd_spmv_set_rw (tests): 4, 16 or 64
+extern "C" void amgd_spmv_set_rw(int rw) { g_rw_forced = rw < 0 ? -2 : rw; }
+static int lane_rw(uint64_t n) {
+  if (g_rw_forced == -2) g_rw_forced = sl_env("AMGD_SL_RW", 0);
+  if (g_rw_forced == 4 || g_rw_forced == 16 || g_rw_forced == 64) return (int)g_rw_forced;
+  return n >= (1u << 22) ? 64 : n >= (1u << 16) ? 16 : 4;
+}
+#define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_)                                  \
+  do {                                                                                        \
+    const int rw_ = lane_rw(n_);                                                              \
+    const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
+    if (rw_ == 64)                                                                            \
+      k_spmv_lane<LIST, 64><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
+                                                       al, y_, be, f_);                       \
+    else if (rw_ == 16)                                                                       \
+      k_spmv_lane<LIST, 16><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
+                                                       al, y_, be, f_);                       \
+    else                                                                                      \
+      k_spmv_lane<LIST, 4><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,   \
+                                                      al, y_, be, f_);                        \
+  } while (0)
 // ordered sums (x == nullptr) or products of the listed rows only
-template <bool BN>
 __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, const uint32_t *col,
                                                         const double *a, const uint32_t *list,
                                                         uint32_t n, const double *x, double *z) {
@@ -566,8 +567,7 @@ __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, cons
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
     const uint32_t i = list[r];
-    const double t = BN ? wave_row_sum_bn(col, a, x, ro[i], ro[i + 1], lane)
-                        : wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
+    const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) z[i] = t;
   }
 }
@@ -576,14 +576,11 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
   if (!n) return;
   if ((int64_t)n < sl_min_list()) {          // too few rows to fill the chip one row per lane
     int g = (int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536);
-    if (spmv_bn()) k_spmv_wave_list<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
-    else k_spmv_wave_list<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
+    k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
     KCHECK();
     return;
   }
-  int g = (int)std::min<uint64_t>(((uint64_t)n + 255) / 256, 16384);
-  k_spmv_lane<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n, list, x, z, 0.0, nullptr,
-                                             1.0, nullptr);
+  LANE_LAUNCH(true, n, list, x, z, 0.0, nullptr, 1.0, nullptr);
   KCHECK();
 }
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
@@ -618,13 +615,10 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   }
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
-    int g = (int)std::min<uint64_t>(((uint64_t)M->rn + 255) / 256, 16384);
-    k_spmv_lane<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z, alpha,
-                                                y, beta, f);
+    LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f);
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
-    if (spmv_bn()) k_spmv_wave<true><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
-    else k_spmv_wave<false><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
+    k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   } else {
     int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
     k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
@@ -2131,4 +2125,43 @@ extern "C" uint64_t amgd_to_host_cols(const dcsr *A, unsigned long *h_ro, unsign
     amgd_d2h(h_a, A->a, A->nnz * 8);
   }
   return A->nnz;
+}
+
+// ---------------------------------------------------------------------------
+// SpMV micro-benchmark matrices (test API only): rn rows of len0..len1 entries,
+// columns start(i) + k*gap (sorted, distinct, start spread over the column range)
+// ---------------------------------------------------------------------------
+__global__ void k_bench_rowlen(uint32_t rn, uint32_t len0, uint32_t len1, uint64_t *cnt) {
+  GRID_STRIDE(i, rn) {
+    uint64_t h = (i * 0x9E3779B97F4A7C15ull) >> 33;
+    cnt[i] = len0 + (len1 > len0 ? h % (len1 - len0 + 1) : 0);
+  }
+}
+__global__ void k_bench_fill(const uint64_t *ro, uint32_t rn, uint32_t cn, uint32_t gap,
+                             uint32_t *col, double *a) {
+  GRID_STRIDE(i, rn) {
+    const uint64_t k0 = ro[i], len = ro[i + 1] - k0;
+    const uint64_t span = len ? (len - 1) * gap + 1 : 0;
+    uint64_t start = (uint64_t)i * cn / rn;
+    start = start > span / 2 ? start - span / 2 : 0;
+    if (start + span > cn) start = cn > span ? cn - span : 0;
+    for (uint64_t k = 0; k < len; k++) {
+      col[k0 + k] = (uint32_t)(start + k * gap);
+      a[k0 + k] = 1.0 + (double)((k0 + k) % 7) * 0.125;
+    }
+  }
+}
+extern "C" dcsr *amgd_bench_matrix(uint32_t rn, uint32_t cn, uint32_t len0, uint32_t len1,
+                                   uint32_t gap) {
+  hipStream_t s = amgd_s();
+  uint64_t *ro = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
+  k_bench_rowlen<<<grid_for(rn), 256, 0, s>>>(rn, len0, len1, ro);
+  const uint64_t nnz = amgd_scan_u64(ro, rn);
+  dcsr *A = (dcsr *)malloc(sizeof(dcsr));
+  A->rn = rn; A->cn = cn; A->nnz = nnz; A->ro = ro;
+  A->col = (uint32_t *)amgd_alloc(nnz * 4 + 4);
+  A->a = (double *)amgd_alloc(nnz * 8 + 8);
+  k_bench_fill<<<grid_for(rn), 256, 0, s>>>(ro, rn, cn, gap, A->col, A->a);
+  KCHECK();
+  return A;
 }

@@ -151,8 +151,8 @@ API void amgd_test_qf_stats(uint64_t *out) {
 }
 
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
-extern void amgd_spmv_set_bn(int on);
-API void amgd_test_spmv_bn(int on) { amgd_spmv_set_bn(on); }
+extern void amgd_spmv_set_rw(int rw);
+API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_qfactor_set_coop_lds(int m);
 API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }
 extern void amgd_spgemm_force_flat(int on);
@@ -203,4 +203,28 @@ API int amgd_test_spmv_rows(const hcsr *HA, const uint32_t *list, uint32_t n, co
   amgd_free(dz); amgd_free(dl);
   dcsr_free(&A);
   return 0;
+}
+
+/* SpMV micro-benchmark: a generated matrix (amgd_bench_matrix), reps products timed
+   with HIP events on the library stream; with_x = 0: ordered row sums (no gather).
+   Returns ms per product and the matrix's nnz. */
+extern dcsr *amgd_bench_matrix(uint32_t rn, uint32_t cn, uint32_t len0, uint32_t len1, uint32_t gap);
+API double amgd_test_spmv_bench(uint32_t rn, uint32_t cn, uint32_t len0, uint32_t len1, uint32_t gap,
+                                int with_x, int reps, uint64_t *nnz) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = amgd_bench_matrix(rn, cn, len0, len1, gap);
+  double *x = (double *)amgd_alloc((size_t)cn * 8 + 8), *z = (double *)amgd_alloc((size_t)rn * 8 + 8);
+  amgd_vfill(x, cn, 0.5);
+  amgd_spmv(A, with_x ? x : NULL, z, 0.0, NULL, 1.0, NULL);   /* warm */
+  amgd_timer_reset();
+  for (int r = 0; r < reps; r++) {
+    amgd_timer_start(7);
+    amgd_spmv(A, with_x ? x : NULL, z, 0.0, NULL, 1.0, NULL);
+    amgd_timer_stop(7);
+  }
+  double ms = amgd_timer_ms(7) / reps;
+  *nnz = A->nnz;
+  amgd_free(x); amgd_free(z);
+  dcsr_free(&A);
+  return ms;
 }

@@ -189,12 +189,12 @@ def _rowsums(L):
     return refops.spmv(L, np.ones(L.cn))          # a*1.0 == a: the ordered row sums
 
 
-@pytest.fixture(params=[1, 0], ids=["bn", "lane0"])
-def bn(request):
-    """wave-per-row row sums: binade-grid chunk adds (default) or lane 0's ordered adds"""
-    oa.spmv_bn(request.param)
+@pytest.fixture(params=[-1, 4, 16, 64], ids=["rw_auto", "rw4", "rw16", "rw64"])
+def rw(request):
+    """rows per wavefront of the lane-per-row kernel (-1: chosen by row count)"""
+    oa.spmv_rw(request.param)
     yield request.param
-    oa.spmv_bn(-1)
+    oa.spmv_rw(-1)
 
 
 def _adversarial_rows(rng, rn=700):
@@ -239,15 +239,17 @@ def _adversarial_rows(rng, rn=700):
                       np.array(vals))
 
 
-def test_spmv_wave_adversarial_rows(bn):
-    """wave-per-row SpMV / row sums on adversarial rows, bit for bit against the
-    sequential loop (nan compared as nan)"""
+@pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
+def test_spmv_adversarial_rows(sl_min, rw):
+    """long-row SpMV / row sums / listed rows on adversarial rows through the wave-per-row
+    and the lane-per-row kernels (every RW), bit for bit against the sequential loop
+    (nan compared as nan)"""
     A = _adversarial_rows(np.random.default_rng(77))
     with np.errstate(all="ignore"):
         want_s = _rowsums(A)
         x = np.where(np.random.default_rng(3).random(A.cn) < 0.5, 1.0, 0.5)
         want = refops.spmv(A, x)
-    oa.spmv_sl_min(1 << 40)                      # whole matrix: wave-per-row kernel
+    oa.spmv_sl_min(sl_min)
     try:
         got_s = oa.test_spmv_f(A, None)
         got = oa.test_spmv(A, x)
@@ -261,8 +263,8 @@ def test_spmv_wave_adversarial_rows(bn):
                                                                        w[~np.isnan(w)].view(np.uint64))
 
 
-@pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
-def test_spmv_long_rows_ragged(sl_min, bn):
+@pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
+def test_spmv_long_rows_ragged(sl_min, rw):
     """long-row SpMV kernels on ragged rows: wave-per-row (default below 2^20 rows) and
     lane-per-row (forced with the row threshold at 0), with and without y, the f row
     mask and x = NULL (ordered row sums)"""
@@ -283,8 +285,8 @@ def test_spmv_long_rows_ragged(sl_min, bn):
         oa.spmv_sl_min(-1)
 
 
-@pytest.mark.parametrize("sl_min", [-1, 0], ids=["wave", "lane"])
-def test_spmv_rows_listed(sl_min, bn):
+@pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
+def test_spmv_rows_listed(sl_min, rw):
     """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
     threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
     rng = np.random.default_rng(29)

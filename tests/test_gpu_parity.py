@@ -42,17 +42,21 @@ def test_gpu_bitexact_vs_reference_fixture(case):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("mode", [(1 << 40, -1), (0, 64), (0, 16)], ids=["wave", "rw64", "rw16"])
 @pytest.mark.parametrize("case", ["p27_8", "sem_e3_N2", "p7_14", "aniso_12"])
-def test_gpu_bitexact_lane_spmv_forced(case):
-    """every SpMV with long rows (whole-matrix and listed rows) through the lane-per-row
-    kernel, which by default runs only from 2^20 / 65536 rows: hierarchy still bit-exact"""
+def test_gpu_bitexact_spmv_kernel_forced(case, mode):
+    """every SpMV with long rows (whole-matrix and listed rows) through the wave-per-row
+    kernel, or through the lane kernel with 64 / 16 rows per wavefront (small fixtures
+    pick 4 by default): hierarchy still bit-exact"""
     z = np.load(os.path.join(GOLD, case + ".npz"))
     ref = parity.from_npz(z)
-    oa.spmv_sl_min(0)
+    oa.spmv_sl_min(mode[0])
+    oa.spmv_rw(mode[1])
     try:
         h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
     finally:
         oa.spmv_sl_min(-1)
+        oa.spmv_rw(-1)
     bad = parity.compare(ref, h, exact=True)
     assert not bad, bad
 
