@@ -1665,22 +1665,25 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
 }
 // Symbolic pass for rows with many products: distinct columns counted with an LDS
 // byte map over a column window [wb, wb+SW) instead of a hash table (no probing, no
-// CAS; counting needs no order).  Each thread walks its own layers (B rows, sorted)
-// from a cursor while the columns stay inside the window; windows cover the row's
-// column range [cmin, cmax].  No capacity limit: every row gets its exact count.
+// CAS; counting needs no order).  Layers (B rows, sorted) are taken one WAVEFRONT
+// at a time: the 64 lanes load 64 consecutive columns from the layer's cursor
+// (one coalesced 256 B load), mark the in-window ones (a prefix, the row being
+// sorted) and advance the cursor by their count until the layer leaves the window.
+// Windows cover the row's column range [cmin, cmax].  No capacity limit: every row
+// gets its exact count.
 template <int SW>
 __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t nrows,
                                                  const uint64_t *aro, const uint32_t *acol,
                                                  const uint64_t *bro, const uint32_t *bcol,
                                                  uint64_t *cnt) {
-  constexpr int NT = 256, MAXL = 1024;
+  constexpr int NT = 256, NW = NT / 64, MAXL = 1024;
   __shared__ uint32_t map[SW / 4];
   __shared__ uint64_t lbs[MAXL];
   __shared__ uint32_t lend[MAXL], lcur[MAXL];
   __shared__ uint32_t s_min, s_max;
   __shared__ unsigned long long s_tot;
   uint8_t *mb = (uint8_t *)map;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     const uint64_t a0 = aro[i], a1 = aro[i + 1];
@@ -1710,23 +1713,20 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
       const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + SW - 1);
       for (int q = t; q < SW / 4; q += NT) map[q] = 0;
       __syncthreads();
-      for (uint32_t e = t; e < nl; e += NT) {
+      for (uint32_t e = wv; e < nl; e += NW) {
         const uint64_t b0 = lbs[e];
         const uint32_t L = lend[e];
         uint32_t c = lcur[e];
         while (c < L) {
-          uint32_t cc[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) cc[u] = (c + u < L) ? bcol[b0 + c + u] : 0xffffffffu;
-          int u = 0;
-          for (; u < 4; u++) {
-            if (cc[u] > we) break;
-            mb[cc[u] - wb] = 1;
-          }
-          c += u;
-          if (u < 4) break;
+          const uint32_t j = c + lane;
+          const uint32_t cc = j < L ? bcol[b0 + j] : 0xffffffffu;
+          const bool in = cc <= we;
+          if (in) mb[cc - wb] = 1;
+          const uint32_t n = (uint32_t)__popcll(__ballot(in));
+          c += n;
+          if (n < 64) break;                 // the layer left the window (or ended)
         }
-        lcur[e] = c;
+        if (lane == 0) lcur[e] = c;
       }
       __syncthreads();
       uint32_t n = 0;
@@ -1946,16 +1946,22 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_win<16384, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
                                            B->a, cnt2, cnt, tcol, ta);                          \
   }
+  static int nt3 = -1;           // AMGD_SG_NT3: threads of the 8192-slot k-sequential kernel
+  if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 256; }
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
     SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
-    SG_NUM(k_sg_kseq, 256, 13, 3, 8192u)
+    if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
+    else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
+    else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
   } else if (kseq) {
     SG_NUM(k_sg_kseq, 64, 9, 0, 65536u)
     SG_NUM(k_sg_kseq, 64, 11, 1, 65536u)
     SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
-    SG_NUM(k_sg_kseq, 256, 13, 3, 8192u)
+    if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
+    else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
+    else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
   } else {
     SG_NUM(k_sg_row, 64, 9, 0, 65536u)
     SG_NUM(k_sg_row, 64, 11, 1, 65536u)
