@@ -1082,6 +1082,47 @@ __device__ __forceinline__ void sg_emit(uint32_t *hk, double *hv, uint32_t *wtot
     __syncthreads();
   }
   const uint32_t n = base;
+  // Column order by rank: when the row's column span fits a bitmap in the free tail
+  // of hk (and its word prefix in the free tail of hv), each key's rank is the
+  // number of set bits below it -- O(n + span/32) instead of a bitonic sort.
+  __shared__ uint32_t s_mm[2];
+  if (t == 0) { s_mm[0] = 0xffffffffu; s_mm[1] = 0; }
+  __syncthreads();
+  {
+    uint32_t mn = 0xffffffffu, mx = 0;
+    for (uint32_t s = t; s < n; s += NT) { mn = min(mn, hk[s]); mx = max(mx, hk[s]); }
+    if (mn != 0xffffffffu) { atomicMin(&s_mm[0], mn); atomicMax(&s_mm[1], mx); }
+  }
+  __syncthreads();
+  const uint32_t cmin = s_mm[0], cmax = s_mm[1];
+  const uint32_t words = n ? ((cmax - cmin) >> 5) + 1 : 0;
+  if (n && words + 1 <= S - n) {
+    uint32_t *bm = hk + n;
+    uint32_t *pre = (uint32_t *)(hv + n);          // 2*(S-n) words free
+    for (uint32_t w = t; w < words; w += NT) bm[w] = 0;
+    __syncthreads();
+    for (uint32_t s = t; s < n; s += NT) {
+      const uint32_t d = hk[s] - cmin;
+      atomicOr(&bm[d >> 5], 1u << (d & 31));
+    }
+    __syncthreads();
+    const uint32_t per = (words + NT - 1) / NT, w0 = t * per, w1 = min(words, w0 + per);
+    uint32_t loc = 0;
+    for (uint32_t w = w0; w < w1; w++) loc += __popc(bm[w]);
+    const uint32_t incl = block_incl_scan<NT>(loc, wtot);
+    uint32_t run = incl - loc;
+    for (uint32_t w = w0; w < w1; w++) { pre[w] = run; run += __popc(bm[w]); }
+    __syncthreads();
+    for (uint32_t s = t; s < n; s += NT) {
+      const uint32_t k = hk[s], d = k - cmin, w = d >> 5;
+      const uint32_t rank = pre[w] + __popc(bm[w] & ((1u << (d & 31)) - 1u));
+      xcol[ob + rank] = k;
+      xa[ob + rank] = hv[s];
+    }
+    if (t == 0) *cnt_i = n;
+    __syncthreads();
+    return;
+  }
   uint32_t P = 1;
   while (P < n) P <<= 1;
   for (uint32_t s = n + t; s < P; s += NT) hk[s] = EMPTY_KEY;
@@ -1946,19 +1987,28 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_win<16384, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
                                            B->a, cnt2, cnt, tcol, ta);                          \
   }
-  static int nt3 = -1;           // AMGD_SG_NT3: threads of the 8192-slot k-sequential kernel
-  if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 256; }
+  // threads per row of the 4096- / 8192-slot k-sequential kernels (AMGD_SG_NT2 / _NT3):
+  // one row per work-group walks its layers one dependent step at a time, so more
+  // wavefronts per table keep more of each layer's loads in flight (256^3: RAP
+  // kernels 1876 -> 1619 ms with 1024 threads on the 8192-slot bin)
+  static int nt3 = -1, nt2 = -1;
+  if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 1024; }
+  if (nt2 < 0) { const char *e = getenv("AMGD_SG_NT2"); nt2 = e ? atoi(e) : 512; }
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
-    SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
+    if (nt2 == 1024) { SG_NUM(k_sg_kseq, 1024, 12, 2, 16384u) }
+    else if (nt2 == 512) { SG_NUM(k_sg_kseq, 512, 12, 2, 16384u) }
+    else { SG_NUM(k_sg_kseq, 256, 12, 2, 16384u) }
     if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
     else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
     else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
   } else if (kseq) {
     SG_NUM(k_sg_kseq, 64, 9, 0, 65536u)
     SG_NUM(k_sg_kseq, 64, 11, 1, 65536u)
-    SG_NUM(k_sg_kseq, 256, 12, 2, 16384u)
+    if (nt2 == 1024) { SG_NUM(k_sg_kseq, 1024, 12, 2, 16384u) }
+    else if (nt2 == 512) { SG_NUM(k_sg_kseq, 512, 12, 2, 16384u) }
+    else { SG_NUM(k_sg_kseq, 256, 12, 2, 16384u) }
     if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
     else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
     else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
