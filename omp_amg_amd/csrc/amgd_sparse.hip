@@ -1350,18 +1350,21 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
       __syncthreads();
       const int ne = (int)min((uint64_t)NT, a1 - wb);
       // chunks (layer e, offset j0) of up to 2*NT products, empty layers skipped; the
-      // next chunk's (column, product) loads are issued before the current chunk is
-      // inserted, so the HBM latency of layer k+1 overlaps the LDS work and barrier of k
-      int e = 0;
-      uint32_t j0 = 0;
-      while (e < ne && wlen[e] == 0) e++;
-      uint32_t ca = 0, cb = 0;
-      double pa = 0.0, pb = 0.0;
-      bool va = false, vb = false;
-      // raw B values are carried; the product is formed at insert time (forming it
-      // in fetch would wait for the load right there)
+      // (column, value) loads of the next KD chunks are in flight while the current
+      // chunk is inserted, so the HBM latency of the coming layers overlaps the LDS
+      // work and barriers of this one (a row is a chain of dependent layer steps)
+      constexpr int KD = 3;
+      int ce[KD];
+      uint32_t cj[KD], ca[KD], cb[KD];
+      double pa[KD], pb[KD];
+      bool va[KD], vb[KD];
+      int fe = 0;
+      uint32_t fj = 0;
+      while (fe < ne && wlen[fe] == 0) fe++;
       auto fetch = [&](int ee, uint32_t jj, uint32_t &xa_, uint32_t &xb_, double &ya, double &yb,
                        bool &fa, bool &fb) {
+        fa = fb = false;
+        if (ee >= ne) return;
         const uint32_t L = wlen[ee];
         const uint64_t b0 = wbs[ee];
         const uint32_t ja = jj + t, jb = jj + NT + t;
@@ -1370,35 +1373,48 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
         if (fa) { xa_ = bcol[b0 + ja]; if (MODE) ya = ba[b0 + ja]; }
         if (fb) { xb_ = bcol[b0 + jb]; if (MODE) yb = ba[b0 + jb]; }
       };
-      if (e < ne) fetch(e, 0, ca, cb, pa, pb, va, vb);
-      while (e < ne) {
-        int e2 = e;
-        uint32_t j2 = j0 + 2 * NT;
-        if (j2 >= wlen[e]) {
-          e2 = e + 1;
-          j2 = 0;
-          while (e2 < ne && wlen[e2] == 0) e2++;
+      auto step = [&]() {                           // the chunk after (fe, fj)
+        if (fe >= ne) return;
+        fj += 2 * NT;
+        if (fj >= wlen[fe]) {
+          fe++;
+          fj = 0;
+          while (fe < ne && wlen[fe] == 0) fe++;
         }
-        uint32_t na = 0, nb = 0;
-        double qa = 0.0, qb = 0.0;
-        bool fa = false, fb = false;
-        if (e2 < ne) fetch(e2, j2, na, nb, qa, qb, fa, fb);
-        const double a = MODE ? wav[e] : 0.0;
-        if (va) {
-          const uint32_t sl = sg_insert<LG>(hk, ca, &nfill, MODE == 0);
-          if (MODE) hv[sl] = hv[sl] + pa * a;
+      };
+#pragma unroll
+      for (int d = 0; d < KD; d++) {
+        ce[d] = fe;
+        cj[d] = fj;
+        ca[d] = cb[d] = 0;
+        pa[d] = pb[d] = 0.0;
+        fetch(fe, fj, ca[d], cb[d], pa[d], pb[d], va[d], vb[d]);
+        step();
+      }
+      // raw B values are carried; the product is formed at insert time
+      while (ce[0] < ne) {
+        const double a = MODE ? wav[ce[0]] : 0.0;
+        if (va[0]) {
+          const uint32_t sl = sg_insert<LG>(hk, ca[0], &nfill, MODE == 0);
+          if (MODE) hv[sl] = hv[sl] + pa[0] * a;
           else if (sl == EMPTY_KEY) ovf = 1;
         }
-        if (vb) {
-          const uint32_t sl = sg_insert<LG>(hk, cb, &nfill, MODE == 0);
-          if (MODE) hv[sl] = hv[sl] + pb * a;
+        if (vb[0]) {
+          const uint32_t sl = sg_insert<LG>(hk, cb[0], &nfill, MODE == 0);
+          if (MODE) hv[sl] = hv[sl] + pb[0] * a;
           else if (sl == EMPTY_KEY) ovf = 1;
         }
         if (MODE == 0 && (ovf || nfill > cap)) break;   // racy LDS read: early exit only
-        if (MODE == 1 && e2 != e) __syncthreads();      // layer k before layer k+1
-        e = e2;
-        j0 = j2;
-        ca = na; cb = nb; pa = qa; pb = qb; va = fa; vb = fb;
+        if (MODE == 1 && ce[1] != ce[0]) __syncthreads();   // layer k before layer k+1
+#pragma unroll
+        for (int d = 0; d + 1 < KD; d++) {
+          ce[d] = ce[d + 1]; cj[d] = cj[d + 1]; ca[d] = ca[d + 1]; cb[d] = cb[d + 1];
+          pa[d] = pa[d + 1]; pb[d] = pb[d + 1]; va[d] = va[d + 1]; vb[d] = vb[d + 1];
+        }
+        ce[KD - 1] = fe;
+        cj[KD - 1] = fj;
+        fetch(fe, fj, ca[KD - 1], cb[KD - 1], pa[KD - 1], pb[KD - 1], va[KD - 1], vb[KD - 1]);
+        step();
       }
       __syncthreads();
       if (MODE == 0 && (ovf || nfill > cap)) break;
