@@ -1604,6 +1604,7 @@ __global__ __launch_bounds__(256) void k_spgemm_long(
   __shared__ unsigned long long tot;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     uint32_t i = rows[r];
+    if (MODE == 0 && cnt[i] != OVERFLOW_MARK) continue;   // exact count already (wide bin)
     uint32_t tag = r + 1;  // stamps are unique per (block, row) visit
     if (threadIdx.x == 0) { lo_s = 0xffffffffu; hi_s = 0; tot = 0; }
     __syncthreads();
@@ -1726,8 +1727,9 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
 // at a time: the 64 lanes load 64 consecutive columns from the layer's cursor
 // (one coalesced 256 B load), mark the in-window ones (a prefix, the row being
 // sorted) and advance the cursor by their count until the layer leaves the window.
-// Windows cover the row's column range [cmin, cmax].  No capacity limit: every row
-// gets its exact count.
+// Windows cover the row's column range [cmin, cmax]; rows with more than MAXL layers
+// take them MAXL at a time.  No capacity limit: every row gets its exact count (no
+// dense-slab recount).
 template <int SW>
 __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t nrows,
                                                  const uint64_t *aro, const uint32_t *acol,
@@ -1744,19 +1746,20 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     const uint64_t a0 = aro[i], a1 = aro[i + 1];
-    if (a1 - a0 > (uint64_t)MAXL) {          // more layers than the table: dense-slab recount
-      if (t == 0) cnt[i] = OVERFLOW_MARK;
-      continue;
-    }
-    const uint32_t nl = (uint32_t)(a1 - a0);
+    const uint64_t nl = a1 - a0;
+    // rows with more layers than the table: the layers are taken MAXL at a time in
+    // every window, each chunk's cursors found by bisection for the window start
+    const bool chunked = nl > (uint64_t)MAXL;
     if (t == 0) { s_min = 0xffffffffu; s_max = 0; s_tot = 0; }
     __syncthreads();
-    for (uint32_t e = t; e < nl; e += NT) {
+    for (uint64_t e = t; e < nl; e += NT) {
       const uint32_t k = acol[a0 + e];
       const uint64_t b0 = bro[k], b1 = bro[k + 1];
-      lbs[e] = b0;
-      lend[e] = (uint32_t)(b1 - b0);
-      lcur[e] = 0;
+      if (!chunked) {
+        lbs[e] = b0;
+        lend[e] = (uint32_t)(b1 - b0);
+        lcur[e] = 0;
+      }
       if (b0 < b1) {
         atomicMin(&s_min, bcol[b0]);
         atomicMax(&s_max, bcol[b1 - 1]);
@@ -1770,7 +1773,26 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
       const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + SW - 1);
       for (int q = t; q < SW / 4; q += NT) map[q] = 0;
       __syncthreads();
-      for (uint32_t e = wv; e < nl; e += NW) {
+      for (uint64_t c0 = 0; c0 < nl; c0 += MAXL) {
+      const uint32_t nc = (uint32_t)min((uint64_t)MAXL, nl - c0);
+      if (chunked) {
+        for (uint32_t e = t; e < nc; e += NT) {
+          const uint32_t k = acol[a0 + c0 + e];
+          const uint64_t b0 = bro[k];
+          const uint32_t L = (uint32_t)(bro[k + 1] - b0);
+          uint32_t lo = 0, hi = L;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (bcol[b0 + mid] < wb) lo = mid + 1;
+            else hi = mid;
+          }
+          lbs[e] = b0;
+          lend[e] = L;
+          lcur[e] = lo;
+        }
+        __syncthreads();
+      }
+      for (uint32_t e = wv; e < nc; e += NW) {
         const uint64_t b0 = lbs[e];
         const uint32_t L = lend[e];
         uint32_t c = lcur[e];
@@ -1786,6 +1808,7 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
         if (lane == 0) lcur[e] = c;
       }
       __syncthreads();
+      }
       uint32_t n = 0;
       for (int q = t; q < SW / 4; q += NT) n += __popc(map[q] & 0x01010101u);
       atomicAdd(&s_tot, (unsigned long long)n);
@@ -2175,9 +2198,28 @@ __global__ void k_compact_rows(const uint64_t *sro, const uint32_t *scol, const 
     for (uint64_t t = 0; t < n; t++) { dcol[d0 + t] = scol[s0 + t]; da[d0 + t] = sa[s0 + t]; }
   }
 }
+// long rows: one wavefront per row, coalesced copies
+__global__ __launch_bounds__(256) void k_compact_rows_wave(const uint64_t *sro, const uint32_t *scol,
+                                                          const double *sa, const uint64_t *dro,
+                                                          uint32_t rn, uint32_t *dcol, double *da) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint64_t s0 = sro[i], d0 = dro[i], n = dro[i + 1] - d0;
+    for (uint64_t t = lane; t < n; t += 64) { dcol[d0 + t] = scol[s0 + t]; da[d0 + t] = sa[s0 + t]; }
+  }
+}
 void amgd_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *sa,
                        const uint64_t *dro, uint32_t rn, uint32_t *dcol, double *da) {
-  if (rn) k_compact_rows<<<grid_for(rn), 256, 0, amgd_s()>>>(sro, scol, sa, dro, rn, dcol, da);
+  if (!rn) return;
+  uint64_t nz = 0;
+  HIPCK(hipMemcpyAsync(&nz, dro + rn, 8, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  if (nz >= 16ull * rn)
+    k_compact_rows_wave<<<grid_for((uint64_t)rn * 64, 256, 65536), 256, 0, amgd_s()>>>(
+        sro, scol, sa, dro, rn, dcol, da);
+  else
+    k_compact_rows<<<grid_for(rn), 256, 0, amgd_s()>>>(sro, scol, sa, dro, rn, dcol, da);
   KCHECK();
 }
 
