@@ -13,11 +13,14 @@ value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup
           allgatherv over xGMI, value = rows / max-over-ranks seconds, scaling
           "strong"; --mode replicas runs N independent setups (value = N x rows /
           max time, scaling "weak").
-roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
+roofline: the dominant kernel by time, the long-row SpMV (k_spmv_lane<false,RW>,
+          whole-matrix products: find_support's sweeps, PCG, Lanczos), event-timed
+          live on the library stream; algorithmic bytes = 12 B per entry + 8 B
+          x gather per entry + 16 B per row.
+rap_roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
           and AfP = Af W; instantiated with RAP=1 so rocprof lists them apart;
           k_sg_kseq for long B-operand rows, k_sg_row for short ones, k_sg_win
-          for wide output rows),
-          event-timed live on the library stream; algorithmic bytes = 12 B per
+          for wide output rows), event-timed likewise; algorithmic bytes = 12 B per
           nnz of each operand and result + 8 B per row (DESIGN.md);
           tools/rap_from_prof.py sums the same kernels from a rocprofv3 summary.
 cpu_baseline: the reference's own serial setup (oracle/_ref/libref_amg.so,
@@ -65,7 +68,9 @@ def parse():
                    help="cap on the total time of the CPU baseline (all child runs)")
     p.add_argument("--cpu-child", nargs=2, type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic", type=float, default=None,
-                   help="RAP HBM bytes per launch from a rocprofv3 PMC pass (profiles/)")
+                   help="long-row SpMV HBM bytes per setup from rocprofv3 PMC passes (profiles/)")
+    p.add_argument("--rap-traffic", type=float, default=None,
+                   help="RAP SpGEMM HBM bytes per setup from rocprofv3 PMC passes (profiles/)")
     return p.parse_args()
 
 
@@ -206,7 +211,7 @@ def main():
         t_step = time.perf_counter() - t1
         warm += 1
     barrier()
-    rap_ms, rap_bytes, rap_nnz, st = 0.0, 0, 0, None
+    rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, st = 0.0, 0, 0, 0.0, 0, None
     steps = 0
     if sharded:
         shard.stats(reset=True)
@@ -221,6 +226,8 @@ def main():
         rap_ms += st["rap_kernel_ms"]
         rap_bytes += st["rap_bytes"]
         rap_nnz += st["rap_out_nnz"]
+        mv_ms += st["spmv_kernel_ms"]
+        mv_bytes += st["spmv_bytes"]
         if rank == 0:
             print(f"[bench] step {steps}: {t_step:.2f} s", file=sys.stderr, flush=True)
     barrier()
@@ -237,6 +244,7 @@ def main():
 
     if rank == 0:
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
+        mv_achieved = mv_bytes / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
         out = {
             "metric": "AMG setup rows/sec + RAP SpGEMM nnz/sec at 1/2/4/8 MI355X",
             "value": value,
@@ -264,9 +272,17 @@ def main():
             "rap_spgemm_nnz_per_s": copies * rap_nnz / (rap_ms * 1e-3) if rap_ms > 0 else None,
             "phases_ms": {k: round(st[k], 2) for k in ("t_build_ms", "t_coarsen_ms", "t_smoother_ms",
                                                           "t_interp_ms", "t_rap_ms")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
+            "roofline": {"bound": "hbm", "achieved": mv_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": mv_achieved / HBM_PEAK_GBS,
                          "traffic": args.traffic,
+                         "kernel": "k_spmv_lane<false,RW>: whole-matrix long-row SpMV (ordered row sums; "
+                                   "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
+                                   "HIP-event timed",
+                         "algorithmic_bytes_per_setup": mv_bytes / steps,
+                         "kernel_ms_per_setup": mv_ms / steps},
+            "rap_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": args.rap_traffic,
                          "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",

@@ -31,6 +31,8 @@ typedef struct {
   uint64_t rows0, nnz0;
   uint32_t nlevels, ub_events;   /* ub_events: inputs outside the reference's defined domain */
   size_t peak_bytes;
+  double spmv_kernel_ms;         /* whole-matrix long-row SpMV kernels (k_spmv_lane), event-timed */
+  uint64_t spmv_bytes;           /* their algorithmic HBM bytes */
 } amgd_stats;
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */

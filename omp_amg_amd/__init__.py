@@ -35,7 +35,8 @@ class AmgdStats(C.Structure):
                 ("rap_out_nnz", C.c_uint64), ("rap_bytes", C.c_uint64),
                 ("rows0", C.c_uint64), ("nnz0", C.c_uint64),
                 ("nlevels", C.c_uint32), ("ub_events", C.c_uint32),
-                ("peak_bytes", C.c_size_t)]
+                ("peak_bytes", C.c_size_t), ("spmv_kernel_ms", C.c_double),
+                ("spmv_bytes", C.c_uint64)]
 
 
 class HCsr(C.Structure):

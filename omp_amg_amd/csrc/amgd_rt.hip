@@ -228,16 +228,21 @@ static void tinit() {
   for (int i = 0; i < NTIMERS; i++) g_acc[i] = 0;
   g_tinit = true;
 }
+static std::vector<hipEvent_t> g_evpool;   // recycled timing events (thousands per setup)
+static hipEvent_t ev_get() {
+  if (!g_evpool.empty()) { hipEvent_t e = g_evpool.back(); g_evpool.pop_back(); return e; }
+  hipEvent_t e;
+  HIPCK(hipEventCreate(&e));
+  return e;
+}
 extern "C" void amgd_timer_start(int s) {
   tinit();
-  hipEvent_t a;
-  HIPCK(hipEventCreate(&a));
+  hipEvent_t a = ev_get();
   HIPCK(hipEventRecord(a, amgd_s()));
   g_t0[s] = a;
 }
 extern "C" void amgd_timer_stop(int s) {
-  hipEvent_t b;
-  HIPCK(hipEventCreate(&b));
+  hipEvent_t b = ev_get();
   HIPCK(hipEventRecord(b, amgd_s()));
   g_pend[s].push_back({g_t0[s], b});
 }
@@ -248,8 +253,8 @@ extern "C" double amgd_timer_ms(int s) {
     float ms = 0;
     HIPCK(hipEventElapsedTime(&ms, pr.first, pr.second));
     g_acc[s] += ms;
-    HIPCK(hipEventDestroy(pr.first));
-    HIPCK(hipEventDestroy(pr.second));
+    g_evpool.push_back(pr.first);
+    g_evpool.push_back(pr.second);
   }
   g_pend[s].clear();
   return g_acc[s];
@@ -973,6 +978,8 @@ extern "C" void amgd_rt_shutdown(void) {
       for (auto &pr : g_pend[i]) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
       g_pend[i].clear();
     }
+    for (hipEvent_t e : g_evpool) (void)hipEventDestroy(e);
+    g_evpool.clear();
     g_tinit = false;
   }
   (void)hipStreamDestroy(g_stream);

@@ -740,6 +740,8 @@ API void amgd_dev_sync(void) { amgd_sync(); }
 API void amgd_dev_upload(void *d, const void *h, size_t n) { amgd_h2d(d, h, n); }
 API void amgd_dev_download(void *h, const void *d, size_t n) { amgd_d2h(h, d, n); }
 
+extern uint64_t amgd_spmv_bytes(void);
+extern void amgd_spmv_bytes_reset(void);
 extern void amgd_spgemm_set_timer(int slot);
 extern void amgd_spgemm_bytes_reset(void);
 extern uint64_t amgd_spgemm_bytes(void);
@@ -754,6 +756,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
   memset(&g_st, 0, sizeof g_st);
   g_ub = 0;
   amgd_timer_reset();
+  amgd_spmv_bytes_reset();
   amgd_sync();
   double t_start = amgd_wtime(), t0 = t_start;
   dcsr *A = amgd_build_csr(nz, dAi, dAj, dAv);
@@ -868,6 +871,9 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
   amgd_sync();
   g_st.t_total_ms = (amgd_wtime() - t_start) * 1e3;
   g_st.rap_kernel_ms = amgd_timer_ms(0);
+  g_st.spmv_kernel_ms = amgd_timer_ms(1);
+  g_st.spmv_bytes = amgd_spmv_bytes();
+  amgd_spmv_bytes_reset();
   g_st.rap_bytes = amgd_spgemm_bytes();
   amgd_spgemm_bytes_reset();
   g_st.nlevels = h->nlevels;

@@ -585,6 +585,11 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
 }
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                       double beta, const uint8_t *f);
+// algorithmic bytes of the event-timed (timer slot 1) lane-kernel products: each entry's
+// column + value once, x gathered once per entry, row offsets, z (and y, f) once per row
+static uint64_t g_mv_bytes = 0;
+extern "C" uint64_t amgd_spmv_bytes(void) { return g_mv_bytes; }
+extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = 0; }
 // AMGD_MVLOG=1: one line per whole-matrix SpMV (rows, nnz, kernel, time, effective GB/s)
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
@@ -615,7 +620,11 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   }
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
+    amgd_timer_start(1);                       // roofline: whole-matrix long-row products
     LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f);
+    amgd_timer_stop(1);
+    g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + 16ull * M->rn + 8 +
+                  (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
     k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
