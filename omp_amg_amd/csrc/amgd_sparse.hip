@@ -37,6 +37,18 @@ __global__ void k_row_of_entry(const uint64_t *ro, uint32_t rn, uint32_t *row) {
     for (uint64_t k = ro[i]; k < ro[i + 1]; k++) row[k] = (uint32_t)i;
   }
 }
+// long rows: one wavefront per row (coalesced writes)
+__global__ void k_row_of_entry_wave(const uint64_t *ro, uint32_t rn, uint32_t *row) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6)
+    for (uint64_t k = ro[i] + lane; k < ro[i + 1]; k += 64) row[k] = (uint32_t)i;
+}
+#define WAVE_ROWS_MIN_MEAN 16   // mean row length from which per-row loops go wave-per-row
+static inline bool long_rows(uint64_t nnz, uint32_t rn) {
+  return rn && nnz >= (uint64_t)WAVE_ROWS_MIN_MEAN * rn;
+}
+static inline int wave_grid(uint32_t rn) { return grid_for((uint64_t)rn * 64, 256, 65536); }
 __global__ void k_fill_u64(uint64_t *p, uint64_t n, uint64_t v) { GRID_STRIDE(i, n) p[i] = v; }
 void amgd_row_of_entry_launch(const uint64_t *ro, uint32_t rn, uint32_t *row) {
   if (rn) k_row_of_entry<<<grid_for(rn), 256, 0, amgd_s()>>>(ro, rn, row);
@@ -155,6 +167,48 @@ __global__ void k_sub_fill(const uint64_t *ro, const uint32_t *col, const double
     }
   }
 }
+// long rows: one wavefront per row -- the kept entries of a 64-entry chunk are
+// placed by a ballot prefix, in order
+__global__ void k_sub_count_wave(const uint64_t *ro, const uint32_t *col, uint32_t rn,
+                                 const uint8_t *vr, const uint8_t *vc, const uint32_t *rmap,
+                                 uint64_t *cnt) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    if (!vr[i]) continue;
+    uint64_t c = 0;
+    for (uint64_t k0 = ro[i]; k0 < ro[i + 1]; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      c += __popcll(__ballot(k < ro[i + 1] && vc[col[k]]));
+    }
+    if (lane == 0) cnt[rmap[i]] = c;
+  }
+}
+__global__ void k_sub_fill_wave(const uint64_t *ro, const uint32_t *col, const double *a,
+                                uint32_t rn, const uint8_t *vr, const uint8_t *vc,
+                                const uint32_t *rmap, const uint32_t *cmap, const uint64_t *sro,
+                                uint32_t *scol, double *sa) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    if (!vr[i]) continue;
+    uint64_t o = sro[rmap[i]];
+    for (uint64_t k0 = ro[i]; k0 < ro[i + 1]; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      uint32_t c = 0;
+      bool keep = false;
+      if (k < ro[i + 1]) { c = col[k]; keep = vc[c] != 0; }
+      const unsigned long long m = __ballot(keep);
+      if (keep) {
+        const uint64_t q = o + __popcll(m & below);
+        scol[q] = cmap[c];
+        sa[q] = a[k];
+      }
+      o += __popcll(m);
+    }
+  }
+}
 extern "C" dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *vc) {
   hipStream_t s = amgd_s();
   uint32_t *rmap = (uint32_t *)amgd_alloc(((size_t)A->rn + 1) * 4);
@@ -162,14 +216,21 @@ extern "C" dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *v
   uint32_t srn = amgd_mask_rank(vr, A->rn, rmap);
   uint32_t scn = amgd_mask_rank(vc, A->cn, cmap);
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)srn + 1) * 8);
-  if (A->rn) k_sub_count<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->rn, vr, vc, rmap, cnt);
+  const bool lr = long_rows(A->nnz, A->rn);
+  if (A->rn && lr)
+    k_sub_count_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->rn, vr, vc, rmap, cnt);
+  else if (A->rn)
+    k_sub_count<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->rn, vr, vc, rmap, cnt);
   KCHECK();
   uint64_t nz = amgd_scan_u64(cnt, srn);
   dcsr *S = (dcsr *)malloc(sizeof(dcsr));
   S->rn = srn; S->cn = scn; S->nnz = nz; S->ro = cnt;
   S->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
   S->a = (double *)amgd_alloc(nz * 8 + 8);
-  if (A->rn)
+  if (A->rn && lr)
+    k_sub_fill_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, vr, vc, rmap, cmap,
+                                                      S->ro, S->col, S->a);
+  else if (A->rn)
     k_sub_fill<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, vr, vc, rmap, cmap,
                                                 S->ro, S->col, S->a);
   KCHECK();
@@ -270,7 +331,8 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   T->a = (double *)amgd_alloc(nz * 8 + 8);
   if (nz) {
     uint32_t *row = (uint32_t *)amgd_alloc(nz * 4 + 4);
-    k_row_of_entry<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
+    if (long_rows(nz, A->rn)) k_row_of_entry_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
+    else k_row_of_entry<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
     if (narrow)
       k_tr_fill<uint32_t><<<grid_for(nz), 256, 0, s>>>((const uint32_t *)perm, row, A->a, nz,
                                                        T->col, T->a);
@@ -297,6 +359,17 @@ __global__ void k_rowmask_fill(const uint64_t *ro, const uint32_t *col, const do
     for (uint64_t k = ro[i]; k < ro[i + 1]; k++, o++) { xcol[o] = col[k]; xa[o] = a[k]; }
   }
 }
+__global__ void k_rowmask_fill_wave(const uint64_t *ro, const uint32_t *col, const double *a,
+                                    uint32_t rn, const uint8_t *m, const uint64_t *xro,
+                                    uint32_t *xcol, double *xa) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    if (!m[i]) continue;
+    const uint64_t k0 = ro[i], o = xro[i], n = ro[i + 1] - k0;
+    for (uint64_t t = lane; t < n; t += 64) { xcol[o + t] = col[k0 + t]; xa[o + t] = a[k0 + t]; }
+  }
+}
 extern "C" dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask) {
   hipStream_t s = amgd_s();
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
@@ -306,7 +379,10 @@ extern "C" dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask) {
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
   X->a = (double *)amgd_alloc(nz * 8 + 8);
-  if (A->rn && nz)
+  if (A->rn && nz && long_rows(A->nnz, A->rn))
+    k_rowmask_fill_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, mask, X->ro,
+                                                          X->col, X->a);
+  else if (A->rn && nz)
     k_rowmask_fill<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, mask, X->ro, X->col, X->a);
   KCHECK();
   return X;
