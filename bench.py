@@ -126,6 +126,18 @@ def cpu_baseline(m, reps, budget_s):
                       f"O(rows^2) and it does not terminate on many larger grids, so 256^3 is out of its reach)"}
 
 
+def pmc_traffic():
+    """HBM bytes per setup of the two roofline kernels from the committed rocprofv3
+    PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass, gfx950 correction;
+    tools/gpurun_round.sh) on this same workload: (spmv, rap, source) or Nones"""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_r*.json")))
+    if not files:
+        return None, None, None
+    d = json.load(open(files[-1]))
+    return d["spmv"]["hbm_bytes"], d["rap"]["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+
+
 def heartbeat(period=30.0):
     """progress line on stderr while a long setup runs (keeps batch runners from
     taking a silent multi-minute setup for a hang)"""
@@ -243,6 +255,11 @@ def main():
     comm = shard.stats() if sharded else None
 
     if rank == 0:
+        t_mv, t_rap, t_src = pmc_traffic()
+        if args.traffic is not None:
+            t_mv, t_src = args.traffic, "--traffic"
+        if args.rap_traffic is not None:
+            t_rap = args.rap_traffic
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
         mv_achieved = mv_bytes / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
         out = {
@@ -274,7 +291,9 @@ def main():
                                                           "t_interp_ms", "t_rap_ms")},
             "roofline": {"bound": "hbm", "achieved": mv_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": mv_achieved / HBM_PEAK_GBS,
-                         "traffic": args.traffic,
+                         "traffic": t_mv,
+                         "traffic_unit": "bytes per setup (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": t_src,
                          "kernel": "k_spmv_lane<false,RW>: whole-matrix long-row SpMV (ordered row sums; "
                                    "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
                                    "HIP-event timed",
@@ -282,7 +301,9 @@ def main():
                          "kernel_ms_per_setup": mv_ms / steps},
             "rap_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": args.rap_traffic,
+                         "traffic": t_rap,
+                         "traffic_unit": "bytes per setup (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": t_src,
                          "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",

@@ -745,7 +745,6 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
   __shared__ double s_sh;
   __shared__ int viol_sh;
   __shared__ SpecRec rb[SP_BATCH];
-  __shared__ unsigned long long cnext;
   const int tid = threadIdx.x;
   const uint64_t G = (n + BN_TILE - 1) / BN_TILE;
   const long long LO = (1ll << 52), HI = (1ll << 53);
@@ -756,36 +755,39 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
     __syncthreads();
     uint64_t c = cb;
     while (c < ce) {
-      if (tid == 0) {
-        // runs of chunks guessed in one binade e are walked on the integer grid of
-        // that binade (S stays strictly inside (2^52, 2^53), so t = S * 2^(e-52)
-        // is exact and lies in binade e): the double is formed once per run
-        double t = s;
-        uint64_t q = c;
-        while (q < ce) {
-          const SpecRec r = rb[q - cb];
-          if (r.flag || !(fabs(t) >= 2.2250738585072014e-308) || ilogb(t) != r.e) break;
-          const int e = r.e;
-          long long S = (long long)ldexp(t, 52 - e);
-          const uint64_t q0 = q;
-          for (; q < ce; q++) {
-            const SpecRec rr = rb[q - cb];
-            if (rr.flag || rr.e != e) break;
-            const bool ok = S > 0 ? (S + rr.mn > LO && S + rr.mx < HI)
-                                  : (S + rr.mx < -LO && S + rr.mn > -HI);
-            if (!ok) break;
-            S += rr.M;
-          }
-          t = ldexp((double)S, e - 52);
-          if (q == q0) break;             // no progress: the chunk is added exactly below
-        }
-        s_sh = t;
-        cnext = q;
+      // The run of chunks from c guessed in the running sum's binade e is found by
+      // all threads at once (one chunk per thread, SP_BATCH <= BN_THREADS): chunk q
+      // passes if its guess is e and the running integer sum S + M_c + ... + M_{q-1}
+      // plus its own prefix extremes stays strictly inside (2^52, 2^53); the sum
+      // over the passing prefix is exact (every partial sum before the first failing
+      // chunk is bounded by the binade), so s = (S + P) * 2^(e-52) exactly -- the
+      // serial walk's result in one block scan.
+      const bool normal = fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1.0e300;
+      const int e = normal ? ilogb(s) : 0;
+      const long long S = normal ? (long long)ldexp(s, 52 - e) : 0ll;
+      const uint64_t q = c + (uint64_t)tid;
+      SpecRec r;
+      r.M = 0; r.mn = 0; r.mx = 0; r.e = 0; r.flag = 1;
+      if (q < ce) r = rb[q - cb];
+      bool ok = q < ce && normal && !r.flag && r.e == e;
+      long long total;
+      const long long pre = bn_block_excl_scan(ok ? r.M : 0ll, sh, &total);
+      if (ok) {
+        const long long base = (long long)((unsigned long long)S + (unsigned long long)pre);
+        ok = S > 0 ? (base + r.mn > LO && base + r.mx < HI) : (base + r.mx < -LO && base + r.mn > -HI);
       }
+      if (tid == 0) viol_sh = 0x7fffffff;
       __syncthreads();
-      s = s_sh;
-      c = cnext;
+      if (q < ce && !ok) atomicMin(&viol_sh, tid);
       __syncthreads();
+      const int f = viol_sh;                                  // chunks c .. c+f-1 pass
+      const uint64_t run_end = f == 0x7fffffff ? ce : c + (uint64_t)f;
+      if (run_end > c && (uint64_t)tid == run_end - 1 - c)
+        s_sh = ldexp((double)(long long)((unsigned long long)S + (unsigned long long)(pre + r.M)), e - 52);
+      __syncthreads();
+      if (run_end > c) s = s_sh;
+      __syncthreads();
+      c = run_end;
       if (c < ce) {                         // speculation failed: add this chunk exactly
         uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
         s = binade_range<MODE>(a, b, lo, hi, s, tile, sh, &s_sh, &viol_sh);

@@ -360,12 +360,12 @@ def _seq(p):
 
 
 @pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel",
-                                  "hover", "big"])
+                                  "hover", "big", "pos_big", "spikes"])
 def test_exact_dot_matches_sequential(kind):
     """The binade-parallel exact sum (single block below 64K products, chunk
     speculation over all CUs above) equals the left-to-right loop bit for bit."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
-    n = 3000000 if kind == "big" else 300000
+    n = 3000000 if kind in ("big", "pos_big", "spikes") else 300000
     if kind == "normal":
         a, b = rng.standard_normal(n), rng.standard_normal(n)
     elif kind == "positive":
@@ -380,6 +380,10 @@ def test_exact_dot_matches_sequential(kind):
         a = rng.choice([-1.0, 1.0], n) * 2.0 ** -30; a[0] = 1.0; b = np.ones(n)
     elif kind == "big":       # more chunks than one record batch
         a, b = rng.standard_normal(n) + 0.01, rng.standard_normal(n) + 0.02
+    elif kind == "pos_big":   # monotone sum: binade crossings inside chunks, long passing runs
+        a = np.abs(rng.standard_normal(n)) + 1e-3; b = np.abs(rng.standard_normal(n)) + 1e-3
+    elif kind == "spikes":    # products far above the running sum now and then (huge grid steps)
+        a = rng.standard_normal(n) * 1e-6; a[rng.integers(0, n, 40)] = 1e12; b = np.ones(n)
     elif kind == "range":
         a = rng.standard_normal(n) * 10.0 ** rng.integers(-40, 40, n); b = rng.standard_normal(n)
     else:

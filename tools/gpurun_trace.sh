@@ -1,14 +1,20 @@
+# rocprofv3 kernel trace (per-launch durations kept) + SGLOG of one 256^3 setup
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD
-M=${1:-128}
-rm -rf gpurun_out/trace$M; mkdir -p gpurun_out/trace$M
+rm -rf gpurun_out/trace256; mkdir -p gpurun_out/trace256
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/trace$M -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/probe_scale.py $M > $GRAFT_REPO_ROOT/gpurun_out/trace$M.log 2>&1; echo "prof rc=$?"
-cd $GRAFT_REPO_ROOT && python3 - <<'PY'
-import csv, collections, sys
-M = sys.argv[1] if len(sys.argv) > 1 else "128"
+AMGD_SGLOG=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/trace256 -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/probe_scale.py 256 > $GRAFT_REPO_ROOT/gpurun_out/trace256.log 2>&1; rc=$?
+echo "prof rc=$rc"
+cd $GRAFT_REPO_ROOT
+python3 - <<'PY'
+import csv, collections
+rows = list(csv.DictReader(open('gpurun_out/trace256/run_kernel_trace.csv')))
+print(len(rows), 'launches')
+with open('gpurun_out/trace256/launches.txt', 'w') as f:
+    for r in rows:
+        f.write(f"{int(r['End_Timestamp']) - int(r['Start_Timestamp'])} {r['Start_Timestamp']} {r['Kernel_Name'][:90]}\n")
 PY
-ls -la gpurun_out/trace$M
-grep '"m"' gpurun_out/trace$M.log
+rm -f gpurun_out/trace256/run_kernel_trace.csv
+exit $rc
