@@ -309,30 +309,55 @@ __global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint3
     __syncthreads();
     for (uint32_t k0 = 0; k0 < nz; k0 += B) {
       const uint32_t bn = min((uint32_t)B, nz - k0);
-      // s1 rows of the block (zero, then scatter or look up)
+      // s1 rows of the block (zero, then scatter or look up).  All bn rows are
+      // gathered in one flat pass over (row, entry) or (row, m) pairs, so the loads
+      // of the whole block are in flight together instead of row after row.
       for (uint32_t b = 0; b < bn; b++)
         for (uint32_t m = t; m <= k0 + b; m += NT) S1[b * PAD + m] = 0.0;
+      uint64_t ra0[B];
+      uint32_t rlen[B], spre[B + 1], lpre[B + 1];
+      uint32_t look_cost = 0, scan_cost = 0;
+      spre[0] = lpre[0] = 0;
+#pragma unroll
+      for (int b = 0; b < B; b++) {
+        ra0[b] = 0;
+        rlen[b] = 0;
+        if ((uint32_t)b < bn) {
+          const uint32_t k = k0 + b, sk = Qs[k];
+          ra0[b] = aro[sk];
+          rlen[b] = (uint32_t)(aro[sk + 1] - ra0[b]);
+          const uint32_t lg_len = 32 - __clz(rlen[b] | 1), lg_k = 32 - __clz(k + 1);
+          look_cost += (k + 1) * lg_len * 4;
+          scan_cost += rlen[b] * (4 + lg_k);
+        }
+        spre[b + 1] = spre[b] + rlen[b];
+        lpre[b + 1] = lpre[b] + ((uint32_t)b < bn ? k0 + b + 1 : 0u);
+      }
       __syncthreads();
-      for (uint32_t b = 0; b < bn; b++) {
-        const uint32_t k = k0 + b, sk = Qs[k];
-        const uint64_t a0 = aro[sk], a1 = aro[sk + 1];
-        const uint32_t len = (uint32_t)(a1 - a0);
-        const uint32_t lg_len = 32 - __clz(len | 1), lg_k = 32 - __clz(k + 1);
-        if (((k + NT) / NT) * lg_len * 4 < ((len + NT - 1) / NT) * (4 + lg_k)) {
-          for (uint32_t m = t; m <= k; m += NT)
-            S1[b * PAD + m] = row_lookup(acol, aa, a0, a1, Qs[m]);
-        } else {
-          for (uint64_t e = a0 + t; e < a1; e += NT) {
-            const uint32_t j = acol[e];
-            if (e > a0 && acol[e - 1] == j) continue;
-            uint32_t lo = 0, hi = k + 1;
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (Qs[mid] < j) lo = mid + 1;
-              else hi = mid;
-            }
-            if (lo <= k && Qs[lo] == j) S1[b * PAD + lo] = aa[e];
+      if (look_cost < scan_cost) {
+        for (uint32_t fl = t; fl < lpre[B]; fl += NT) {
+          uint32_t b = 0;
+#pragma unroll
+          for (int q = 1; q < B; q++) b += fl >= lpre[q] ? 1u : 0u;
+          const uint32_t m = fl - lpre[b];
+          S1[b * PAD + m] = row_lookup(acol, aa, ra0[b], ra0[b] + rlen[b], Qs[m]);
+        }
+      } else {
+        for (uint32_t fl = t; fl < spre[B]; fl += NT) {
+          uint32_t b = 0;
+#pragma unroll
+          for (int q = 1; q < B; q++) b += fl >= spre[q] ? 1u : 0u;
+          const uint64_t a0 = ra0[b], e = a0 + (fl - spre[b]);
+          const uint32_t k = k0 + b;
+          const uint32_t j = acol[e];
+          if (e > a0 && acol[e - 1] == j) continue;
+          uint32_t lo = 0, hi = k + 1;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (Qs[mid] < j) lo = mid + 1;
+            else hi = mid;
           }
+          if (lo <= k && Qs[lo] == j) S1[b * PAD + lo] = aa[e];
         }
       }
       __syncthreads();
@@ -919,24 +944,40 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
   else if (hn[0])
     k_qfactor_lds<QF_T0, 64><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
         lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[1] && (t2blk & 2))
+  static int bsm = -1;      // AMGD_QF_BSMALL: k-steps per pass of the 64- / 128-point tiers
+  if (bsm < 0) bsm = getenv("AMGD_QF_BSMALL") ? atoi(getenv("AMGD_QF_BSMALL")) : 4;
+  if (hn[1] && (t2blk & 2) && bsm == 4)
+    k_qfactor_blk<QF_T1, 4, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
+        lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  else if (hn[1] && (t2blk & 2))
     k_qfactor_blk<QF_T1, 8, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
         lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   else if (hn[1])
     k_qfactor_lds<QF_T1, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
         lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[2] && (t2blk & 1))
+  if (hn[2] && (t2blk & 1) && bsm == 4)
+    k_qfactor_blk<QF_T2, 4, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
+        lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+  else if (hn[2] && (t2blk & 1))
     k_qfactor_blk<QF_T2, 8, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
         lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   else if (hn[2])
     k_qfactor_lds<QF_T2, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
         lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   if (qf_blocked()) {
-    if (hn[3])
+    // B = 4 k-steps per pass for the 256- and 512-point tiers: the waves mostly wait
+    // (SQ_WAIT_ANY ~80 %), and the smaller S1/S2 tiles let 4 blocks share a CU
+    // (512 tier, 47782-column call at 256^3: B 8 -> 4: 419 -> 318 ms)
+    static int v256 = -1;   // AMGD_QF_B256: steps per pass of the 256-point tier (4 or 8)
+    if (v256 < 0) v256 = getenv("AMGD_QF_B256") ? atoi(getenv("AMGD_QF_B256")) : 4;
+    if (hn[3] && v256 == 8)
       k_qfactor_blk<256, 8><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
           lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
+    else if (hn[3])
+      k_qfactor_blk<256, 4><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
+          lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
     if (hn[4])
-      k_qfactor_blk<512, 8><<<(int)std::min<unsigned>(hn[4], 8192u), 256, 0, s>>>(
+      k_qfactor_blk<512, 4><<<(int)std::min<unsigned>(hn[4], 8192u), 256, 0, s>>>(
           lists + 4 * L, hn[4], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
     if (hn[5])
       k_qfactor_blk<QF_T3, 4><<<(int)std::min<unsigned>(hn[5], 8192u), 256, 0, s>>>(
