@@ -101,6 +101,7 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
+        L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
@@ -314,6 +315,11 @@ def qf_coop_lds(m: int) -> None:
     """dense cooperative huge-support factor: supports up to m points stage s1/s2/qk in
     LDS, larger ones read them from global memory (-1: default 8192)"""
     lib().amgd_test_qf_coop_lds(int(m))
+
+
+def qa_huge(n: int) -> None:
+    """Q application: supports above n points run the grid-wide kernels (-1: default 8192)"""
+    lib().amgd_test_qa_huge(int(n))
 
 
 def qf_stats() -> dict:

@@ -90,6 +90,7 @@ dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J, const doub
                    uint32_t rn, uint32_t cn, int drop_zero);
 dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *vc);
 dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out);
+dcsr *amgd_drop_zeros(const dcsr *A);                      /* exactly-zero entries removed */
 dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask);  /* rows with mask==0 emptied */  /* perm: CSC idx -> CSR idx */
 dcsr *amgd_spgemm(const dcsr *A, const dcsr *B);           /* A*B, reference semantics */
 dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *B);
@@ -201,6 +202,10 @@ void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback] since th
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                         const double *w, double *sumR, double thr,
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
+/* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
+   returns the count, > cap when the list overflowed */
+uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,
+                        uint32_t tag, uint32_t *out, uint32_t cap);
 uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad);
 uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_t **pi, uint32_t **pj);
 void amgd_skel_binarize(dcsr *A, int mode);

@@ -1109,11 +1109,64 @@ __global__ __launch_bounds__(NT) void k_qapply(const uint32_t *rows, uint32_t nr
     __syncthreads();
   }
 }
+// Huge supports (> QA_HUGE points: the orphan support of min_skel's zero column) are
+// applied by three grid-wide kernels instead of one work-group: the same sums in the
+// same order, spread over the chip (one lane per row of U for sqv2, one lane per
+// column for out, lanes of a wave in lock-step over 32-element batches).
+#define QA_HUGE 8192
+static uint32_t g_qa_huge = QA_HUGE;      // tests: smaller sends more supports to the grid path
+extern "C" void amgd_qapply_set_huge(int n) { g_qa_huge = n < 0 ? QA_HUGE : (uint32_t)n; }
+__global__ void k_qa_big_s1(uint32_t c, const uint64_t *wro, const uint32_t *wcol,
+                            const uint64_t *bro, const uint32_t *bcol, const double *ba,
+                            const double *u, const double *lambda, double *sqv1) {
+  const uint64_t w0 = wro[c];
+  const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+  const uint64_t b0 = bro[c], b1 = bro[c + 1];
+  const double uc = u[c];
+  GRID_STRIDE(m, nz) {
+    const uint32_t j = wcol[w0 + m];
+    sqv1[m] = row_lookup(bcol, ba, b0, b1, j) + uc * lambda[j];
+  }
+}
+__global__ void k_qa_big_rows(uint32_t nz, const double *U, const double *sqv1, double *sqv2) {
+  GRID_STRIDE(i, nz) sqv2[i] = seq_dot_batched(U + tri(i), sqv1, (uint32_t)i + 1);
+}
+__global__ void k_qa_big_cols(uint32_t nz, const double *U, const double *sqv2, double *out) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t ib = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) - lane; ib < nz;
+       ib += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t i = (uint32_t)ib + lane;
+    const double y = mv_ut_lane(U, sqv2, (uint32_t)ib, i, nz);
+    if (i < nz) out[i] = y;
+  }
+}
 static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
                          const double *u, const double *lambda, double *out, uint32_t cb,
                          uint32_t ce) {
   hipStream_t s = amgd_s();
   RowSplit rs = split_rows(Wt, QF_LDS_NZ, cb, ce);
+  if (rs.nb && rs.maxnz > g_qa_huge) {          // the huge supports: grid-wide kernels
+    std::vector<uint32_t> bl(rs.nb);
+    amgd_d2h(bl.data(), rs.bl, (size_t)rs.nb * 4);
+    std::vector<uint64_t> ro(Wt->rn + 1ull), qo(Wt->rn + 1ull);
+    amgd_d2h(ro.data(), Wt->ro, ((size_t)Wt->rn + 1) * 8);
+    amgd_d2h(qo.data(), qoff, ((size_t)Wt->rn + 1) * 8);
+    std::vector<uint32_t> keep;
+    double *scr = (double *)amgd_alloc(2 * rs.maxnz * 8 + 16);
+    for (uint32_t c : bl) {
+      const uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
+      if (nz <= g_qa_huge) { keep.push_back(c); continue; }
+      double *sqv1 = scr, *sqv2 = scr + rs.maxnz + 1;
+      k_qa_big_s1<<<grid_for(nz), 256, 0, s>>>(c, Wt->ro, Wt->col, Bt->ro, Bt->col, Bt->a, u,
+                                              lambda, sqv1);
+      k_qa_big_rows<<<grid_for(nz), 256, 0, s>>>(nz, Q + qo[c], sqv1, sqv2);
+      k_qa_big_cols<<<grid_for(nz), 256, 0, s>>>(nz, Q + qo[c], sqv2, out + ro[c]);
+      KCHECK();
+    }
+    amgd_free(scr);
+    rs.nb = (unsigned)keep.size();
+    if (rs.nb) amgd_h2d(rs.bl, keep.data(), (size_t)rs.nb * 4);
+  }
   if (rs.ns) {
     int g = (int)std::min<unsigned>(rs.ns, 65536u);
     k_qapply<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
@@ -1479,6 +1532,58 @@ __global__ __launch_bounds__(256) void k_list_rowsum(const uint64_t *ro, const d
     if (lane == 0) out[i] = t;
   }
 }
+// Incremental find_support sweeps: the distinct neighbours (columns of M) of the listed
+// rows, first visit claimed by an exchange of the neighbour's stamp with `tag`.
+// Returns the count, which may exceed cap (the list is then incomplete: the caller
+// falls back to full products).
+__global__ void k_fs_expand(const uint64_t *ro, const uint32_t *col, const uint32_t *list,
+                            uint32_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                            unsigned *cnt, uint32_t cap) {
+  GRID_STRIDE(r, n) {
+    const uint32_t i = list[r];
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++) {
+      const uint32_t c = col[k];
+      if (atomicExch(&stamp[c], tag) != tag) {
+        const unsigned p = atomicAdd(cnt, 1u);
+        if (p < cap) out[p] = c;
+      }
+    }
+  }
+}
+__global__ void k_fs_expand_wave(const uint64_t *ro, const uint32_t *col, const uint32_t *list,
+                                 uint32_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                                 unsigned *cnt, uint32_t cap) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n;
+       r += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t i = list[r];
+    for (uint64_t k0 = ro[i]; k0 < ro[i + 1]; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      bool fresh = false;
+      uint32_t c = 0;
+      if (k < ro[i + 1]) { c = col[k]; fresh = atomicExch(&stamp[c], tag) != tag; }
+      const unsigned p = wave_append(cnt, fresh);
+      if (fresh && p < cap) out[p] = c;
+    }
+  }
+}
+extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,
+                                   uint32_t tag, uint32_t *out, uint32_t cap) {
+  if (!n) return 0;
+  unsigned *cnt = (unsigned *)amgd_alloc(16);
+  amgd_memset(cnt, 0, 4);
+  if (M->rn && M->nnz >= 16ull * M->rn)
+    k_fs_expand_wave<<<grid_for((uint64_t)n * 64, 256, 16384), 256, 0, amgd_s()>>>(
+        M->ro, M->col, list, n, stamp, tag, out, cnt, cap);
+  else
+    k_fs_expand<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, M->col, list, n, stamp, tag, out, cnt, cap);
+  KCHECK();
+  unsigned h = 0;
+  amgd_d2h(&h, cnt, 4);
+  amgd_free(cnt);
+  return h;
+}
+
 // One selection sweep: select + remove, then bring rs (row sums of R) and sumR
 // (column sums) up to date for the rows / columns that lost an entry.
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,

@@ -413,7 +413,13 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
   amgd_vop(au2, u, u, nc, AMGD_V_MUL);
   amgd_vop(au2, au2, alpha, nc, AMGD_V_MUL);
   if (!fac->S) {
-    fac->S = amgd_spgemm(W_skel, fac->Wt);           /* W_skel * W_skel' (mxm iftrsp=1) */
+    /* W_skel * W_skel' (mxm iftrsp=1) with its exact zeros dropped.  The zero-valued
+       skeleton entries (min_skel's orphans at column 0) contribute +0 products only,
+       so the product of the operands without them is the same matrix, values and
+       pattern -- without the orphans' dense all-zero block of products. */
+    dcsr *Wn = amgd_drop_zeros(W_skel), *Wnt = amgd_drop_zeros(fac->Wt);
+    fac->S = amgd_spgemm(Wn, Wnt);
+    dcsr_free(&Wn); dcsr_free(&Wnt);
     ph(PH_SPAT);
     amgd_lmop(fac->S, W_skel, fac->kpos, fac->Wt, fac->Q, fac->qoff, au2);
     ph(PH_LMOP);
@@ -493,12 +499,51 @@ static dcsr *find_support(const dcsr *R, double goal) {
      computed in full once, then re-summed for those rows / columns (amgd_fs_select) */
   amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);            /* rs = R*1 */
   amgd_colsum(Rt, sumR);
+  /* Incremental sweeps: a sweep that removed few entries changes rs only on their
+     rows D; w = R'rs then changes on the columns C1 of D, tmp = R w on the rows D2
+     of C1, w2 = R' tmp on the columns C3 of D2 (zeroed entries stay in the
+     pattern).  Those lists are recomputed with the same ordered row sums; every
+     other entry keeps its value.  Large dirty sets fall back to full products. */
+  const char *e_inc = getenv("AMGD_FS_INC");          /* 0 off, 2 at every size (tests) */
+  const int fs_mode = e_inc && *e_inc ? atoi(e_inc) : 1;
+  const int fs_inc = fs_mode == 2 || (fs_mode == 1 && nf >= 4096);
+  const uint32_t cap_c = nc / 4 + 1, cap_r = nf / 4 + 1;
+  uint32_t *st_r = NULL, *st_c = NULL, *L1 = NULL, *L2 = NULL, *L3 = NULL, tag = 0;
+  if (fs_inc) {
+    st_r = (uint32_t *)amgd_alloc((size_t)nf * 4 + 4);
+    st_c = (uint32_t *)amgd_alloc((size_t)nc * 4 + 4);
+    amgd_memset(st_r, 0, (size_t)nf * 4);
+    amgd_memset(st_c, 0, (size_t)nc * 4);
+    L1 = (uint32_t *)amgd_alloc((size_t)cap_c * 4 + 4);
+    L2 = (uint32_t *)amgd_alloc((size_t)cap_r * 4 + 4);
+    L3 = (uint32_t *)amgd_alloc((size_t)cap_c * 4 + 4);
+  }
+  uint64_t prev_off = 0;
+  uint32_t prev_nsel = 0;
   ph(PH_FS);
   for (;;) {
     it++;
-    amgd_spmvt(Rt, rs, w);                                /* w = R'*rs (row order) */
-    amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
-    amgd_spmvt(Rt, tmp, w2);                              /* w2 = R'*(R*w) */
+    int done = 0;
+    if (fs_inc && it > 1 && prev_nsel <= cap_c) {
+      const uint32_t n1 = amgd_fs_expand(Rl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c);
+      if (n1 <= cap_c) {
+        const uint32_t n2 = amgd_fs_expand(Rt, L1, n1, st_r, ++tag, L2, cap_r);
+        if (n2 <= cap_r) {
+          const uint32_t n3 = amgd_fs_expand(Rl, L2, n2, st_c, ++tag, L3, cap_c);
+          if (n3 <= cap_c) {
+            amgd_spmv_rows(Rt, L1, n1, rs, w);          /* w  on C1 */
+            amgd_spmv_rows(Rl, L2, n2, w, tmp);         /* tmp on D2 */
+            amgd_spmv_rows(Rt, L3, n3, tmp, w2);        /* w2 on C3 */
+            done = 1;
+          }
+        }
+      }
+    }
+    if (!done) {
+      amgd_spmvt(Rt, rs, w);                              /* w = R'*rs (row order) */
+      amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
+      amgd_spmvt(Rt, tmp, w2);                            /* w2 = R'*(R*w) */
+    }
     ph(PH_FS_MV);
     amgd_vdiv_guard(vv, w2, w, nc);
     double mv = amgd_max_first(vv, nc, NULL), mw = mv;   /* max(v) twice, amg_setup.c:1316-1317 */
@@ -509,6 +554,8 @@ static dcsr *find_support(const dcsr *R, double goal) {
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    prev_off = ns;
+    prev_nsel = nsel;
     ns += nsel;
     if (getenv("AMGD_FSLOG"))
       fprintf(stderr, "fs L%d nf %u nc %u nnz %lu it %d sel %u rem %u theta %g\n", g_lvl, nf, nc,
@@ -522,6 +569,9 @@ static dcsr *find_support(const dcsr *R, double goal) {
   if (verbose()) printf("    find_support: %d sweeps, %lu entries (R %u x %u, nnz %lu)\n", it,
                        (unsigned long)ns, nf, nc, (unsigned long)R->nnz);
   amgd_free(ones);
+  if (fs_inc) {
+    amgd_free(st_r); amgd_free(st_c); amgd_free(L1); amgd_free(L2); amgd_free(L3);
+  }
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);

@@ -347,6 +347,36 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   return T;
 }
 
+// A without its exactly-zero entries (shape unchanged)
+__global__ void k_nz_count(const uint64_t *ro, const double *a, uint32_t rn, uint64_t *cnt) {
+  GRID_STRIDE(i, rn) {
+    uint64_t c = 0;
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++) c += a[k] != 0.0 ? 1 : 0;
+    cnt[i] = c;
+  }
+}
+__global__ void k_nz_fill(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
+                          const uint64_t *xro, uint32_t *xcol, double *xa) {
+  GRID_STRIDE(i, rn) {
+    uint64_t o = xro[i];
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k++)
+      if (a[k] != 0.0) { xcol[o] = col[k]; xa[o] = a[k]; o++; }
+  }
+}
+extern "C" dcsr *amgd_drop_zeros(const dcsr *A) {
+  hipStream_t s = amgd_s();
+  uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
+  if (A->rn) k_nz_count<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->a, A->rn, cnt);
+  const uint64_t nz = amgd_scan_u64(cnt, A->rn);
+  dcsr *X = (dcsr *)malloc(sizeof(dcsr));
+  X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
+  X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
+  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  if (A->rn && nz) k_nz_fill<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, X->ro, X->col, X->a);
+  KCHECK();
+  return X;
+}
+
 // rows of A kept where mask != 0, the others emptied (shape unchanged)
 __global__ void k_rowmask_count(const uint64_t *ro, uint32_t rn, const uint8_t *m, uint64_t *cnt) {
   GRID_STRIDE(i, rn) cnt[i] = m[i] ? ro[i + 1] - ro[i] : 0;

@@ -62,6 +62,23 @@ API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, doub
       amgd_free(all); amgd_free(pi); amgd_free(pj); amgd_free(ones);
       break;
     }
+    case 7: {                     /* Q application: Q = qfactor(A, B); X = A's pattern with
+                                     values qapply(A, Q, B, u, lambda), u / lambda generated */
+      uint64_t tot = 0, *qoff = NULL;
+      double *Q = amgd_qfactor(A, B, &qoff, &tot);
+      double *u = (double *)amgd_alloc((size_t)A->rn * 8 + 8);
+      double *lam = (double *)amgd_alloc((size_t)A->cn * 8 + 8);
+      double *hu = (double *)malloc((size_t)A->rn * 8 + 8), *hl = (double *)malloc((size_t)A->cn * 8 + 8);
+      for (uint32_t i = 0; i < A->rn; i++) hu[i] = 0.5 + (double)(i % 3);
+      for (uint32_t j = 0; j < A->cn; j++) hl[j] = 1.0 / (1.0 + (double)(j % 7));
+      amgd_h2d(u, hu, (size_t)A->rn * 8);
+      amgd_h2d(lam, hl, (size_t)A->cn * 8);
+      free(hu); free(hl);
+      X = dcsr_empty_like_pattern(A);
+      amgd_qapply(A, Q, qoff, B, u, lam, X->a);
+      amgd_free(Q); amgd_free(qoff); amgd_free(u); amgd_free(lam);
+      break;
+    }
     default: return -2;
   }
   down(X, HX);
@@ -151,6 +168,8 @@ API void amgd_test_qf_stats(uint64_t *out) {
 }
 
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
+extern void amgd_qapply_set_huge(int n);
+API void amgd_test_qa_huge(int n) { amgd_qapply_set_huge(n); }
 extern void amgd_spmv_set_rw(int rw);
 API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_qfactor_set_coop_lds(int m);

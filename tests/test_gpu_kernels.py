@@ -515,6 +515,21 @@ def test_qfactor_tiers_bitexact(structure, mode, coop_lds):
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
 
 
+@pytest.mark.parametrize("structure", ["tiers", "scattered"])
+def test_qapply_huge_grid_path(structure):
+    """Q application of huge supports by the grid-wide kernels (threshold lowered to 600
+    points) equals the one-work-group path bit for bit (default threshold 8192)"""
+    W, A = _qfactor_case(structure)
+    X1 = oa.test_csr_op(7, W, A)
+    oa.qa_huge(600)
+    try:
+        X2 = oa.test_csr_op(7, W, A)
+    finally:
+        oa.qa_huge(-1)
+    assert int((np.diff(W.row_off) > 600).sum()) > 0
+    assert np.array_equal(X1.a.view(np.uint64), X2.a.view(np.uint64))
+
+
 @pytest.mark.parametrize("case", ["short", "long", "ties", "over_lds"])
 def test_expand_pick(case):
     """expand_support's per-row pick: short rows (rank-count kernel), long rows (LDS

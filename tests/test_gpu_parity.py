@@ -157,3 +157,33 @@ def test_gpu_incremental_coarsen_matches_full_sweeps(m, stencil, min_rows, list_
     h_full = abi.run_setup(oa.lib(), Ai, Aj, Av)
     bad = parity.compare(h_full, h_inc, exact=True)
     assert not bad, bad
+
+
+# incremental find_support sweeps (amgd_setup.c find_support): forced at every size,
+# and off, the hierarchy must stay bit-identical to the reference's / the oracle's
+@pytest.mark.parametrize("mode", ["2", "0"], ids=["fs_inc_always", "fs_inc_off"])
+@pytest.mark.parametrize("case", ["p7_12", "p27_8", "sem_e3_N2", "aniso_12", "amgdmp", "p2d9_24"])
+def test_gpu_fs_incremental_bitexact_fixture(case, mode, monkeypatch):
+    monkeypatch.setenv("AMGD_FS_INC", mode)
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("gen", [("p7_32", "1", lambda: problems.poisson3d(32)),
+                                 ("aniso_16", "2", lambda: problems.poisson3d(16, eps=1e-3)),
+                                 ("p27_16", "2", lambda: problems.poisson3d(16, 27))],
+                         ids=lambda g: g[0])
+def test_gpu_fs_incremental_matches_full(gen, monkeypatch):
+    """incremental sweeps (default: from 4096 F rows; "2": at every size) vs
+    AMGD_FS_INC=0: identical hierarchies (aniso 24^3 is not used: the reference's own
+    loop does not terminate on it -- the oracle runs past 120 s as well)"""
+    Ai, Aj, Av = gen[2]()
+    monkeypatch.setenv("AMGD_FS_INC", gen[1])
+    h_inc = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    monkeypatch.setenv("AMGD_FS_INC", "0")
+    h_full = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    bad = parity.compare(h_full, h_inc, exact=True)
+    assert not bad, bad
