@@ -100,6 +100,7 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
+        L.amgd_test_qf_split.argtypes = [C.c_int]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
@@ -322,11 +323,18 @@ def qa_huge(n: int) -> None:
     lib().amgd_test_qa_huge(int(n))
 
 
+def qf_split(on: int) -> None:
+    """huge supports factored per connected component of A on the support (1, the
+    default) or as one sequential factor (0); -1: back to the default / AMGD_QF_SPLIT"""
+    lib().amgd_test_qf_split(int(on))
+
+
 def qf_stats() -> dict:
-    """huge supports factored sparse / sent to the dense kernel since the last call"""
-    out = (C.c_uint64 * 2)()
+    """huge supports factored sparse / sent to the dense kernel / split into components,
+    since the last call"""
+    out = (C.c_uint64 * 3)()
     lib().amgd_test_qf_stats(out)
-    return {"sparse": int(out[0]), "fallback": int(out[1])}
+    return {"sparse": int(out[0]), "fallback": int(out[1]), "split": int(out[2])}
 
 
 def lmop_stats(reset: bool = True) -> dict:

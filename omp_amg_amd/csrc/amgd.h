@@ -196,7 +196,7 @@ void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, mis
 void amgd_lmop_stats_reset(void);
 void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
 void amgd_qfactor_set_sparse(int m);   /* huge supports: 0 dense, 1 sparse first, 2 tiny capacity */
-void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback] since the last call */
+void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] since the last call */
 /* one find_support sweep: select/remove, then re-sum rs (rows) and sumR (columns) that lost
    an entry */
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,

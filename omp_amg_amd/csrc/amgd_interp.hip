@@ -813,17 +813,184 @@ static int qf_blocked() {
 }
 static uint32_t g_coop_lds_max = QF_COOP_MAX;   // tests: smaller forces the global-memory variant
 extern "C" void amgd_qfactor_set_coop_lds(int m) { g_coop_lds_max = m < 0 ? QF_COOP_MAX : (uint32_t)m; }
-static unsigned long g_qf_stats[2];   // huge supports factored sparse / sent to the dense kernel
+static unsigned long g_qf_stats[3];   // huge supports factored sparse / sent to the dense kernel / split
 extern "C" void amgd_qfactor_set_sparse(int m) { g_qf_sparse = m; }
 extern "C" void amgd_qfactor_stats(unsigned long *st) {
   st[0] = g_qf_stats[0];
   st[1] = g_qf_stats[1];
-  g_qf_stats[0] = g_qf_stats[1] = 0;
+  st[2] = g_qf_stats[2];
+  g_qf_stats[0] = g_qf_stats[1] = g_qf_stats[2] = 0;
 }
 #define QF_T0 32
 #define QF_T1 64
 #define QF_T2 128
 #define QF_T3 1024
+// ---------------------------------------------------------------------------
+// Huge supports split by connected components.  The Gram matrix A(Qj, Qj) of the
+// orphan support (min_skel's column 0) is block-diagonal over the connected
+// components of A restricted to Qj.  In the reference's factor every term that
+// couples two components has an exact zero factor, so each sum it adds to starts
+// at +0 and ends with the same bits over its own component only, and every
+// cross-component entry of U is qk * al = +0 * (negative) = -0.  The support is
+// therefore factored as independent sub-supports (one per component, members in
+// ascending order, through the usual tiers) and scattered into the -0-filled
+// triangle: bit-identical to factoring the whole support, in parallel instead of
+// one sequential k-loop over tens of thousands of points.
+// ---------------------------------------------------------------------------
+__global__ void k_cc_init(const uint32_t *Qj, uint32_t nz, uint32_t *pos, uint32_t *lab) {
+  GRID_STRIDE(k, nz) {
+    pos[Qj[k]] = (uint32_t)k;
+    lab[k] = (uint32_t)k;
+  }
+}
+__global__ void k_cc_reset(const uint32_t *Qj, uint32_t nz, uint32_t *pos) {
+  GRID_STRIDE(k, nz) pos[Qj[k]] = 0xffffffffu;
+}
+// min-label hooking over the edges of A inside the support, then pointer jumping
+__global__ void k_cc_hook(const uint32_t *Qj, uint32_t nz, const uint64_t *aro,
+                          const uint32_t *acol, const uint32_t *pos, uint32_t *lab,
+                          unsigned *changed) {
+  GRID_STRIDE(k, nz) {
+    const uint32_t r = Qj[k];
+    uint32_t m = lab[k];
+    for (uint64_t e = aro[r]; e < aro[r + 1]; e++) {
+      const uint32_t p = pos[acol[e]];
+      if (p != 0xffffffffu) m = min(m, lab[p]);
+    }
+    bool ch = false;
+    for (uint64_t e = aro[r]; e < aro[r + 1]; e++) {   // both ends of each edge (any pattern)
+      const uint32_t p = pos[acol[e]];
+      if (p == 0xffffffffu) continue;
+      const uint32_t lp = lab[p];
+      if (m < lp) { atomicMin(&lab[lp], m); atomicMin(&lab[p], m); ch = true; }
+    }
+    const uint32_t lk = lab[k];
+    if (m < lk) { atomicMin(&lab[lk], m); atomicMin(&lab[k], m); ch = true; }
+    if (ch) *changed = 1u;
+  }
+}
+__global__ void k_cc_jump(uint32_t nz, uint32_t *lab) {
+  GRID_STRIDE(k, nz) {
+    uint32_t l = lab[k];
+    while (lab[l] != l) l = lab[l];
+    lab[k] = l;
+  }
+}
+__global__ void k_cc_keys(uint32_t nz, const uint32_t *lab, uint64_t *key) {
+  GRID_STRIDE(k, nz) key[k] = ((uint64_t)lab[k] << 32) | k;
+}
+// component heads in the (label, k) order -> per-member component start flags
+__global__ void k_cc_heads(uint32_t nz, const uint64_t *skey, uint64_t *head) {
+  GRID_STRIDE(t, nz) head[t] = (t == 0 || (skey[t] >> 32) != (skey[t - 1] >> 32)) ? 1 : 0;
+}
+__global__ void k_cc_sub(uint32_t nz, const uint64_t *skey, const uint64_t *hscan,
+                         const uint32_t *Qj, uint64_t *sro, uint32_t *scol, uint32_t *member) {
+  GRID_STRIDE(t, nz) {
+    const uint32_t k = (uint32_t)(skey[t] & 0xffffffffu);
+    scol[t] = Qj[k];
+    member[t] = k;
+    if (t == 0 || (skey[t] >> 32) != (skey[t - 1] >> 32)) sro[hscan[t]] = t;
+  }
+}
+// U[tri(gi) + gj] = Qs[qoff_s[comp] + tri(li) + lj], one thread per member row
+__global__ void k_cc_scatter(uint32_t nz, const uint64_t *sro, uint32_t ncomp,
+                             const uint32_t *member, const uint64_t *qoff_s, const double *Qs,
+                             double *U) {
+  GRID_STRIDE(t, nz) {
+    uint32_t lo = 0, hi = ncomp;                 // component of member t
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sro[mid] <= t) lo = mid; else hi = mid;
+    }
+    const uint64_t m0 = sro[lo];
+    const uint64_t li = t - m0, gi = member[t];
+    const double *src = Qs + qoff_s[lo] + tri(li);
+    double *dst = U + tri(gi);
+    for (uint64_t lj = 0; lj <= li; lj++) dst[member[m0 + lj]] = src[lj];
+  }
+}
+static int g_qf_split = -1;     // AMGD_QF_SPLIT=0: no component split of huge supports
+static int g_qf_split_depth = 0;
+extern "C" void amgd_qfactor_set_split(int on) { g_qf_split = on < 0 ? -1 : on; }
+static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, double *Q,
+                          uint32_t cb, uint32_t ce, uint64_t tot);
+// Factor support c by components if it has more than one; returns false (nothing
+// done) when it is one component.
+static bool qfactor_split(uint32_t c, const dcsr *Wt, const dcsr *A, uint64_t w0, uint32_t nz,
+                          double *U) {
+  if (g_qf_split < 0) { const char *e = getenv("AMGD_QF_SPLIT"); g_qf_split = e ? atoi(e) : 1; }
+  if (!g_qf_split || g_qf_split_depth > 0) return false;
+  hipStream_t s = amgd_s();
+  const uint32_t *Qj = Wt->col + w0;
+  uint32_t *pos = (uint32_t *)amgd_alloc((size_t)A->cn * 4 + 4);
+  HIPCK(hipMemsetAsync(pos, 0xff, (size_t)A->cn * 4, s));
+  uint32_t *lab = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+  unsigned *chg = (unsigned *)amgd_alloc(16);
+  k_cc_init<<<grid_for(nz), 256, 0, s>>>(Qj, nz, pos, lab);
+  for (int round = 0; round < 1000000; round++) {
+    HIPCK(hipMemsetAsync(chg, 0, 4, s));
+    k_cc_hook<<<grid_for(nz), 256, 0, s>>>(Qj, nz, A->ro, A->col, pos, lab, chg);
+    k_cc_jump<<<grid_for(nz), 256, 0, s>>>(nz, lab);
+    unsigned h = 0;
+    amgd_d2h(&h, chg, 4);
+    if (!h) break;
+  }
+  amgd_free(pos);
+  amgd_free(chg);
+  uint64_t *key = (uint64_t *)amgd_alloc((size_t)nz * 8 + 8), *skey = (uint64_t *)amgd_alloc((size_t)nz * 8 + 8);
+  k_cc_keys<<<grid_for(nz), 256, 0, s>>>(nz, lab, key);
+  size_t tb = 0;
+  HIPCK(rocprim::radix_sort_keys(nullptr, tb, key, skey, (size_t)nz, 0, 64, s));
+  void *tmp = amgd_alloc(tb + 16);
+  HIPCK(rocprim::radix_sort_keys(tmp, tb, key, skey, (size_t)nz, 0, 64, s));
+  amgd_free(tmp); amgd_free(key); amgd_free(lab);
+  uint64_t *hs = (uint64_t *)amgd_alloc((size_t)nz * 8 + 16);
+  k_cc_heads<<<grid_for(nz), 256, 0, s>>>(nz, skey, hs);
+  const uint32_t ncomp = (uint32_t)amgd_scan_u64(hs, nz);
+  bool done = false;
+  if (ncomp > 1) {
+    dcsr sub;
+    sub.rn = ncomp;
+    sub.cn = Wt->cn;
+    sub.nnz = nz;
+    sub.ro = (uint64_t *)amgd_alloc(((size_t)ncomp + 1) * 8);
+    sub.col = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+    sub.a = nullptr;
+    uint32_t *member = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+    k_cc_sub<<<grid_for(nz), 256, 0, s>>>(nz, skey, hs, Qj, sub.ro, sub.col, member);
+    const uint64_t endv = nz;
+    amgd_h2d(sub.ro + ncomp, &endv, 8);
+    uint64_t *qoff_s = (uint64_t *)amgd_alloc(((size_t)ncomp + 1) * 8);
+    k_qsize<<<grid_for(ncomp), 256, 0, s>>>(sub.ro, ncomp, qoff_s);
+    const uint64_t tot_s = amgd_scan_u64(qoff_s, ncomp);
+    double *Qs = (double *)amgd_alloc(tot_s * 8 + 8);
+    g_qf_split_depth++;
+    qfactor_range(&sub, A, qoff_s, Qs, 0, ncomp, tot_s);
+    g_qf_split_depth--;
+    const uint64_t tn = (uint64_t)nz * (nz + 1) / 2;
+    k_fill_negzero<<<grid_for(tn, 256, 65536), 256, 0, s>>>(U, tn);
+    k_cc_scatter<<<grid_for(nz), 256, 0, s>>>(nz, sub.ro, ncomp, member, qoff_s, Qs, U);
+    KCHECK();
+    amgd_free(Qs); amgd_free(qoff_s); amgd_free(member); amgd_free(sub.col);
+    g_qf_stats[2]++;
+    if (getenv("AMGD_SGLOG")) {
+      std::vector<uint64_t> hro(ncomp + 1);
+      amgd_d2h(hro.data(), sub.ro, (ncomp + 1) * 8);
+      uint64_t mx = 0, big = 0;
+      for (uint32_t q = 0; q < ncomp; q++) {
+        mx = std::max(mx, hro[q + 1] - hro[q]);
+        big += hro[q + 1] - hro[q] > 1024;
+      }
+      fprintf(stderr, "qfactor split: support %u of %u points -> %u components (largest %lu, %lu past 1024)\n",
+              c, nz, ncomp, (unsigned long)mx, (unsigned long)big);
+    }
+    amgd_free(sub.ro);
+    done = true;
+  }
+  amgd_free(hs); amgd_free(skey);
+  return done;
+}
+
 // the factors of the coarse points cb <= c < ce (all tiers), into Q at qoff
 static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, double *Q,
                           uint32_t cb, uint32_t ce, uint64_t tot) {
@@ -893,6 +1060,13 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
     amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
     amgd_d2h(qo.data(), qoff, (size_t)(rn + 1) * 8);
     const int sp = qf_sparse_mode();
+    std::vector<uint32_t> bigs;
+    for (uint32_t c : big) {
+      const uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
+      if (!qfactor_split(c, Wt, A, ro[c], nz, Q + qo[c])) bigs.push_back(c);
+    }
+    big.swap(bigs);
+    if (!big.empty()) amgd_sync();          // the side stream must see the split's writes ordered
     for (uint32_t c : big) {
       uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
       bignz.push_back(nz);

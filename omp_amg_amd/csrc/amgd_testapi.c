@@ -161,10 +161,11 @@ API void amgd_test_lmop_stats(uint64_t *out, int reset) {
    capacity, which forces the dense fallback) and [sparse, fallback] counters */
 API void amgd_test_qf_sparse(int m) { amgd_qfactor_set_sparse(m); }
 API void amgd_test_qf_stats(uint64_t *out) {
-  unsigned long st[2];
+  unsigned long st[3];
   amgd_qfactor_stats(st);
   out[0] = st[0];
   out[1] = st[1];
+  out[2] = st[2];
 }
 
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
@@ -174,6 +175,9 @@ extern void amgd_spmv_set_rw(int rw);
 API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_qfactor_set_coop_lds(int m);
 API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }
+/* huge supports factored per connected component (1, default) or whole (0); -1: env */
+extern void amgd_qfactor_set_split(int on);
+API void amgd_test_qf_split(int on) { amgd_qfactor_set_split(on); }
 extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
 /* window of the dense-accumulator numeric kernel for wide rows: 0 (hash kernels), 8192, 16384 */

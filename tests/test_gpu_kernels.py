@@ -468,6 +468,16 @@ def _qfactor_case(structure):
             c = np.sort(rng.choice(np.arange(lo, lo + 3 * nz), size=nz, replace=False))
             cols.extend(c.tolist())
             ro.append(len(cols))
+    elif structure == "blocks":                # huge supports made of disjoint components
+        blk = lambda a, n: np.arange(a, a + n)
+        for parts in ([blk(400, 500), blk(4000, 600)],                  # two tier-sized ones
+                      [blk(800, 1300), blk(4400, 1200), np.arange(7000, 7600, 9)],
+                      [blk(0, 300), np.arange(1000, 3000, 2), blk(5000, 200)]):
+            c = np.unique(np.concatenate(parts))
+            cols.extend(c.tolist()); ro.append(len(cols))
+        for nz in (20, 700):                   # ordinary tiers beside them
+            c = np.sort(rng.choice(np.arange(m ** 3), size=nz, replace=False))
+            cols.extend(c.tolist()); ro.append(len(cols))
     else:                                      # huge supports only
         if structure == "scattered":           # isolated points: a diagonal Gram matrix
             c = np.sort(rng.choice(np.arange(0, m ** 3, 7), size=1100, replace=False))
@@ -492,24 +502,55 @@ def test_qfactor_tiers_bitexact(structure, mode, coop_lds):
     sparse kernel (mode 1), the dense cooperative kernel (mode 0), or the sparse
     kernel with a capacity too small to finish, which must hand over to the dense one.
     coop_lds: supports above it run the dense kernel's global-memory variant (the one
-    supports past 8192 points take)"""
+    supports past 8192 points take).  Component splitting is off here (see
+    test_qfactor_split_bitexact)"""
     W, A = _qfactor_case(structure)
     oa.qf_sparse(mode)
     oa.qf_coop_lds(coop_lds)
+    oa.qf_split(0)
     oa.qf_stats()
     try:
         X = oa.test_csr_op(5, W, A)
     finally:
         oa.qf_sparse(1)
         oa.qf_coop_lds(-1)
+        oa.qf_split(-1)
     st = oa.qf_stats()
     nhuge = int((np.diff(W.row_off) > 1024).sum())
     if mode == 0:
-        assert st == {"sparse": 0, "fallback": 0}
+        assert st == {"sparse": 0, "fallback": 0, "split": 0}
     elif mode == 2:
-        assert st == {"sparse": 0, "fallback": nhuge}
+        assert st == {"sparse": 0, "fallback": nhuge, "split": 0}
     else:
         assert st["sparse"] + st["fallback"] == nhuge and st["sparse"] > 0, st
+    ref = _oracle_qfactor(W, A)
+    assert X.nnz == len(ref)
+    assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
+
+
+@pytest.mark.parametrize("structure,mode", [("blocks", 1), ("blocks", 0), ("scattered", 1),
+                                            ("tiers", 1)])
+def test_qfactor_split_bitexact(structure, mode):
+    """huge supports whose Gram matrix is block-diagonal (several connected components
+    of A on the support) are factored per component -- through the ordinary tiers, or
+    the huge kernels for components past 1024 points -- and scattered into a -0-filled
+    triangle: bit for bit the oracle's one sequential factor, cross-component -0 included.
+    'blocks' holds two-, three- and many-component supports; 'scattered' a diagonal one
+    (1100 components) and a random one; a single-component support stays whole"""
+    W, A = _qfactor_case(structure)
+    oa.qf_sparse(mode)
+    oa.qf_split(1)
+    oa.qf_stats()
+    try:
+        X = oa.test_csr_op(5, W, A)
+    finally:
+        oa.qf_sparse(1)
+        oa.qf_split(-1)
+    st = oa.qf_stats()
+    if structure == "blocks":                # 2 + 3 + 3 components; 1300 / 1200 stay huge
+        assert st["split"] == 3 and st["sparse"] + st["fallback"] == (2 if mode else 0), st
+    elif structure == "scattered":
+        assert st["split"] >= 1, st
     ref = _oracle_qfactor(W, A)
     assert X.nnz == len(ref)
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
