@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+        L.amgd_test_lmop_prune.argtypes = [C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
@@ -339,9 +340,17 @@ def qf_stats() -> dict:
 
 def lmop_stats(reset: bool = True) -> dict:
     """interp_lmop path counters since the last reset"""
-    out = (C.c_uint64 * 4)()
+    out = (C.c_uint64 * 5)()
     lib().amgd_test_lmop_stats(out, int(reset))
-    return {"fast": out[0], "general": out[1], "dirty_prefix": out[2], "misses": out[3]}
+    return {"fast": out[0], "general": out[1], "dirty_prefix": out[2], "misses": out[3],
+            "pruned": out[4]}
+
+
+def lmop_prune(n: int) -> None:
+    """general walk: supports of at least n points whose factor graph splits into
+    components emit same-component contributions only (0: never; -1: default 4096 /
+    AMGD_LMOP_PRUNE)"""
+    lib().amgd_test_lmop_prune(int(n))
 
 
 def spgemm_win(w: int) -> None:

@@ -192,7 +192,7 @@ void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dc
 void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt, const double *Q,
                const uint64_t *qoff, const double *u);
 uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm);
-void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses */
+void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses, pruned supports */
 void amgd_lmop_stats_reset(void);
 void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
 void amgd_qfactor_set_sparse(int m);   /* huge supports: 0 dense, 1 sparse first, 2 tiny capacity */

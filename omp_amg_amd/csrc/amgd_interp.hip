@@ -869,6 +869,7 @@ __global__ void k_cc_hook(const uint32_t *Qj, uint32_t nz, const uint64_t *aro,
     if (ch) *changed = 1u;
   }
 }
+__global__ void k_cc_init_iota(uint32_t nz, uint32_t *lab) { GRID_STRIDE(k, nz) lab[k] = (uint32_t)k; }
 __global__ void k_cc_jump(uint32_t nz, uint32_t *lab) {
   GRID_STRIDE(k, nz) {
     uint32_t l = lab[k];
@@ -1533,6 +1534,215 @@ __global__ void k_csq(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
 }
 extern void amgd_row_of_entry_launch(const uint64_t *ro, uint32_t rn, uint32_t *row);
 
+// ---------------------------------------------------------------------------
+// Huge supports, pruned.  Let G be the graph on the support with an edge k - t
+// wherever the factor entry q_t[k] (k < t) is nonzero.  If k and m lie in different
+// components of G, every product q_t[k] * q_t[m] has a zero factor, so the QQt entry
+// sums only signed zeros from +0 and is +0, and u_c * (+0) is a signed zero: adding
+// it to S (whose entries start at +0 and so never hold -0) changes no bit.  Such
+// contributions are dropped; the walk still steps over them (each landing depends on
+// the previous one), but only same-component keys are written, and each value sums
+// over the component's members only (the other t contribute signed zeros too).  The
+// kept contributions keep their (k, m) order, so the stable sort and the ordered
+// accumulation are those of the full path.  For the orphan support of an anisotropic
+// level 1 (10^4 - 3.4*10^4 points in ~100 components) this replaces nz^2 keys and
+// nz^3 value work by sum(size^2) and sum(size^3).
+// ---------------------------------------------------------------------------
+__global__ void k_qnz_count(const double *U, uint32_t nz, uint64_t *cnt) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nz;
+       t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const double *row = U + tri(t);
+    uint32_t c = 0;
+    for (uint64_t k = lane; k < t; k += 64) c += row[k] != 0.0;
+    for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) cnt[t] = c;
+  }
+}
+__global__ void k_qnz_fill(const double *U, uint32_t nz, const uint64_t *eoff, uint32_t *ea,
+                           uint32_t *eb) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nz;
+       t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const double *row = U + tri(t);
+    uint64_t o = eoff[t];
+    for (uint64_t k0 = 0; k0 < t; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      const bool p = k < t && row[k] != 0.0;
+      const unsigned long long b = __ballot(p);
+      if (p) {
+        const uint64_t w = o + __popcll(b & ((1ull << lane) - 1));
+        ea[w] = (uint32_t)t;
+        eb[w] = (uint32_t)k;
+      }
+      o += __popcll(b);
+    }
+  }
+}
+__global__ void k_edge_hook(const uint32_t *ea, const uint32_t *eb, uint64_t ne, uint32_t *lab,
+                            unsigned *changed) {
+  GRID_STRIDE(e, ne) {
+    const uint32_t a = lab[ea[e]], b = lab[eb[e]];
+    if (a != b) {
+      atomicMin(&lab[a > b ? a : b], a > b ? b : a);
+      *changed = 1u;
+    }
+  }
+}
+// per member (sorted by (label, index)): component index and component offsets;
+// hscan = exclusive scan of the head flags, so a head's component is hscan[t]
+__global__ void k_comp_meta_x(uint32_t nz, const uint64_t *skey, const uint64_t *hscan,
+                              uint32_t *compid, uint32_t *members, uint64_t *cro) {
+  GRID_STRIDE(t, nz) {
+    const uint32_t k = (uint32_t)(skey[t] & 0xffffffffu);
+    const bool head = t == 0 || (skey[t] >> 32) != (skey[t - 1] >> 32);
+    const uint32_t cid = (uint32_t)hscan[t] - (head ? 0u : 1u);
+    members[t] = k;
+    compid[k] = cid;
+    if (head) cro[cid] = t;
+  }
+}
+__global__ void k_comp_rank(uint32_t nz, const uint32_t *members, const uint32_t *compid,
+                            const uint64_t *cro, uint32_t *rank, uint64_t *kcnt) {
+  GRID_STRIDE(t, nz) {
+    const uint32_t k = members[t];
+    const uint32_t cid = compid[k];
+    rank[k] = (uint32_t)(t - cro[cid]);
+    kcnt[k] = cro[cid + 1] - cro[cid];
+  }
+}
+// sp_add's walk for row k of the support (k_lmop_land), keys written for same-component m
+__global__ void k_lmop_land_pr(const uint32_t *Qj, uint32_t nz, const uint64_t *sro,
+                               const uint32_t *scol, uint32_t srn, uint64_t snnz,
+                               const int64_t *rmax, const int64_t *b64, const int64_t *b4k,
+                               const uint32_t *compid, const uint32_t *rank, const uint64_t *koff,
+                               uint64_t *key) {
+  GRID_STRIDE(k, nz) {
+    const uint32_t ck = compid[k];
+    const uint64_t o = koff[k];
+    uint32_t r = Qj[k];
+    uint64_t t = sro[r];
+    bool live = sro[r + 1] != t;
+    for (uint32_t m = 0; m < nz; m++) {
+      uint64_t land = snnz;
+      if (live) {
+        const uint32_t xm = Qj[m];
+        const uint64_t end = sro[r + 1];
+        if (t < end && rmax[r] >= (int64_t)xm) {
+          land = lower_bound_u32(scol, t, end, xm);
+        } else {
+          const uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xm);
+          if (r2 >= srn) live = false;
+          else { r = r2; land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xm); }
+        }
+        if (live) t = land + 1;
+      }
+      if (compid[m] == ck) key[o + rank[m]] = land;
+    }
+  }
+}
+__global__ void k_lmop_val_pr(uint64_t n, uint32_t nz, const uint64_t *koff, const uint32_t *compid,
+                              const uint32_t *rank, const uint32_t *members, const uint64_t *cro,
+                              const double *Qc, double uc, const uint64_t *key, uint64_t snnz,
+                              double *val) {
+  GRID_STRIDE(o, n) {
+    if (key[o] >= snnz) { val[o] = 0.0; continue; }
+    uint32_t lo = 0, hi = nz;                  // last k with koff[k] <= o
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (koff[mid] <= o) lo = mid; else hi = mid;
+    }
+    const uint32_t k = lo, j = (uint32_t)(o - koff[k]);
+    const uint64_t c0 = cro[compid[k]], c1 = cro[compid[k] + 1];
+    const uint32_t m = members[c0 + j];
+    const uint32_t rk = rank[k];
+    double q = 0.0;
+    for (uint64_t p = c0 + (rk > j ? rk : j); p < c1; p++) {
+      const double *qt = Qc + tri(members[p]);
+      q += qt[k] * qt[m];
+    }
+    val[o] = uc * q;
+  }
+}
+static int g_lmop_prune = -1;   // supports of at least this many points are pruned (0: never)
+extern "C" void amgd_lmop_set_prune(int n) { g_lmop_prune = n; }
+static uint32_t lmop_prune_min() {
+  if (g_lmop_prune < 0) {
+    const char *e = getenv("AMGD_LMOP_PRUNE");
+    g_lmop_prune = e ? atoi(e) : 4096;
+  }
+  return (uint32_t)g_lmop_prune;
+}
+extern "C" void amgd_lmop_note_pruned(void);
+// contributions of the single support c, pruned; false (nothing done) if its factor
+// graph is connected
+static bool lmop_pruned(dcsr *S, const dcsr *Wt, const double *Q, uint64_t qo, uint64_t w0,
+                        uint32_t nz, double uc, const int64_t *rmax, const int64_t *b64,
+                        const int64_t *b4k, int eb) {
+  hipStream_t s = amgd_s();
+  const double *U = Q + qo;
+  uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)nz + 1) * 8);
+  k_qnz_count<<<grid_for((uint64_t)nz * 64, 256, 16384), 256, 0, s>>>(U, nz, cnt);
+  const uint64_t ne = amgd_scan_u64(cnt, nz);
+  uint32_t *ea = (uint32_t *)amgd_alloc(ne * 4 + 4), *eb_ = (uint32_t *)amgd_alloc(ne * 4 + 4);
+  k_qnz_fill<<<grid_for((uint64_t)nz * 64, 256, 16384), 256, 0, s>>>(U, nz, cnt, ea, eb_);
+  amgd_free(cnt);
+  uint32_t *lab = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+  unsigned *chg = (unsigned *)amgd_alloc(16);
+  k_cc_init_iota<<<grid_for(nz), 256, 0, s>>>(nz, lab);
+  for (int it = 0; it < 100000 && ne; it++) {
+    HIPCK(hipMemsetAsync(chg, 0, 4, s));
+    k_edge_hook<<<grid_for(ne), 256, 0, s>>>(ea, eb_, ne, lab, chg);
+    k_cc_jump<<<grid_for(nz), 256, 0, s>>>(nz, lab);
+    unsigned h = 0;
+    amgd_d2h(&h, chg, 4);
+    if (!h) break;
+  }
+  amgd_free(chg); amgd_free(ea); amgd_free(eb_);
+  uint64_t *key = (uint64_t *)amgd_alloc((size_t)nz * 8 + 8), *skey = (uint64_t *)amgd_alloc((size_t)nz * 8 + 8);
+  k_cc_keys<<<grid_for(nz), 256, 0, s>>>(nz, lab, key);
+  size_t tb = 0;
+  HIPCK(rocprim::radix_sort_keys(nullptr, tb, key, skey, (size_t)nz, 0, 64, s));
+  void *tmp = amgd_alloc(tb + 16);
+  HIPCK(rocprim::radix_sort_keys(tmp, tb, key, skey, (size_t)nz, 0, 64, s));
+  amgd_free(tmp); amgd_free(key); amgd_free(lab);
+  uint64_t *hs = (uint64_t *)amgd_alloc((size_t)nz * 8 + 16);
+  k_cc_heads<<<grid_for(nz), 256, 0, s>>>(nz, skey, hs);
+  const uint32_t ncomp = (uint32_t)amgd_scan_u64(hs, nz);
+  if (ncomp <= 1) { amgd_free(hs); amgd_free(skey); return false; }
+  uint32_t *compid = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4), *rank = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+  uint32_t *members = (uint32_t *)amgd_alloc((size_t)nz * 4 + 4);
+  uint64_t *cro = (uint64_t *)amgd_alloc(((size_t)ncomp + 1) * 8);
+  k_comp_meta_x<<<grid_for(nz), 256, 0, s>>>(nz, skey, hs, compid, members, cro);
+  const uint64_t endv = nz;
+  amgd_h2d(cro + ncomp, &endv, 8);
+  uint64_t *koff = (uint64_t *)amgd_alloc(((size_t)nz + 1) * 8);
+  k_comp_rank<<<grid_for(nz), 256, 0, s>>>(nz, members, compid, cro, rank, koff);
+  const uint64_t n = amgd_scan_u64(koff, nz);
+  amgd_free(hs); amgd_free(skey);
+  uint64_t *k1 = (uint64_t *)amgd_alloc(n * 8 + 8), *k2 = (uint64_t *)amgd_alloc(n * 8 + 8);
+  double *v1 = (double *)amgd_alloc(n * 8 + 8), *v2 = (double *)amgd_alloc(n * 8 + 8);
+  k_lmop_land_pr<<<grid_for(nz, 64, 65536), 64, 0, s>>>(Wt->col + w0, nz, S->ro, S->col, S->rn,
+                                                       S->nnz, rmax, b64, b4k, compid, rank,
+                                                       koff, k1);
+  k_lmop_val_pr<<<grid_for(n, 256, 65536), 256, 0, s>>>(n, nz, koff, compid, rank, members, cro, U,
+                                                       uc, k1, S->nnz, v1);
+  KCHECK();
+  tb = 0;
+  HIPCK(rocprim::radix_sort_pairs(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
+  tmp = amgd_alloc(tb + 16);
+  HIPCK(rocprim::radix_sort_pairs(tmp, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
+  k_seg_accum<<<grid_for(n), 256, 0, s>>>(k2, v2, n, S->nnz, S->a);
+  KCHECK();
+  amgd_free(tmp); amgd_free(k1); amgd_free(k2); amgd_free(v1); amgd_free(v2);
+  amgd_free(compid); amgd_free(rank); amgd_free(members); amgd_free(cro); amgd_free(koff);
+  amgd_lmop_note_pruned();
+  if (getenv("AMGD_SGLOG"))
+    fprintf(stderr, "lmop pruned: support of %u points, %u components, %lu of %lu contributions\n",
+            nz, ncomp, (unsigned long)n, (unsigned long)nz * nz);
+  return true;
+}
+
 // General path: adds the contributions of coarse points c in [cb, ce) to S->a
 // (which the caller has zeroed or already holds the contributions of c < cb).
 extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff,
@@ -1566,11 +1776,29 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
   while (eb < 64 && (S->nnz >> eb) != 0) eb++;   // keys are 0..S->nnz
   HIPCK(rocprim::radix_sort_pairs(nullptr, tb, key, key2, val, val2, (size_t)CH, 0, eb, s));
   void *tmp = amgd_alloc(tb + 16);
+  const uint32_t pmin = lmop_prune_min();
+  std::vector<uint64_t> hqo;
+  std::vector<double> hu;
+  auto huge = [&](uint32_t c) { return pmin && hro[c + 1] - hro[c] >= pmin; };
   uint32_t c0 = cb;
   while (c0 < ce) {
+    if (huge(c0)) {                        // a support of >= pmin points: pruned if it splits
+      if (hqo.empty()) {
+        hqo.resize(rn + 1);
+        amgd_d2h(hqo.data(), qoff, (rn + 1) * 8);
+        hu.resize(rn);
+        amgd_d2h(hu.data(), u, (size_t)rn * 8);
+      }
+      if (lmop_pruned(S, Wt, Q, hqo[c0], hro[c0], (uint32_t)(hro[c0 + 1] - hro[c0]), hu[c0], rmax,
+                      b64, b4k, eb)) {
+        c0++;
+        continue;
+      }
+    }
     uint32_t c1 = c0;
-    // take whole coarse rows while they fit (a single oversized row gets its own chunk)
-    while (c1 < ce && (hcoff[c1 + 1] - hcoff[c0] <= CH || c1 == c0)) c1++;
+    // take whole coarse rows while they fit (a single oversized row gets its own chunk;
+    // a support to prune starts a chunk of its own)
+    while (c1 < ce && (hcoff[c1 + 1] - hcoff[c0] <= CH || c1 == c0) && (c1 == c0 || !huge(c1))) c1++;
     uint64_t n = hcoff[c1] - hcoff[c0];
     if (n > CH) {   // one huge support: grow buffers for it
       amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2); amgd_free(tmp);

@@ -358,9 +358,10 @@ static int lmop_mode() {
 }
 extern "C" void amgd_lmop_set_mode(int m) { g_lmop_mode = m; }
 
-static uint64_t g_lmop_stats[4];   // fast calls, general calls, dirty-prefix calls, misses
-extern "C" void amgd_lmop_stats(uint64_t *out) { for (int i = 0; i < 4; i++) out[i] = g_lmop_stats[i]; }
-extern "C" void amgd_lmop_stats_reset(void) { for (int i = 0; i < 4; i++) g_lmop_stats[i] = 0; }
+static uint64_t g_lmop_stats[5];   // fast calls, general calls, dirty-prefix calls, misses, pruned supports
+extern "C" void amgd_lmop_stats(uint64_t *out) { for (int i = 0; i < 5; i++) out[i] = g_lmop_stats[i]; }
+extern "C" void amgd_lmop_stats_reset(void) { for (int i = 0; i < 5; i++) g_lmop_stats[i] = 0; }
+extern "C" void amgd_lmop_note_pruned(void) { g_lmop_stats[4]++; }
 
 extern "C" void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt,
                           const double *Q, const uint64_t *qoff, const double *u) {

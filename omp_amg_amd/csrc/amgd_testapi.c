@@ -152,6 +152,9 @@ API void amgd_test_free(hcsr *H) {
 
 /* interp_lmop path control and counters: [fast, general, dirty-prefix, misses] */
 API void amgd_test_lmop_mode(int m) { amgd_lmop_set_mode(m); }
+/* supports of at least n points take the pruned general walk (0: never, -1: env/default) */
+extern void amgd_lmop_set_prune(int n);
+API void amgd_test_lmop_prune(int n) { amgd_lmop_set_prune(n); }
 API void amgd_test_lmop_stats(uint64_t *out, int reset) {
   amgd_lmop_stats(out);
   if (reset) amgd_lmop_stats_reset();

@@ -172,6 +172,25 @@ def test_gpu_fs_incremental_bitexact_fixture(case, mode, monkeypatch):
     assert not bad, bad
 
 
+# lmop: every support takes the general walk, supports of >= 8 points pruned to the
+# components of their factor graph -- against the reference's fixtures
+@pytest.mark.parametrize("case", ["p7_12", "aniso_12", "sem_e3_N2"])
+def test_gpu_lmop_pruned_bitexact_fixture(case):
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    oa.lmop_mode(1)
+    oa.lmop_prune(8)
+    oa.lmop_stats(reset=True)
+    try:
+        h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    finally:
+        oa.lmop_mode(0)
+        oa.lmop_prune(-1)
+    assert oa.lmop_stats(reset=True)["pruned"] > 0
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("gen", [("p7_32", "1", lambda: problems.poisson3d(32)),
                                  ("aniso_16", "2", lambda: problems.poisson3d(16, eps=1e-3)),
                                  ("p27_16", "2", lambda: problems.poisson3d(16, 27))],
