@@ -102,6 +102,8 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_stats.argtypes = [C.POINTER(C.c_uint64)]
         L.amgd_test_qf_coop_lds.argtypes = [C.c_int]
         L.amgd_test_qf_split.argtypes = [C.c_int]
+        L.amgd_test_mv_long.argtypes = [C.c_int64]
+        L.amgd_test_fs_long.argtypes = [C.c_int64]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
@@ -328,6 +330,18 @@ def qf_split(on: int) -> None:
     """huge supports factored per connected component of A on the support (1, the
     default) or as one sequential factor (0); -1: back to the default / AMGD_QF_SPLIT"""
     lib().amgd_test_qf_split(int(on))
+
+
+def mv_long(n: int) -> None:
+    """listed-row products: rows past n entries take the block-per-row exact kernel
+    (0: never; -1: default 4096 / AMGD_MV_LONG)"""
+    lib().amgd_test_mv_long(int(n))
+
+
+def fs_long(n: int) -> None:
+    """find_support: rows / columns of R past n entries take the grid-wide expand and the
+    block-per-column select (0: never; -1: default 4096 / AMGD_FS_LONG)"""
+    lib().amgd_test_fs_long(int(n))
 
 
 def qf_stats() -> dict:

@@ -796,10 +796,12 @@ static RowSplit split_rows(const dcsr *Wt, uint32_t cap, uint32_t cb, uint32_t c
 static void free_split(RowSplit &rs) { amgd_free(rs.sl); }
 
 static int g_qf_sparse = -1;   // 0: dense cooperative only, 1: sparse first, 2: tiny capacity
+static bool g_qf_sparse_forced = false;   // set by the environment or a test
 static int qf_sparse_mode() {
   if (g_qf_sparse < 0) {
     const char *e = getenv("AMGD_QF_SPARSE");
     g_qf_sparse = e ? atoi(e) : 1;
+    g_qf_sparse_forced = e != nullptr;
   }
   return g_qf_sparse;
 }
@@ -814,7 +816,10 @@ static int qf_blocked() {
 static uint32_t g_coop_lds_max = QF_COOP_MAX;   // tests: smaller forces the global-memory variant
 extern "C" void amgd_qfactor_set_coop_lds(int m) { g_coop_lds_max = m < 0 ? QF_COOP_MAX : (uint32_t)m; }
 static unsigned long g_qf_stats[3];   // huge supports factored sparse / sent to the dense kernel / split
-extern "C" void amgd_qfactor_set_sparse(int m) { g_qf_sparse = m; }
+extern "C" void amgd_qfactor_set_sparse(int m) {
+  g_qf_sparse = m;
+  g_qf_sparse_forced = m >= 0 && m != 1;   // 1 (the default) restores the automatic choice
+}
 extern "C" void amgd_qfactor_stats(unsigned long *st) {
   st[0] = g_qf_stats[0];
   st[1] = g_qf_stats[1];
@@ -1060,7 +1065,13 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
     std::vector<uint64_t> ro(rn + 1), qo(rn + 1);
     amgd_d2h(ro.data(), Wt->ro, (size_t)(rn + 1) * 8);
     amgd_d2h(qo.data(), qoff, (size_t)(rn + 1) * 8);
-    const int sp = qf_sparse_mode();
+    // components of a split support (connected clusters, heavy fill) up to 8192 points
+    // factor dense unless a mode is forced: 1537 points at aniso 256^3 level 0, sparse
+    // 3.0 s -> dense 0.21 s
+    const int sp0 = qf_sparse_mode();
+    auto sp_of = [&](uint32_t nz) {
+      return g_qf_split_depth > 0 && nz <= 8192 && !g_qf_sparse_forced ? 0 : sp0;
+    };
     std::vector<uint32_t> bigs;
     for (uint32_t c : big) {
       const uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
@@ -1071,6 +1082,7 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
     for (uint32_t c : big) {
       uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
       bignz.push_back(nz);
+      const int sp = sp_of(nz);
       if (!sp) {
         bigstat.push_back(nullptr);
         launch_coop(c, nz);
@@ -1833,6 +1845,16 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
 // find_support pieces (amg_setup.c:1260).  Removed entries are zeroed in place
 // (equivalent for every later use: DESIGN.md "find_support").
 // ---------------------------------------------------------------------------
+// rows / columns of R past this many entries take grid-wide kernels (AMGD_FS_LONG, tests)
+static int64_t g_fs_long = -1;
+extern "C" void amgd_fs_set_long(int64_t n) { g_fs_long = n; }
+static uint32_t fs_long() {
+  if (g_fs_long < 0) {
+    const char *e = getenv("AMGD_FS_LONG");
+    g_fs_long = e && *e ? atoll(e) : 4096;
+  }
+  return g_fs_long == 0 ? 0xffffffffu : (uint32_t)g_fs_long;
+}
 __global__ void k_csc_gemv(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
                            const double *a, const double *x, uint32_t n, double *z) {
   GRID_STRIDE(c, n) {
@@ -1872,13 +1894,15 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
                                                    const uint64_t *perm, double *ta, double *a,
                                                    const double *rs, const uint32_t *list,
                                                    const unsigned *nlist, uint32_t *si,
-                                                   uint32_t *sj, unsigned *removed) {
+                                                   uint32_t *sj, unsigned *removed,
+                                                   uint32_t maxlen) {
   const uint32_t sub = threadIdx.x & (G - 1);
   const uint32_t n = *nlist;
   const uint64_t g0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
   for (uint64_t r = g0; r < n; r += gs) {
     const uint32_t c = list[r];
+    if (tro[c + 1] - tro[c] > maxlen) continue;      // k_fs_select_long
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
     for (uint64_t q = tro[c] + sub; q < tro[c + 1]; q += G) {
@@ -1896,6 +1920,43 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
       sj[r] = c;
       if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
     }
+  }
+}
+// bad columns past fs_long() entries: one 1024-thread block each (k_fs_select skips them);
+// llist holds their slots in the bad list
+__global__ __launch_bounds__(1024) void k_fs_select_long(const uint64_t *tro, const uint32_t *trow,
+                                                         const uint64_t *perm, double *ta, double *a,
+                                                         const double *rs, const uint32_t *list,
+                                                         const uint32_t *llist, const unsigned *nl,
+                                                         uint32_t *si, uint32_t *sj,
+                                                         unsigned *removed) {
+  __shared__ double smx[16];
+  __shared__ unsigned long long sbest[16];
+  const unsigned n = *nl;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (unsigned t = blockIdx.x; t < n; t += gridDim.x) {
+    const uint32_t r = llist[t], c = list[r];
+    double mx = -DBL_MAX;
+    uint64_t best = ~0ull;
+    for (uint64_t q = tro[c] + threadIdx.x; q < tro[c + 1]; q += 1024) {
+      double x = ta[q] * rs[trow[q]];
+      if (x > mx) { mx = x; best = q; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      double om = __shfl_xor(mx, o, 64);
+      unsigned long long ob = __shfl_xor((unsigned long long)best, o, 64);
+      if (om > mx || (om == mx && ob < best)) { mx = om; best = ob; }
+    }
+    if (lane == 0) { smx[w] = mx; sbest[w] = best; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int q = 1; q < 16; q++)
+        if (smx[q] > mx || (smx[q] == mx && sbest[q] < best)) { mx = smx[q]; best = sbest[q]; }
+      si[r] = best != ~0ull ? trow[best] : 0u;
+      sj[r] = c;
+      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
+    }
+    __syncthreads();
   }
 }
 // short rows: one thread per listed row, in order
@@ -1954,11 +2015,12 @@ __global__ void k_fs_expand(const uint64_t *ro, const uint32_t *col, const uint3
 }
 __global__ void k_fs_expand_wave(const uint64_t *ro, const uint32_t *col, const uint32_t *list,
                                  uint32_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
-                                 unsigned *cnt, uint32_t cap) {
+                                 unsigned *cnt, uint32_t cap, uint32_t maxlen) {
   const int lane = threadIdx.x & 63;
   for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n;
        r += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
     const uint32_t i = list[r];
+    if (ro[i + 1] - ro[i] > maxlen) continue;     // k_fs_expand_long
     for (uint64_t k0 = ro[i]; k0 < ro[i + 1]; k0 += 64) {
       const uint64_t k = k0 + lane;
       bool fresh = false;
@@ -1969,16 +2031,54 @@ __global__ void k_fs_expand_wave(const uint64_t *ro, const uint32_t *col, const 
     }
   }
 }
+// Long rows (past fs_long() entries: the orphan coarse point's column, 10^4 - 10^5 rows)
+// spread over the whole grid; k_fs_expand_wave skips them.
+__global__ void k_fs_expand_long(const uint64_t *ro, const uint32_t *col, const uint32_t *llist,
+                                 const unsigned *nl, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                                 unsigned *cnt, uint32_t cap) {
+  const unsigned n = *nl;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (unsigned r = 0; r < n; r++) {
+    const uint32_t i = llist[r];
+    const uint64_t k1 = ro[i + 1];
+    for (uint64_t b = ro[i] + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < k1;
+         b += stride) {                       // uniform per wavefront (wave_append)
+      const uint64_t k = b + lane;
+      bool fresh = false;
+      uint32_t c = 0;
+      if (k < k1) { c = col[k]; fresh = atomicExch(&stamp[c], tag) != tag; }
+      const unsigned p = wave_append(cnt, fresh);
+      if (fresh && p < cap) out[p] = c;
+    }
+  }
+}
+// entries r of list (n, or *nd when nd is given) whose row list[r] is longer than
+// maxlen: the row (slot = 0) or the slot r (slot = 1) appended to out
+__global__ void k_pick_long(const uint64_t *ro, const uint32_t *list, uint32_t n, const unsigned *nd,
+                            uint32_t maxlen, int slot, uint32_t *out, unsigned *cnt) {
+  const uint64_t m = nd ? *nd : n;
+  GRID_STRIDE(r, m) {
+    const uint32_t i = list[r];
+    if (ro[i + 1] - ro[i] > maxlen) out[atomicAdd(cnt, 1u)] = slot ? (uint32_t)r : i;
+  }
+}
 extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,
                                    uint32_t tag, uint32_t *out, uint32_t cap) {
   if (!n) return 0;
   unsigned *cnt = (unsigned *)amgd_alloc(16);
-  amgd_memset(cnt, 0, 4);
-  if (M->rn && M->nnz >= 16ull * M->rn)
+  amgd_memset(cnt, 0, 8);
+  if (M->rn && M->nnz >= 16ull * M->rn) {
+    uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 4);
+    const uint32_t ml = fs_long();
+    k_pick_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, nullptr, ml, 0, ll, cnt + 1);
+    k_fs_expand_long<<<512, 256, 0, amgd_s()>>>(M->ro, M->col, ll, cnt + 1, stamp, tag, out, cnt, cap);
     k_fs_expand_wave<<<grid_for((uint64_t)n * 64, 256, 16384), 256, 0, amgd_s()>>>(
-        M->ro, M->col, list, n, stamp, tag, out, cnt, cap);
-  else
+        M->ro, M->col, list, n, stamp, tag, out, cnt, cap, ml);
+    amgd_free(ll);
+  } else {
     k_fs_expand<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, M->col, list, n, stamp, tag, out, cnt, cap);
+  }
   KCHECK();
   unsigned h = 0;
   amgd_d2h(&h, cnt, 4);
@@ -1997,15 +2097,21 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(16);
   amgd_memset(cnt, 0, 16);
+  uint32_t *llist = nullptr;
   if (nc) {
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
+    llist = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
+    k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, fs_long(), 1,
+                                                       llist, cnt + 3);
+    k_fs_select_long<<<64, 1024, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, llist,
+                                         cnt + 3, sel_i, sel_j, cnt + 1);
     uint64_t avg = (Rt->nnz + nc - 1) / nc;
     int G = 4;
     while (G < 64 && (uint64_t)G * 2 <= avg) G <<= 1;
     const int gb = grid_for((uint64_t)nc * G, 256, 16384);
 #define FS_SEL(GG)                                                                        \
     k_fs_select<GG><<<gb, 256, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, cnt + 2, \
-                                       sel_i, sel_j, cnt + 1)
+                                       sel_i, sel_j, cnt + 1, fs_long())
     switch (G) {
       case 4: FS_SEL(4); break;
       case 8: FS_SEL(8); break;
@@ -2033,6 +2139,7 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   }
   amgd_free(list);
   amgd_free(cnt);
+  if (llist) amgd_free(llist);
   *nremoved = h[1];
   return h[0];
 }

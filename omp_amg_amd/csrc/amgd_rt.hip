@@ -502,16 +502,20 @@ __device__ __forceinline__ double bn_product(const double *a, const double *b, u
   return MODE_ == 0 ? x * b[i] : MODE_ == 1 ? x * x : (x * b[i]) * b[i];
 }
 // the whole block adds products [lo, hi) to the running sum s (uniform), in order
+// MODE 0: a[i]*b[i], 1: a[i]^2, 2: (a[i]*b[i])*b[i], 3: a[i]*b[gcol[i]] (a row of a
+// sparse matrix times a gathered vector), 4: a[i]
 template <int MODE>
 __device__ double binade_range(const double *a, const double *b, uint64_t lo, uint64_t hi, double s,
-                               double *tile, long long *sh, double *s_sh, int *viol_sh) {
+                               double *tile, long long *sh, double *s_sh, int *viol_sh,
+                               const uint32_t *gcol = nullptr) {
   const int tid = threadIdx.x;
   for (uint64_t base = lo; base < hi; base += BN_TILE) {
     int tlen = (int)min((uint64_t)BN_TILE, hi - base);
     for (int q = tid; q < tlen; q += BN_THREADS) {
       uint64_t i = base + q;
       double x = a[i];
-      tile[q] = MODE == 0 ? x * b[i] : MODE == 1 ? x * x : (x * b[i]) * b[i];
+      tile[q] = MODE == 0 ? x * b[i] : MODE == 1 ? x * x : MODE == 2 ? (x * b[i]) * b[i]
+              : MODE == 3 ? x * b[gcol[i]] : x;
     }
     __syncthreads();
     int j = 0, rounds = 0;
@@ -608,6 +612,34 @@ __device__ double binade_range(const double *a, const double *b, uint64_t lo, ui
     __syncthreads();
   }
   return s;
+}
+
+// Long rows of a row-list product (amgd_spmv_rows): one block per row, the ordered sum
+// sum_k a[k]*x[col[k]] (or sum_k a[k]) from +0, left to right, bit for bit, by the
+// binade scan.  nlist is read on the device; surplus blocks exit at once.
+template <int MODE>
+__global__ __launch_bounds__(BN_THREADS) void k_rows_exact(const uint64_t *ro, const uint32_t *col,
+                                                           const double *a, const double *x,
+                                                           const uint32_t *list,
+                                                           const unsigned *nlist, double *z) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  __shared__ double s_sh;
+  __shared__ int viol_sh;
+  const unsigned n = *nlist;
+  for (unsigned r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t i = list[r];
+    const double s = binade_range<MODE>(a, x, ro[i], ro[i + 1], 0.0, tile, sh, &s_sh, &viol_sh, col);
+    if (threadIdx.x == 0) z[i] = s;
+    __syncthreads();
+  }
+}
+extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
+                                const double *x, const uint32_t *list, const unsigned *nlist,
+                                int blocks, double *z) {
+  if (x) k_rows_exact<3><<<blocks, BN_THREADS, 0, amgd_s()>>>(ro, col, a, x, list, nlist, z);
+  else k_rows_exact<4><<<blocks, BN_THREADS, 0, amgd_s()>>>(ro, col, a, x, list, nlist, z);
+  KCHECK();
 }
 
 template <int MODE>

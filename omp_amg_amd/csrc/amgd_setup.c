@@ -520,17 +520,22 @@ static dcsr *find_support(const dcsr *R, double goal) {
   }
   uint64_t prev_off = 0;
   uint32_t prev_nsel = 0;
+  const int fslog = getenv("AMGD_FSLOG") != NULL;
   ph(PH_FS);
   for (;;) {
     it++;
     int done = 0;
+    uint32_t n1 = 0, n2 = 0, n3 = 0;
+    double t0 = 0, t1 = 0;
+    if (fslog) { amgd_sync(); t0 = amgd_wtime(); }
     if (fs_inc && it > 1 && prev_nsel <= cap_c) {
-      const uint32_t n1 = amgd_fs_expand(Rl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c);
+      n1 = amgd_fs_expand(Rl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c);
       if (n1 <= cap_c) {
-        const uint32_t n2 = amgd_fs_expand(Rt, L1, n1, st_r, ++tag, L2, cap_r);
+        n2 = amgd_fs_expand(Rt, L1, n1, st_r, ++tag, L2, cap_r);
         if (n2 <= cap_r) {
-          const uint32_t n3 = amgd_fs_expand(Rl, L2, n2, st_c, ++tag, L3, cap_c);
+          n3 = amgd_fs_expand(Rl, L2, n2, st_c, ++tag, L3, cap_c);
           if (n3 <= cap_c) {
+            if (fslog) { amgd_sync(); t1 = amgd_wtime(); }
             amgd_spmv_rows(Rt, L1, n1, rs, w);          /* w  on C1 */
             amgd_spmv_rows(Rl, L2, n2, w, tmp);         /* tmp on D2 */
             amgd_spmv_rows(Rt, L3, n3, tmp, w2);        /* w2 on C3 */
@@ -557,9 +562,12 @@ static dcsr *find_support(const dcsr *R, double goal) {
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
-    if (getenv("AMGD_FSLOG"))
-      fprintf(stderr, "fs L%d nf %u nc %u nnz %lu it %d sel %u rem %u theta %g\n", g_lvl, nf, nc,
-              (unsigned long)R->nnz, it, nsel, nrem, theta);
+    if (fslog) {
+      amgd_sync();
+      fprintf(stderr, "fs L%d nf %u nc %u nnz %lu it %d sel %u rem %u theta %g | %s n %u/%u/%u expand %.3f ms, sweep+max+sel %.3f ms\n",
+              g_lvl, nf, nc, (unsigned long)R->nnz, it, nsel, nrem, theta, done ? "inc" : "full",
+              n1, n2, n3, done ? (t1 - t0) * 1e3 : 0., (amgd_wtime() - (done ? t1 : t0)) * 1e3);
+    }
     ph(PH_FS_SEL);
     if (nrem == 0) { g_ub++; break; }                    /* no progress: reference loops */
     if (ns + nc > cap) { g_ub++; break; }

@@ -552,7 +552,8 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
-                                                   double beta, const uint8_t *f) {
+                                                   double beta, const uint8_t *f,
+                                                   uint32_t maxlen = 0xffffffffu) {
   constexpr int SEG = 1024 / RW;
   __shared__ double buf[4][RW][SEG + 1];
   __shared__ uint64_t rk0[4][RW];
@@ -563,7 +564,8 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     const uint64_t r = rb + lane;
     const bool own = lane < RW && r < n;
     const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
-    const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    if (LIST && k1 - k0 > maxlen) k1 = k0;      // a long row: left to k_rows_exact
     const uint32_t len = (uint32_t)(k1 - k0);
     if (lane < RW) {
       rk0[w][lane] = k0;
@@ -636,7 +638,7 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
 #pragma unroll
       for (int q = 0; q < 16; q++) v[q] = hv[q] ? (x ? an[q] * x[cn[q]] : an[q]) : 0.0;
     }
-    if (own) {
+    if (own && (!LIST || ro[i + 1] - ro[i] <= maxlen)) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
@@ -651,42 +653,75 @@ static int lane_rw(uint64_t n) {
   if (g_rw_forced == 4 || g_rw_forced == 16 || g_rw_forced == 64) return (int)g_rw_forced;
   return n >= (1u << 22) ? 64 : n >= (1u << 16) ? 16 : 4;
 }
-#define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_)                                  \
+#define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
     const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
     if (rw_ == 64)                                                                            \
       k_spmv_lane<LIST, 64><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
-                                                       al, y_, be, f_);                       \
+                                                       al, y_, be, f_, ml_);                  \
     else if (rw_ == 16)                                                                       \
       k_spmv_lane<LIST, 16><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
-                                                       al, y_, be, f_);                       \
+                                                       al, y_, be, f_, ml_);                  \
     else                                                                                      \
       k_spmv_lane<LIST, 4><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,   \
-                                                      al, y_, be, f_);                        \
+                                                      al, y_, be, f_, ml_);                   \
   } while (0)
-// ordered sums (x == nullptr) or products of the listed rows only
+// ordered sums (x == nullptr) or products of the listed rows only (rows longer than
+// maxlen are skipped: k_rows_exact does them)
 __global__ __launch_bounds__(256) void k_spmv_wave_list(const uint64_t *ro, const uint32_t *col,
                                                         const double *a, const uint32_t *list,
-                                                        uint32_t n, const double *x, double *z) {
+                                                        uint32_t n, const double *x, double *z,
+                                                        uint32_t maxlen) {
   __shared__ double buf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
     const uint32_t i = list[r];
+    if (ro[i + 1] - ro[i] > maxlen) continue;
     const double t = wave_row_sum(col, a, x, ro[i], ro[i + 1], buf[w], lane);
     if (lane == 0) z[i] = t;
   }
 }
+// the listed rows longer than maxlen, appended to out (count in *cnt)
+__global__ void k_list_long(const uint64_t *ro, const uint32_t *list, uint32_t n, uint32_t maxlen,
+                            uint32_t *out, unsigned *cnt) {
+  GRID_STRIDE(r, n) {
+    const uint32_t i = list[r];
+    if (ro[i + 1] - ro[i] > maxlen) out[atomicAdd(cnt, 1u)] = i;
+  }
+}
+extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
+                                const double *x, const uint32_t *list, const unsigned *nlist,
+                                int blocks, double *z);
+// Rows past SPMV_LONG entries (the orphan coarse point's column of find_support's R:
+// 10^4 - 10^5 entries) take one 1024-thread block each (exact binade scan) instead of
+// one lane / wave adding them one by one.
+#define SPMV_LONG 4096
+static int64_t g_mv_long = -1;    // AMGD_MV_LONG: long-row threshold of the listed products
+extern "C" void amgd_spmv_set_long(int64_t n) { g_mv_long = n; }
+static uint32_t mv_long() {
+  if (g_mv_long < 0) g_mv_long = sl_env("AMGD_MV_LONG", SPMV_LONG);
+  return g_mv_long == 0 ? 0xffffffffu : (uint32_t)g_mv_long;
+}
 extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x,
                                double *z) {
   if (!n) return;
+  const uint32_t ml = mv_long();
+  if (ml != 0xffffffffu) {
+    uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 16);
+    unsigned *cnt = (unsigned *)(ll + n);
+    amgd_memset(cnt, 0, 4);
+    k_list_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, ml, ll, cnt);
+    amgd_rows_exact(M->ro, M->col, M->a, x, ll, cnt, (int)std::min<uint32_t>(n, 64u), z);
+    amgd_free(ll);
+  }
   if ((int64_t)n < sl_min_list()) {          // too few rows to fill the chip one row per lane
     int g = (int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536);
-    k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z);
+    k_spmv_wave_list<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, list, n, x, z, ml);
     KCHECK();
     return;
   }
-  LANE_LAUNCH(true, n, list, x, z, 0.0, nullptr, 1.0, nullptr);
+  LANE_LAUNCH(true, n, list, x, z, 0.0, nullptr, 1.0, nullptr, ml);
   KCHECK();
 }
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
@@ -727,7 +762,7 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     amgd_timer_start(1);                       // roofline: whole-matrix long-row products
-    LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f);
+    LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
     amgd_timer_stop(1);
     g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + 16ull * M->rn + 8 +
                   (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);

@@ -181,6 +181,12 @@ API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }
 /* huge supports factored per connected component (1, default) or whole (0); -1: env */
 extern void amgd_qfactor_set_split(int on);
 API void amgd_test_qf_split(int on) { amgd_qfactor_set_split(on); }
+/* long-row thresholds: listed products (k_rows_exact) and find_support's expand / select;
+   0 disables, -1 restores the environment / default (4096) */
+extern void amgd_spmv_set_long(int64_t n);
+extern void amgd_fs_set_long(int64_t n);
+API void amgd_test_mv_long(int64_t n) { amgd_spmv_set_long(n); }
+API void amgd_test_fs_long(int64_t n) { amgd_fs_set_long(n); }
 extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
 /* window of the dense-accumulator numeric kernel for wide rows: 0 (hash kernels), 8192, 16384 */

@@ -239,10 +239,19 @@ def _adversarial_rows(rng, rn=700):
                       np.array(vals))
 
 
+@pytest.fixture(params=[-1, 64], ids=["long4096", "long64"])
+def mv_long(request):
+    """listed products: rows past 4096 (default) / 64 entries take k_rows_exact"""
+    oa.mv_long(request.param)
+    yield request.param
+    oa.mv_long(-1)
+
+
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_adversarial_rows(sl_min, rw):
+def test_spmv_adversarial_rows(sl_min, rw, mv_long):
     """long-row SpMV / row sums / listed rows on adversarial rows through the wave-per-row
-    and the lane-per-row kernels (every RW), bit for bit against the sequential loop
+    and the lane-per-row kernels (every RW) and, for listed rows past the long-row
+    threshold, the block-per-row binade scan, bit for bit against the sequential loop
     (nan compared as nan)"""
     A = _adversarial_rows(np.random.default_rng(77))
     with np.errstate(all="ignore"):
@@ -255,9 +264,10 @@ def test_spmv_adversarial_rows(sl_min, rw):
         got = oa.test_spmv(A, x)
         rows = np.arange(A.rn, dtype=np.uint32)[::-1].copy()
         got_l = oa.test_spmv_rows(A, rows, x, np.zeros(A.rn))
+        got_ls = oa.test_spmv_rows(A, rows, None, np.zeros(A.rn))
     finally:
         oa.spmv_sl_min(-1)
-    for g, w in ((got_s, want_s), (got, want), (got_l, want)):
+    for g, w in ((got_s, want_s), (got, want), (got_l, want), (got_ls, want_s)):
         assert np.array_equal(g.view(np.uint64), w.view(np.uint64)) or \
             np.array_equal(np.isnan(g), np.isnan(w)) and np.array_equal(g[~np.isnan(g)].view(np.uint64),
                                                                        w[~np.isnan(w)].view(np.uint64))
@@ -286,7 +296,7 @@ def test_spmv_long_rows_ragged(sl_min, rw):
 
 
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_rows_listed(sl_min, rw):
+def test_spmv_rows_listed(sl_min, rw, mv_long):
     """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
     threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
     rng = np.random.default_rng(29)
@@ -528,15 +538,16 @@ def test_qfactor_tiers_bitexact(structure, mode, coop_lds):
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("structure,mode", [("blocks", 1), ("blocks", 0), ("scattered", 1),
-                                            ("tiers", 1)])
+@pytest.mark.parametrize("structure,mode", [("blocks", 1), ("blocks", 0), ("blocks", 2),
+                                            ("scattered", 1), ("tiers", 1)])
 def test_qfactor_split_bitexact(structure, mode):
     """huge supports whose Gram matrix is block-diagonal (several connected components
     of A on the support) are factored per component -- through the ordinary tiers, or
     the huge kernels for components past 1024 points -- and scattered into a -0-filled
     triangle: bit for bit the oracle's one sequential factor, cross-component -0 included.
     'blocks' holds two-, three- and many-component supports; 'scattered' a diagonal one
-    (1100 components) and a random one; a single-component support stays whole"""
+    (1100 components) and a random one; a single-component support stays whole.
+    mode: 1 automatic (components up to 8192 points dense), 0 dense, 2 forced sparse"""
     W, A = _qfactor_case(structure)
     oa.qf_sparse(mode)
     oa.qf_split(1)
@@ -547,8 +558,9 @@ def test_qfactor_split_bitexact(structure, mode):
         oa.qf_sparse(1)
         oa.qf_split(-1)
     st = oa.qf_stats()
-    if structure == "blocks":                # 2 + 3 + 3 components; 1300 / 1200 stay huge
-        assert st["split"] == 3 and st["sparse"] + st["fallback"] == (2 if mode else 0), st
+    if structure == "blocks":                # 2 + 3 + 69 components; 1300 / 1200 stay huge,
+        # factored dense unless a sparse mode is forced (mode 2: sparse, then the fallback)
+        assert st["split"] == 3 and st["sparse"] + st["fallback"] == (2 if mode == 2 else 0), st
     elif structure == "scattered":
         assert st["split"] >= 1, st
     ref = _oracle_qfactor(W, A)

@@ -160,14 +160,23 @@ def test_gpu_incremental_coarsen_matches_full_sweeps(m, stencil, min_rows, list_
 
 
 # incremental find_support sweeps (amgd_setup.c find_support): forced at every size,
-# and off, the hierarchy must stay bit-identical to the reference's / the oracle's
-@pytest.mark.parametrize("mode", ["2", "0"], ids=["fs_inc_always", "fs_inc_off"])
+# and off, the hierarchy must stay bit-identical to the reference's / the oracle's.
+# "long8": rows / columns of R past 8 entries through the grid-wide expand, the
+# block-per-column select and the block-per-row exact products (default: 4096)
+@pytest.mark.parametrize("mode", ["2", "0", "2long8"], ids=["fs_inc_always", "fs_inc_off", "long8"])
 @pytest.mark.parametrize("case", ["p7_12", "p27_8", "sem_e3_N2", "aniso_12", "amgdmp", "p2d9_24"])
 def test_gpu_fs_incremental_bitexact_fixture(case, mode, monkeypatch):
-    monkeypatch.setenv("AMGD_FS_INC", mode)
+    monkeypatch.setenv("AMGD_FS_INC", mode[0])
     z = np.load(os.path.join(GOLD, case + ".npz"))
     ref = parity.from_npz(z)
-    h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    if mode.endswith("long8"):
+        oa.fs_long(8)
+        oa.mv_long(8)
+    try:
+        h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    finally:
+        oa.fs_long(-1)
+        oa.mv_long(-1)
     bad = parity.compare(ref, h, exact=True)
     assert not bad, bad
 
