@@ -1996,7 +1996,8 @@ __global__ __launch_bounds__(256) void k_list_rowsum(const uint64_t *ro, const d
   }
 }
 // Incremental find_support sweeps: the distinct neighbours (columns of M) of the listed
-// rows, first visit claimed by an exchange of the neighbour's stamp with `tag`.
+// rows, first visit claimed by an exchange of the neighbour's stamp with `tag` (a plain
+// load first skips the exchange for neighbours already claimed: most of them).
 // Returns the count, which may exceed cap (the list is then incomplete: the caller
 // falls back to full products).
 __global__ void k_fs_expand(const uint64_t *ro, const uint32_t *col, const uint32_t *list,
@@ -2006,7 +2007,7 @@ __global__ void k_fs_expand(const uint64_t *ro, const uint32_t *col, const uint3
     const uint32_t i = list[r];
     for (uint64_t k = ro[i]; k < ro[i + 1]; k++) {
       const uint32_t c = col[k];
-      if (atomicExch(&stamp[c], tag) != tag) {
+      if (stamp[c] != tag && atomicExch(&stamp[c], tag) != tag) {
         const unsigned p = atomicAdd(cnt, 1u);
         if (p < cap) out[p] = c;
       }
@@ -2025,7 +2026,7 @@ __global__ void k_fs_expand_wave(const uint64_t *ro, const uint32_t *col, const 
       const uint64_t k = k0 + lane;
       bool fresh = false;
       uint32_t c = 0;
-      if (k < ro[i + 1]) { c = col[k]; fresh = atomicExch(&stamp[c], tag) != tag; }
+      if (k < ro[i + 1]) { c = col[k]; fresh = stamp[c] != tag && atomicExch(&stamp[c], tag) != tag; }
       const unsigned p = wave_append(cnt, fresh);
       if (fresh && p < cap) out[p] = c;
     }
@@ -2047,7 +2048,7 @@ __global__ void k_fs_expand_long(const uint64_t *ro, const uint32_t *col, const 
       const uint64_t k = b + lane;
       bool fresh = false;
       uint32_t c = 0;
-      if (k < k1) { c = col[k]; fresh = atomicExch(&stamp[c], tag) != tag; }
+      if (k < k1) { c = col[k]; fresh = stamp[c] != tag && atomicExch(&stamp[c], tag) != tag; }
       const unsigned p = wave_append(cnt, fresh);
       if (fresh && p < cap) out[p] = c;
     }

@@ -614,34 +614,6 @@ __device__ double binade_range(const double *a, const double *b, uint64_t lo, ui
   return s;
 }
 
-// Long rows of a row-list product (amgd_spmv_rows): one block per row, the ordered sum
-// sum_k a[k]*x[col[k]] (or sum_k a[k]) from +0, left to right, bit for bit, by the
-// binade scan.  nlist is read on the device; surplus blocks exit at once.
-template <int MODE>
-__global__ __launch_bounds__(BN_THREADS) void k_rows_exact(const uint64_t *ro, const uint32_t *col,
-                                                           const double *a, const double *x,
-                                                           const uint32_t *list,
-                                                           const unsigned *nlist, double *z) {
-  __shared__ double tile[BN_TILE];
-  __shared__ long long sh[BN_THREADS / 64 + 1];
-  __shared__ double s_sh;
-  __shared__ int viol_sh;
-  const unsigned n = *nlist;
-  for (unsigned r = blockIdx.x; r < n; r += gridDim.x) {
-    const uint32_t i = list[r];
-    const double s = binade_range<MODE>(a, x, ro[i], ro[i + 1], 0.0, tile, sh, &s_sh, &viol_sh, col);
-    if (threadIdx.x == 0) z[i] = s;
-    __syncthreads();
-  }
-}
-extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
-                                const double *x, const uint32_t *list, const unsigned *nlist,
-                                int blocks, double *z) {
-  if (x) k_rows_exact<3><<<blocks, BN_THREADS, 0, amgd_s()>>>(ro, col, a, x, list, nlist, z);
-  else k_rows_exact<4><<<blocks, BN_THREADS, 0, amgd_s()>>>(ro, col, a, x, list, nlist, z);
-  KCHECK();
-}
-
 template <int MODE>
 __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, const double *b,
                                                            uint64_t n, double *out) {
@@ -829,6 +801,233 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
     __syncthreads();
   }
   if (tid == 0) *out = s;
+}
+// ---------------------------------------------------------------------------
+// Long rows of a row-list product (amgd_spmv_rows): the ordered sums
+// sum_k a[k]*x[col[k]] (MODE 3) or sum_k a[k] (MODE 4) of rows of 10^4 - 10^5 entries,
+// bit for bit, by the speculation above applied per row: the rows' BN_TILE chunks are
+// summed and speculated on by the whole grid, then one block per row walks its chunk
+// records (binade_range for a chunk that fails).  The row list and its length live on
+// the device; every kernel reads the length there.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double seg_product(const double *a, const double *x, const uint32_t *col,
+                                             uint64_t k, int MODE_) {
+  return MODE_ == 3 ? a[k] * x[col[k]] : a[k];
+}
+// chunk offsets of the listed rows (exclusive scan of ceil(len / BN_TILE)); one block
+__global__ __launch_bounds__(BN_THREADS) void k_seg_prep(const uint64_t *ro, const uint32_t *list,
+                                                         const unsigned *nl, uint64_t *choff) {
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  const unsigned n = *nl;
+  long long run = 0;
+  for (unsigned b = 0; b < n; b += BN_THREADS) {
+    const unsigned r = b + threadIdx.x;
+    long long c = 0;
+    if (r < n) {
+      const uint32_t i = list[r];
+      c = (long long)((ro[i + 1] - ro[i] + BN_TILE - 1) / BN_TILE);
+    }
+    long long total;
+    const long long pre = bn_block_excl_scan(c, sh, &total);
+    if (r < n) choff[r] = (uint64_t)(run + pre);
+    run += total;
+  }
+  if (threadIdx.x == 0) choff[n] = (uint64_t)run;
+}
+__device__ __forceinline__ unsigned seg_row_of(const uint64_t *choff, unsigned n, uint64_t g) {
+  unsigned lo = 0, hi = n;                     // last r with choff[r] <= g
+  while (hi - lo > 1) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (choff[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+template <int MODE>
+__global__ __launch_bounds__(SP_T) void k_seg_csum(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, const double *x,
+                                                   const uint32_t *list, const unsigned *nl,
+                                                   const uint64_t *choff, double *csum) {
+  __shared__ double red[SP_T];
+  const unsigned n = *nl;
+  const uint64_t G = choff[n];
+  for (uint64_t g = blockIdx.x; g < G; g += gridDim.x) {
+    const unsigned r = seg_row_of(choff, n, g);
+    const uint32_t i = list[r];
+    const uint64_t lo = ro[i] + (g - choff[r]) * BN_TILE, hi = min(ro[i + 1], lo + BN_TILE);
+    double t = 0;
+    for (uint64_t k = lo + threadIdx.x; k < hi; k += SP_T) t += seg_product(a, x, col, k, MODE);
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int o = SP_T / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) csum[g] = red[0];
+    __syncthreads();
+  }
+}
+// per row: chunk sums -> exclusive prefixes (a guess of the running sum; any order)
+__global__ void k_seg_prefix(const unsigned *nl, const uint64_t *choff, double *csum) {
+  const unsigned n = *nl;
+  GRID_STRIDE(r, n) {
+    double t = 0;
+    for (uint64_t g = choff[r]; g < choff[r + 1]; g++) { const double v = csum[g]; csum[g] = t; t += v; }
+  }
+}
+template <int MODE>
+__global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, const double *x,
+                                                   const uint32_t *list, const unsigned *nl,
+                                                   const uint64_t *choff, const double *approx,
+                                                   SpecRec *rec) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long ssum[SP_T / 64], smin[SP_T / 64], smax[SP_T / 64];
+  __shared__ int sflag;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const unsigned n = *nl;
+  const uint64_t G = choff[n];
+  for (uint64_t g = blockIdx.x; g < G; g += gridDim.x) {
+    const unsigned r = seg_row_of(choff, n, g);
+    const uint32_t i = list[r];
+    const uint64_t lo = ro[i] + (g - choff[r]) * BN_TILE, hi = min(ro[i + 1], lo + BN_TILE);
+    const int tlen = (int)(hi - lo);
+    for (int q = tid; q < tlen; q += SP_T) tile[q] = seg_product(a, x, col, lo + q, MODE);
+    if (tid == 0) sflag = 0;
+    __syncthreads();
+    const double gs = approx[g];
+    int flag = !(fabs(gs) >= 1e-290) || !(fabs(gs) < 1e300);
+    const int e = flag ? 0 : ilogb(gs);
+    const double u = ldexp(1.0, e - 52);
+    long long loc = 0, lmin = 0x7fffffffffffffffll, lmax = -0x7fffffffffffffffll;
+    const int first = tid * SP_PER;
+    for (int q = 0; q < SP_PER; q++) {
+      const int idx = first + q;
+      if (idx >= tlen) break;
+      const double v = tile[idx] / u;
+      const double rr = rint(v);
+      if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) { flag = 1; break; }
+      loc += (long long)rr;
+      lmin = loc < lmin ? loc : lmin;
+      lmax = loc > lmax ? loc : lmax;
+    }
+    if (flag) atomicOr(&sflag, 1);
+    long long xs = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long y = __shfl_up(xs, o, 64);
+      if (lane >= o) xs += y;
+    }
+    const long long pre_w = xs - loc;
+    long long mn = first < tlen ? pre_w + lmin : 0x7fffffffffffffffll;
+    long long mx = first < tlen ? pre_w + lmax : -0x7fffffffffffffffll;
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long m1 = __shfl_xor(mn, o, 64), m2 = __shfl_xor(mx, o, 64);
+      mn = m1 < mn ? m1 : mn;
+      mx = m2 > mx ? m2 : mx;
+    }
+    if (lane == 63) ssum[w] = xs;
+    if (lane == 0) { smin[w] = mn; smax[w] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      long long run = 0, gmn = 0x7fffffffffffffffll, gmx = -0x7fffffffffffffffll;
+      for (int q = 0; q < SP_T / 64; q++) {
+        if (smin[q] != 0x7fffffffffffffffll) {
+          gmn = run + smin[q] < gmn ? run + smin[q] : gmn;
+          gmx = run + smax[q] > gmx ? run + smax[q] : gmx;
+        }
+        run += ssum[q];
+      }
+      SpecRec rc;
+      rc.M = run; rc.mn = gmn; rc.mx = gmx; rc.e = e; rc.flag = sflag;
+      rec[g] = rc;
+    }
+    __syncthreads();
+  }
+}
+// one block per row: the run of passing chunks found by a block scan (k_dot_resolve),
+// a failing chunk added by binade_range
+template <int MODE>
+__global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, const uint32_t *col,
+                                                            const double *a, const double *x,
+                                                            const uint32_t *list, const unsigned *nl,
+                                                            const uint64_t *choff, const SpecRec *rec,
+                                                            double *z) {
+  __shared__ double tile[BN_TILE];
+  __shared__ long long sh[BN_THREADS / 64 + 1];
+  __shared__ double s_sh;
+  __shared__ int viol_sh;
+  const int tid = threadIdx.x;
+  const long long LO = (1ll << 52), HI = (1ll << 53);
+  const unsigned n = *nl;
+  for (unsigned r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t i = list[r];
+    const uint64_t c0 = choff[r], c1 = choff[r + 1], k0 = ro[i], k1 = ro[i + 1];
+    double s = 0.0;
+    uint64_t c = c0;
+    while (c < c1) {
+      const uint64_t ce = min(c1, c + (uint64_t)BN_THREADS);
+      const bool normal = fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1.0e300;
+      const int e = normal ? ilogb(s) : 0;
+      const long long S = normal ? (long long)ldexp(s, 52 - e) : 0ll;
+      const uint64_t q = c + (uint64_t)tid;
+      SpecRec rc;
+      rc.M = 0; rc.mn = 0; rc.mx = 0; rc.e = 0; rc.flag = 1;
+      if (q < ce) rc = rec[q];
+      bool ok = q < ce && normal && !rc.flag && rc.e == e;
+      long long total;
+      const long long pre = bn_block_excl_scan(ok ? rc.M : 0ll, sh, &total);
+      if (ok) {
+        const long long base = (long long)((unsigned long long)S + (unsigned long long)pre);
+        ok = S > 0 ? (base + rc.mn > LO && base + rc.mx < HI) : (base + rc.mx < -LO && base + rc.mn > -HI);
+      }
+      if (tid == 0) viol_sh = 0x7fffffff;
+      __syncthreads();
+      if (q < ce && !ok) atomicMin(&viol_sh, tid);
+      __syncthreads();
+      const int f = viol_sh;
+      const uint64_t run_end = f == 0x7fffffff ? ce : c + (uint64_t)f;
+      if (run_end > c && (uint64_t)tid == run_end - 1 - c)
+        s_sh = ldexp((double)(long long)((unsigned long long)S + (unsigned long long)(pre + rc.M)), e - 52);
+      __syncthreads();
+      if (run_end > c) s = s_sh;
+      __syncthreads();
+      c = run_end;
+      if (c < ce) {
+        const uint64_t lo = k0 + (c - c0) * BN_TILE, hi = min(k1, lo + BN_TILE);
+        s = binade_range<MODE>(a, x, lo, hi, s, tile, sh, &s_sh, &viol_sh, col);
+        c++;
+      }
+    }
+    if (tid == 0) z[i] = s;
+    __syncthreads();
+  }
+}
+// max_entries: an upper bound on the listed rows' total length (the matrix's nnz),
+// nmax on their count: sizes the chunk records
+extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
+                                const double *x, const uint32_t *list, const unsigned *nlist,
+                                uint32_t nmax, uint64_t max_entries, double *z) {
+  if (!nmax) return;
+  hipStream_t st = amgd_s();
+  const uint64_t gmax = max_entries / BN_TILE + nmax + 1;
+  uint64_t *choff = (uint64_t *)amgd_alloc(((size_t)nmax + 1) * 8);
+  double *csum = (double *)amgd_alloc(gmax * 8);
+  SpecRec *rec = (SpecRec *)amgd_alloc(gmax * sizeof(SpecRec));
+  const int G = (int)std::min<uint64_t>(gmax, 1024);
+  const int R = (int)std::min<uint32_t>(nmax, 256);
+  k_seg_prep<<<1, BN_THREADS, 0, st>>>(ro, list, nlist, choff);
+  if (x) {
+    k_seg_csum<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
+    k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
+    k_seg_spec<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
+    k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+  } else {
+    k_seg_csum<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
+    k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
+    k_seg_spec<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
+    k_seg_resolve<4><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+  }
+  KCHECK();
+  amgd_free(choff); amgd_free(csum); amgd_free(rec);
 }
 #define SP_MIN_N (16ull * BN_TILE)
 template <int MODE>

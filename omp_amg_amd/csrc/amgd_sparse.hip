@@ -692,9 +692,9 @@ __global__ void k_list_long(const uint64_t *ro, const uint32_t *list, uint32_t n
 }
 extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
                                 const double *x, const uint32_t *list, const unsigned *nlist,
-                                int blocks, double *z);
+                                uint32_t nmax, uint64_t max_entries, double *z);
 // Rows past SPMV_LONG entries (the orphan coarse point's column of find_support's R:
-// 10^4 - 10^5 entries) take one 1024-thread block each (exact binade scan) instead of
+// 10^4 - 10^5 entries) take the grid-wide exact scan (amgd_rt.hip k_seg_*) instead of
 // one lane / wave adding them one by one.
 #define SPMV_LONG 4096
 static int64_t g_mv_long = -1;    // AMGD_MV_LONG: long-row threshold of the listed products
@@ -712,7 +712,8 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
     unsigned *cnt = (unsigned *)(ll + n);
     amgd_memset(cnt, 0, 4);
     k_list_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, ml, ll, cnt);
-    amgd_rows_exact(M->ro, M->col, M->a, x, ll, cnt, (int)std::min<uint32_t>(n, 64u), z);
+    amgd_rows_exact(M->ro, M->col, M->a, x, ll, cnt, std::min<uint64_t>(n, M->nnz / (ml + 1) + 1),
+                    M->nnz, z);
     amgd_free(ll);
   }
   if ((int64_t)n < sl_min_list()) {          // too few rows to fill the chip one row per lane

@@ -273,6 +273,48 @@ def test_spmv_adversarial_rows(sl_min, rw, mv_long):
                                                                        w[~np.isnan(w)].view(np.uint64))
 
 
+def test_spmv_rows_multichunk_exact():
+    """listed rows of 4097 - 130000 entries (many 4096-entry chunks each) through the
+    grid-wide speculation + per-row resolve: sums growing across binades, exact ties,
+    cancellation to zero, mixed magnitudes, an inf -- bit for bit the sequential loop,
+    listed in any order and beside short rows"""
+    rng = np.random.default_rng(61)
+    cn = 200000
+    lens = [4097, 9000, 50000, 130000, 5, 70000, 8193, 0, 20000]
+    ro, cols, vals = [0], [], []
+    for q, L in enumerate(lens):
+        kind = q % 5
+        if kind == 0:
+            v = np.abs(rng.standard_normal(L)) * 2.0 ** rng.integers(-3, 4, L)
+        elif kind == 1:
+            v = np.where(rng.random(L) < 0.5, 2.0 ** -53, 1.0) * (1 + (rng.random(L) < 0.3))
+        elif kind == 2:
+            h = rng.standard_normal((L + 1) // 2)
+            v = np.concatenate([h, -h])[:L]
+        elif kind == 3:
+            v = rng.standard_normal(L) * 10.0 ** rng.integers(-12, 12, L)
+        else:
+            v = rng.standard_normal(L)
+            if L > 10:
+                v[L // 3] = np.inf
+        c = np.sort(rng.choice(cn, size=L, replace=False))
+        cols.extend(c.tolist())
+        vals.extend(v.tolist())
+        ro.append(len(cols))
+    A = refops.Csr(len(lens), cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64),
+                   np.array(vals))
+    x = np.where(rng.random(cn) < 0.5, 1.0, 0.75)
+    with np.errstate(all="ignore"):
+        want = refops.spmv(A, x)
+        want_s = _rowsums(A)
+    rows = np.array([3, 0, 8, 5, 2, 7, 1, 6, 4], dtype=np.uint32)
+    z0 = np.full(A.rn, -7.25)
+    got = oa.test_spmv_rows(A, rows, x, z0)
+    got_s = oa.test_spmv_rows(A, rows, None, z0)
+    for g, w in ((got, want), (got_s, want_s)):
+        assert np.array_equal(g.view(np.uint64), w.view(np.uint64)), np.nonzero(g != w)
+
+
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
 def test_spmv_long_rows_ragged(sl_min, rw):
     """long-row SpMV kernels on ragged rows: wave-per-row (default below 2^20 rows) and
