@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
         L.amgd_test_fs_long.argtypes = [C.c_int64]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
+        L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]

@@ -1845,15 +1845,22 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
 // find_support pieces (amg_setup.c:1260).  Removed entries are zeroed in place
 // (equivalent for every later use: DESIGN.md "find_support").
 // ---------------------------------------------------------------------------
-// rows / columns of R past this many entries take grid-wide kernels (AMGD_FS_LONG, tests)
-static int64_t g_fs_long = -1;
+// Outlier rows / columns of R (the orphan coarse point's: 10^4 - 10^5 entries among
+// rows of ~10) take grid-wide kernels.  By default an outlier is longer than
+// max(4096, 16 x M's mean row): where every row is long (coarse levels of a 3D Poisson
+// hierarchy) the per-row kernels already fill the chip.  AMGD_FS_LONG /
+// amgd_fs_set_long (tests) force an absolute threshold (0: never).
+static int64_t g_fs_long = -1;        // -1: environment or automatic, -2: automatic
 extern "C" void amgd_fs_set_long(int64_t n) { g_fs_long = n; }
-static uint32_t fs_long() {
-  if (g_fs_long < 0) {
+static uint32_t fs_long(const dcsr *M) {
+  if (g_fs_long == -1) {
     const char *e = getenv("AMGD_FS_LONG");
-    g_fs_long = e && *e ? atoll(e) : 4096;
+    g_fs_long = e && *e ? atoll(e) : -2;
   }
-  return g_fs_long == 0 ? 0xffffffffu : (uint32_t)g_fs_long;
+  if (g_fs_long == 0) return 0xffffffffu;
+  if (g_fs_long > 0) return (uint32_t)g_fs_long;
+  const uint64_t mean = M->rn ? M->nnz / M->rn : 0;
+  return (uint32_t)std::min<uint64_t>(0xfffffffeu, std::max<uint64_t>(4096, 16 * mean));
 }
 __global__ void k_csc_gemv(const uint64_t *tro, const uint32_t *trow, const uint64_t *perm,
                            const double *a, const double *x, uint32_t n, double *z) {
@@ -2071,7 +2078,7 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
   amgd_memset(cnt, 0, 8);
   if (M->rn && M->nnz >= 16ull * M->rn) {
     uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 4);
-    const uint32_t ml = fs_long();
+    const uint32_t ml = fs_long(M);
     k_pick_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, nullptr, ml, 0, ll, cnt + 1);
     k_fs_expand_long<<<512, 256, 0, amgd_s()>>>(M->ro, M->col, ll, cnt + 1, stamp, tag, out, cnt, cap);
     k_fs_expand_wave<<<grid_for((uint64_t)n * 64, 256, 16384), 256, 0, amgd_s()>>>(
@@ -2102,7 +2109,8 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   if (nc) {
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
     llist = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
-    k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, fs_long(), 1,
+    const uint32_t ml = fs_long(Rt);
+    k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, ml, 1,
                                                        llist, cnt + 3);
     k_fs_select_long<<<64, 1024, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, llist,
                                          cnt + 3, sel_i, sel_j, cnt + 1);
@@ -2112,7 +2120,7 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
     const int gb = grid_for((uint64_t)nc * G, 256, 16384);
 #define FS_SEL(GG)                                                                        \
     k_fs_select<GG><<<gb, 256, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, cnt + 2, \
-                                       sel_i, sel_j, cnt + 1, fs_long())
+                                       sel_i, sel_j, cnt + 1, ml)
     switch (G) {
       case 4: FS_SEL(4); break;
       case 8: FS_SEL(8); break;

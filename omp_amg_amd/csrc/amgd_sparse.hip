@@ -693,21 +693,29 @@ __global__ void k_list_long(const uint64_t *ro, const uint32_t *list, uint32_t n
 extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
                                 const double *x, const uint32_t *list, const unsigned *nlist,
                                 uint32_t nmax, uint64_t max_entries, double *z);
-// Rows past SPMV_LONG entries (the orphan coarse point's column of find_support's R:
-// 10^4 - 10^5 entries) take the grid-wide exact scan (amgd_rt.hip k_seg_*) instead of
-// one lane / wave adding them one by one.
+// Outlier rows (the orphan coarse point's column of find_support's R: 10^4 - 10^5
+// entries among rows of ~10) take the grid-wide exact scan (amgd_rt.hip k_seg_*)
+// instead of one lane / wave adding them one by one while the rest of the chip idles.
+// By default a row is an outlier past max(SPMV_LONG, 16 x the matrix's mean row):
+// where every row is long (coarse levels of a 3D Poisson hierarchy, means of 10^3 -
+// 10^4) the lane kernels keep the whole chip busy and the per-row block walk of the
+// segmented scan would be far slower.  AMGD_MV_LONG / amgd_spmv_set_long (tests) force
+// an absolute threshold (0: never).
 #define SPMV_LONG 4096
-static int64_t g_mv_long = -1;    // AMGD_MV_LONG: long-row threshold of the listed products
+static int64_t g_mv_long = -1;    // -1: environment or automatic, -2: automatic
 extern "C" void amgd_spmv_set_long(int64_t n) { g_mv_long = n; }
-static uint32_t mv_long() {
-  if (g_mv_long < 0) g_mv_long = sl_env("AMGD_MV_LONG", SPMV_LONG);
-  return g_mv_long == 0 ? 0xffffffffu : (uint32_t)g_mv_long;
+static uint32_t mv_long(const dcsr *M) {
+  if (g_mv_long == -1) g_mv_long = sl_env("AMGD_MV_LONG", -2);
+  if (g_mv_long == 0) return 0xffffffffu;
+  if (g_mv_long > 0) return (uint32_t)g_mv_long;
+  const uint64_t mean = M->rn ? M->nnz / M->rn : 0;
+  return (uint32_t)std::min<uint64_t>(0xfffffffeu, std::max<uint64_t>(SPMV_LONG, 16 * mean));
 }
 extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x,
                                double *z) {
   if (!n) return;
-  const uint32_t ml = mv_long();
-  if (ml != 0xffffffffu) {
+  const uint32_t ml = mv_long(M);
+  if (ml != 0xffffffffu && M->nnz > ml) {
     uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 16);
     unsigned *cnt = (unsigned *)(ll + n);
     amgd_memset(cnt, 0, 4);
@@ -749,6 +757,58 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
           (unsigned long)M->nnz, k, x ? 1 : 0, ms,
           (12.0 * M->nnz + 16.0 * M->rn + (x ? 8.0 * M->nnz : 0.0)) / (ms * 1e6));
 }
+// Multi-GPU: a whole-matrix long-row product of >= MV_SHARD_MIN entries is split into
+// contiguous row ranges of equal nnz (the row offsets are the work prefix); each rank
+// runs the lane kernel on its rows (same per-row ordered sums, so the same bits) and
+// one in-place allgatherv of z (8 B per row, >= 32 entries per row were read for it)
+// completes the vector on every rank.  find_support's sweeps re-multiply the same
+// pattern hundreds of times (removed entries are zeroed in place), so the split of a
+// (row offsets, rows, nnz) triple is cached: no host sync beyond the allgatherv.  A
+// stale entry (arena address reuse) still partitions [0, rn) identically on every
+// rank -- only the balance could suffer.
+#define MV_SHARD_MIN (1ull << 24)
+struct MvSplit { const uint64_t *ro; uint32_t rn; uint64_t nnz; std::vector<uint32_t> split; std::vector<uint64_t> pre; };
+static std::vector<MvSplit> g_mv_split;
+static uint64_t g_mv_shard_calls = 0;
+extern "C" uint64_t amgd_spmv_shard_calls(void) { return g_mv_shard_calls; }   // (test API)
+static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alpha, const double *y,
+                         double beta, const uint8_t *f) {
+  const int N = amgd_nshards();
+  if (N <= 1 || M0->rn < 64u * (uint32_t)N || !amgd_shard_worth(M0->nnz, MV_SHARD_MIN)) return false;
+  const MvSplit *sp = nullptr;
+  for (const MvSplit &e : g_mv_split)
+    if (e.ro == M0->ro && e.rn == M0->rn && e.nnz == M0->nnz && (int)e.split.size() == N + 1) sp = &e;
+  if (!sp) {
+    MvSplit e{M0->ro, M0->rn, M0->nnz, std::vector<uint32_t>(N + 1), std::vector<uint64_t>(N + 1)};
+    amgd_shard_split(M0->ro, M0->rn, e.split.data());
+    amgd_gather_u64_at(M0->ro, e.split.data(), N + 1, e.pre.data());
+    if (g_mv_split.size() >= 16) g_mv_split.erase(g_mv_split.begin());
+    g_mv_split.push_back(std::move(e));
+    sp = &g_mv_split.back();
+  }
+  g_mv_shard_calls++;
+  int fs, ls;
+  amgd_my_shards(&fs, &ls);
+  amgd_timer_start(1);
+  for (int q = fs; q < ls; q++) {
+    const uint32_t r0 = sp->split[q], n = sp->split[q + 1] - r0;
+    if (!n) continue;
+    dcsr Ms = *M0;
+    Ms.ro = M0->ro + r0;                       // absolute offsets: rows r0 .. r0+n
+    const dcsr *M = &Ms;
+    LANE_LAUNCH(false, n, (const uint32_t *)nullptr, x, z + r0, alpha, y ? y + r0 : nullptr, beta,
+                f ? f + r0 : nullptr, 0xffffffffu);
+    g_mv_bytes += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8 * (sp->pre[q + 1] - sp->pre[q]) : 0) +
+                  16ull * n + 8 + (y && alpha != 0.0 ? 8ull * n : 0) + (f ? (uint64_t)n : 0);
+  }
+  amgd_timer_stop(1);
+  KCHECK();
+  std::vector<uint64_t> off(N + 1);
+  for (int s = 0; s <= N; s++) off[s] = 8ull * sp->split[s];
+  void *b = z;
+  amgd_allgatherv(1, &b, off.data());
+  return true;
+}
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                       double beta, const uint8_t *f) {
   if (M->rn == 0) return;
@@ -760,6 +820,7 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
     KCHECK();
     return;
   }
+  if (M->nnz >= 32ull * M->rn && spmv_sharded(M, x, z, alpha, y, beta, f)) return;
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     amgd_timer_start(1);                       // roofline: whole-matrix long-row products

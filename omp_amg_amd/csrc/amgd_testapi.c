@@ -171,6 +171,10 @@ API void amgd_test_qf_stats(uint64_t *out) {
   out[2] = st[2];
 }
 
+/* whole-matrix SpMVs that ran row-sharded (multi-GPU) since the library loaded */
+extern uint64_t amgd_spmv_shard_calls(void);
+API uint64_t amgd_test_spmv_shard_calls(void) { return amgd_spmv_shard_calls(); }
+
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */
 extern void amgd_qapply_set_huge(int n);
 API void amgd_test_qa_huge(int n) { amgd_qapply_set_huge(n); }

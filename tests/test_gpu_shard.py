@@ -105,6 +105,60 @@ def test_sim_sharded_spgemm_kernel(sim):
     assert np.array_equal(X1.a.view(np.uint64), X3.a.view(np.uint64))
 
 
+@pytest.mark.parametrize("n", [2, 3, 7])
+def test_sim_sharded_spmv_kernel(sim, n):
+    """whole-matrix long-row SpMV split by nnz over n shards (lane kernel on each row
+    range, allgatherv of z) vs one GPU, bit for bit: ragged rows (empty, short, one of
+    5000 entries), plain / y-scaled / row-sum forms"""
+    rng = np.random.default_rng(11 + n)
+    rn, cn = 3000, 2500
+    lens = rng.integers(0, 80, size=rn)
+    lens[::97] = 0
+    lens[1234] = 2400
+    lens[2999] = 2500
+    ro = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    col = np.concatenate([np.sort(rng.choice(cn, size=l, replace=False)) for l in lens]).astype(np.uint32)
+    a = rng.standard_normal(int(ro[-1])) * np.exp2(rng.integers(-30, 30, size=int(ro[-1])))
+    A = abi.Csr(rn, cn, ro, col, a)
+    x = rng.standard_normal(cn)
+    y = rng.standard_normal(rn)
+    oa.spmv_sl_min(0)
+    try:
+        z1 = oa.test_spmv(A, x)
+        zy1 = oa.test_spmv(A, x, alpha=0.5, y=y, beta=-2.0)
+        zs1 = oa.test_spmv_f(A)
+        c0 = oa.lib().amgd_test_spmv_shard_calls()
+        sim(n)
+        z = oa.test_spmv(A, x)
+        zy = oa.test_spmv(A, x, alpha=0.5, y=y, beta=-2.0)
+        zs = oa.test_spmv_f(A)
+        assert oa.lib().amgd_test_spmv_shard_calls() - c0 == 3
+    finally:
+        oa.spmv_sl_min(-1)
+    for u, v in ((z1, z), (zy1, zy), (zs1, zs)):
+        assert np.array_equal(u.view(np.uint64), v.view(np.uint64))
+
+
+@pytest.mark.parametrize("gen", [("sem_e4_N3", lambda: problems.sem_laplacian(4, 4, 3, 3, seed=3, jitter=0.2)),
+                                 ("p27_20", lambda: problems.poisson3d(20, 27))],
+                         ids=lambda g: g[0])
+def test_sim_sharded_spmv_setup(sim, gen):
+    """full setup with every long-row whole-matrix SpMV sharded (lane kernel forced at
+    every size, min work 0) vs one GPU: the hierarchy is bit-identical"""
+    Ai, Aj, Av = gen[1]()
+    oa.spmv_sl_min(0)
+    try:
+        h1 = abi.run_setup(oa.lib(), Ai, Aj, Av)
+        c0 = oa.lib().amgd_test_spmv_shard_calls()
+        sim(4)
+        h4 = abi.run_setup(oa.lib(), Ai, Aj, Av)
+        assert oa.lib().amgd_test_spmv_shard_calls() > c0
+    finally:
+        oa.spmv_sl_min(-1)
+    bad = parity.compare(h1, h4, exact=True)
+    assert not bad, bad
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
