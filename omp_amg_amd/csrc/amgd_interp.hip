@@ -1296,6 +1296,78 @@ __global__ __launch_bounds__(NT) void k_qapply(const uint32_t *rows, uint32_t nr
     __syncthreads();
   }
 }
+// Small supports (nz <= SEG: most coarse points of the fine levels) take SEG lanes each,
+// 256 / SEG supports per work-group, synchronised per wavefront: a 64-lane group per
+// support left most lanes idle and paid three block barriers per support.  Same sums in
+// the same order as k_qapply.
+template <int SEG>
+__global__ __launch_bounds__(256) void k_qapply_small(const uint32_t *rows, uint32_t nrows,
+                                                      const uint64_t *wro, const uint32_t *wcol,
+                                                      const double *Q, const uint64_t *qoff,
+                                                      const uint64_t *bro, const uint32_t *bcol,
+                                                      const double *ba, const double *u,
+                                                      const double *lambda, double *out) {
+  constexpr int G = 256 / SEG;
+  __shared__ double s1[G][SEG], s2[G][SEG];
+  const int g = threadIdx.x / SEG, m = threadIdx.x % SEG;
+  for (uint64_t rb = (uint64_t)blockIdx.x * G; rb < nrows; rb += (uint64_t)gridDim.x * G) {
+    const uint64_t r = rb + g;
+    uint32_t c = 0, nz = 0;
+    uint64_t w0 = 0;
+    if (r < nrows) {
+      c = rows[r];
+      w0 = wro[c];
+      nz = (uint32_t)(wro[c + 1] - w0);
+    }
+    const bool act = (uint32_t)m < nz;
+    const double *Qc = act ? Q + qoff[c] : Q;
+    if (act) {
+      const uint32_t j = wcol[w0 + m];
+      s1[g][m] = row_lookup(bcol, ba, bro[c], bro[c + 1], j) + u[c] * lambda[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (act) {
+      const double *U = Qc + tri(m);
+      double v = 0;
+      for (int j = 0; j <= m; j++) v += U[j] * s1[g][j];
+      s2[g][m] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (act) {
+      double y = 0;
+      for (uint32_t j = m; j < nz; j++) y += Qc[tri(j) + m] * s2[g][j];
+      out[w0 + m] = y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+// supports of a list with nz <= lim appended to small, the rest to rest (cnt[0], cnt[1])
+// (nd: the list's length on the device, read instead of n)
+__global__ void k_split_small(const uint32_t *list, unsigned n, const unsigned *nd,
+                              const uint64_t *wro, uint32_t lim, uint32_t *small, uint32_t *rest,
+                              unsigned *cnt) {
+  if (nd) n = *nd;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t iters = (n + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {   // uniform trip count (wave_append)
+    const uint64_t r = c0 + it * stride;
+    const bool v = r < n;
+    const uint32_t c = v ? list[r] : 0;
+    const bool sm = v && wro[c + 1] - wro[c] <= lim;
+    const unsigned p = wave_append(&cnt[0], sm);
+    if (sm) small[p] = c;
+    const unsigned q = wave_append(&cnt[1], v && !sm);
+    if (v && !sm) rest[q] = c;
+  }
+}
+static int g_qa_small = -1;     // AMGD_QA_SMALL=0: every support <= 512 points on k_qapply<64>
 // Huge supports (> QA_HUGE points: the orphan support of min_skel's zero column) are
 // applied by three grid-wide kernels instead of one work-group: the same sums in the
 // same order, spread over the chip (one lane per row of U for sqv2, one lane per
@@ -1353,6 +1425,31 @@ static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, 
     amgd_free(scr);
     rs.nb = (unsigned)keep.size();
     if (rs.nb) amgd_h2d(rs.bl, keep.data(), (size_t)rs.nb * 4);
+  }
+  if (g_qa_small < 0) {
+    const char *e = getenv("AMGD_QA_SMALL");
+    g_qa_small = e && *e ? atoi(e) : 1;
+  }
+  if (rs.ns && g_qa_small) {        // <= 16 and 17..32 points: lane groups; the rest below
+    uint32_t *l16 = (uint32_t *)amgd_alloc(3ull * rs.ns * 4 + 16);
+    uint32_t *l32 = l16 + rs.ns, *lrest = l32 + rs.ns, *tmp = lrest;
+    unsigned *cnt = (unsigned *)amgd_alloc(32);
+    amgd_memset(cnt, 0, 32);
+    k_split_small<<<grid_for(rs.ns), 256, 0, s>>>(rs.sl, rs.ns, nullptr, Wt->ro, 16, l16, tmp, cnt);
+    k_split_small<<<grid_for(rs.ns), 256, 0, s>>>(tmp, rs.ns, cnt + 1, Wt->ro, 32, l32, rs.sl,
+                                                 cnt + 2);
+    unsigned h[4];
+    KCHECK();
+    amgd_d2h(h, cnt, 16);
+    if (h[0])
+      k_qapply_small<16><<<(int)std::min<uint64_t>((h[0] + 15) / 16, 65536), 256, 0, s>>>(
+          l16, h[0], Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col, Bt->a, u, lambda, out);
+    if (h[2])
+      k_qapply_small<32><<<(int)std::min<uint64_t>((h[2] + 7) / 8, 65536), 256, 0, s>>>(
+          l32, h[2], Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col, Bt->a, u, lambda, out);
+    rs.ns = h[3];
+    amgd_free(cnt);
+    amgd_free(l16);
   }
   if (rs.ns) {
     int g = (int)std::min<unsigned>(rs.ns, 65536u);

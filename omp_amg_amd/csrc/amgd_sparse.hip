@@ -247,13 +247,26 @@ __global__ void k_iota_u64(uint64_t *p, uint64_t n) { GRID_STRIDE(i, n) p[i] = i
 __global__ void k_iota_u32(uint32_t *p, uint64_t n) { GRID_STRIDE(i, n) p[i] = (uint32_t)i; }
 // P = u64 (perm handed back to the caller) or u32 (nnz < 2^32, perm internal:
 // a third less radix-sort traffic and a narrower perm read here)
+// (four entries per thread per step: their perm loads, then all eight gathers, in flight
+// together -- the gathers are the cost)
 template <typename P>
 __global__ void k_tr_fill(const P *perm, const uint32_t *row, const double *a, uint64_t nz,
                           uint32_t *tcol, double *ta) {
-  GRID_STRIDE(t, nz) {
-    const uint64_t p = perm[t];
-    tcol[t] = row[p];
-    ta[t] = a[p];
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t0 < nz; t0 += 4 * S) {
+    uint64_t p[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) p[u] = t0 + u * S < nz ? (uint64_t)perm[t0 + u * S] : 0;
+    uint32_t r[4];
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (t0 + u * S < nz) { r[u] = row[p[u]]; v[u] = a[p[u]]; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (t0 + u * S < nz) { tcol[t0 + u * S] = r[u]; ta[t0 + u * S] = v[u]; }
+    }
   }
 }
 // row offsets of the transpose from the sorted column keys: ro[c] = #keys < c, i.e.
@@ -334,10 +347,10 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
     if (long_rows(nz, A->rn)) k_row_of_entry_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
     else k_row_of_entry<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
     if (narrow)
-      k_tr_fill<uint32_t><<<grid_for(nz), 256, 0, s>>>((const uint32_t *)perm, row, A->a, nz,
+      k_tr_fill<uint32_t><<<grid_for((nz + 3) / 4, 256, 16384), 256, 0, s>>>((const uint32_t *)perm, row, A->a, nz,
                                                        T->col, T->a);
     else
-      k_tr_fill<uint64_t><<<grid_for(nz), 256, 0, s>>>((const uint64_t *)perm, row, A->a, nz,
+      k_tr_fill<uint64_t><<<grid_for((nz + 3) / 4, 256, 16384), 256, 0, s>>>((const uint64_t *)perm, row, A->a, nz,
                                                        T->col, T->a);
     KCHECK();
     amgd_free(row);
@@ -1951,7 +1964,9 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
   __shared__ uint32_t map[SW / 4];
   __shared__ uint64_t lbs[MAXL];
   __shared__ uint32_t lend[MAXL], lcur[MAXL];
+  __shared__ uint16_t lact[MAXL];
   __shared__ uint32_t s_min, s_max;
+  __shared__ unsigned s_nact;
   __shared__ unsigned long long s_tot;
   uint8_t *mb = (uint8_t *)map;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2004,18 +2019,47 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
         }
         __syncthreads();
       }
-      for (uint32_t e = wv; e < nc; e += NW) {
+      // the layers with a column in this window (one peek per layer, all threads at
+      // once), then one wavefront walk per active layer: a wide row's layers mostly
+      // miss most windows, and a dependent load per missed layer per window was the
+      // kernel's cost
+      if (t == 0) s_nact = 0;
+      __syncthreads();
+      for (uint32_t e0 = 0; e0 < nc; e0 += NT) {      // uniform trip count (wave_append)
+        const uint32_t e = e0 + t;
+        bool act = false;
+        if (e < nc) {
+          const uint32_t c = lcur[e];
+          act = c < lend[e] && bcol[lbs[e] + c] <= we;
+        }
+        const unsigned p = wave_append(&s_nact, act);
+        if (act) lact[p] = (uint16_t)e;
+      }
+      __syncthreads();
+      const uint32_t na = s_nact;
+      for (uint32_t q = wv; q < na; q += NW) {
+        const uint32_t e = lact[q];
         const uint64_t b0 = lbs[e];
         const uint32_t L = lend[e];
         uint32_t c = lcur[e];
         while (c < L) {
-          const uint32_t j = c + lane;
-          const uint32_t cc = j < L ? bcol[b0 + j] : 0xffffffffu;
-          const bool in = cc <= we;
-          if (in) mb[cc - wb] = 1;
-          const uint32_t n = (uint32_t)__popcll(__ballot(in));
+          // eight 64-column loads in flight per step (the layer is sorted: the in-window
+          // columns are a prefix; loads past it are wasted, not wrong)
+          uint32_t cc[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const uint32_t j = c + 64 * u + lane;
+            cc[u] = j < L ? bcol[b0 + j] : 0xffffffffu;
+          }
+          uint32_t n = 0;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const bool in = cc[u] <= we;
+            if (in) mb[cc[u] - wb] = 1;
+            n += (uint32_t)__popcll(__ballot(in));
+          }
           c += n;
-          if (n < 64) break;                 // the layer left the window (or ended)
+          if (n < 512) break;                // the layer left the window (or ended)
         }
         if (lane == 0) lcur[e] = c;
       }
