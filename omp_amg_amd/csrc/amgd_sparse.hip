@@ -1257,8 +1257,10 @@ __global__ void k_spgemm_ub(const uint64_t *aro, const uint32_t *acol, uint32_t 
 // bin takes the rest.  skip0: rows with v == 0 go nowhere.
 #define SG_MAXBIN 6
 struct SgBins { uint64_t lim[SG_MAXBIN]; };
+// sk (optional): rows with sk[i] <= sk_le are left out (the tiny rows of k_sg_tiny)
 __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int skip0,
-                           uint32_t *lists, unsigned *counts) {
+                           uint32_t *lists, unsigned *counts, const uint64_t *sk = nullptr,
+                           uint64_t sk_le = 0) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (rn + stride - 1) / stride;
@@ -1267,6 +1269,7 @@ __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int
     bool ok = i < rn;
     uint64_t x = ok ? v[i] : 0;
     if (skip0 && x == 0) ok = false;
+    if (ok && sk && sk[i] <= sk_le) ok = false;
     int bin = nb - 1;
     for (int q = nb - 2; q >= 0; q--)
       if (x <= b.lim[q]) bin = q;
@@ -1934,6 +1937,77 @@ extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
 extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; }
 extern "C" uint64_t amgd_spgemm_bytes(void) { return g_sg_bytes; }
 
+// Tiny rows (at most SG_TINY products: the fine levels' near-diagonal products, 10^6 -
+// 10^7 rows of 1-8 products) take one thread each, the row's distinct columns kept
+// sorted in registers (fixed-size arrays, every index compile-time): one work-group per
+// row spent most of its time clearing a 4096-slot LDS table.  Products are visited in
+// the hash kernels' order -- A entries ascending (the last of duplicate columns, as
+// everywhere), each B row ascending -- and every column's sum starts from +0.0 and adds
+// its products in that order: the same bits.  MODE 0 writes the distinct count, MODE 1
+// the nonzero sums in column order at xro[i] and their count.
+#define SG_TINY 32
+__global__ void k_tiny_list(const uint64_t *ub, uint32_t rn, uint32_t *list, unsigned *cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t iters = (rn + stride - 1) / stride;
+  for (uint64_t it = 0; it < iters; it++) {   // uniform trip count (wave_append)
+    const uint64_t i = i0 + it * stride;
+    const bool take = i < rn && ub[i] <= SG_TINY;
+    const unsigned p = wave_append(cnt, take);
+    if (take) list[p] = (uint32_t)i;
+  }
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_sg_tiny(const uint32_t *rows, uint32_t nrows,
+                                                 const uint64_t *aro, const uint32_t *acol,
+                                                 const double *aa, const uint64_t *bro,
+                                                 const uint32_t *bcol, const double *ba,
+                                                 uint64_t *cnt, const uint64_t *xro, uint32_t *xcol,
+                                                 double *xa) {
+  constexpr uint32_t T = SG_TINY, EMPTY = 0xffffffffu;
+  GRID_STRIDE(r, nrows) {
+    const uint32_t i = rows[r];
+    uint32_t K[T];
+    double V[T];
+#pragma unroll
+    for (uint32_t q = 0; q < T; q++) { K[q] = EMPTY; V[q] = 0.0; }
+    const uint64_t a0 = aro[i], a1 = aro[i + 1];
+    for (uint64_t ka = a0; ka < a1; ka++) {
+      const uint32_t k = acol[ka];
+      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
+      const double av = MODE ? aa[ka] : 0.0;
+      const uint64_t b1 = bro[k + 1];
+      for (uint64_t kb = bro[k]; kb < b1; kb++) {
+        const uint32_t j = bcol[kb];
+        const double p = MODE ? ba[kb] * av : 0.0;
+        bool found = false;
+#pragma unroll
+        for (uint32_t q = 0; q < T; q++)
+          if (K[q] == j) { if (MODE) V[q] = V[q] + p; found = true; }
+        if (!found) {                        // sorted insert (EMPTY sorts last)
+#pragma unroll
+          for (uint32_t q = T - 1; q > 0; q--) {
+            if (K[q - 1] > j) { K[q] = K[q - 1]; V[q] = V[q - 1]; }
+            else if (K[q] > j) { K[q] = j; V[q] = 0.0 + p; }
+          }
+          if (K[0] > j) { K[0] = j; V[0] = 0.0 + p; }
+        }
+      }
+    }
+    uint32_t n = 0;
+    if (MODE == 0) {
+#pragma unroll
+      for (uint32_t q = 0; q < T; q++) n += K[q] != EMPTY ? 1u : 0u;
+    } else {
+      const uint64_t ob = xro[i];
+#pragma unroll
+      for (uint32_t q = 0; q < T; q++)
+        if (K[q] != EMPTY && V[q] != 0.0) { xcol[ob + n] = K[q]; xa[ob + n] = V[q]; n++; }
+    }
+    cnt[i] = n;
+  }
+}
+
 // SGLOG: rows with >= 1024 outputs binned by column span (<=4K, 8K, 16K, 32K, 64K, more)
 __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn,
                             unsigned long long *h) {
@@ -2136,14 +2210,25 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   HIPCK(hipMemsetAsync(counts, 0, 64, s));
   HIPCK(hipMemsetAsync(cnt, 0, L * 8, s));
   unsigned hc[SG_MAXBIN] = {0};
+  // tiny rows (<= SG_TINY products): their own list (bin slot 5) and kernel, left out
+  // of every other bin (AMGD_SG_TINY=0: off)
+  static int tiny_on = -1;
+  if (tiny_on < 0) { const char *e = getenv("AMGD_SG_TINY"); tiny_on = e && *e ? atoi(e) : 1; }
+  uint32_t *tlist = lists + 5 * L;
+  const uint64_t *tsk = tiny_on ? ub : nullptr;
   if (rn) {
     k_spgemm_ub<<<grid_for(rn), 256, 0, s>>>(A->ro, A->col, rn, B->ro, ub);
     SgBins b;
     b.lim[0] = 2048;
-    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(ub, rn, b, 2, 0, lists, counts);
+    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(ub, rn, b, 2, 0, lists, counts, tsk, SG_TINY);
+    if (tiny_on) k_tiny_list<<<grid_for(rn), 256, 0, s>>>(ub, rn, tlist, counts + 5);
     KCHECK();
-    amgd_d2h(hc, counts, 8);
+    amgd_d2h(hc, counts, 24);
   }
+  const unsigned ntiny = hc[5];
+  if (ntiny)
+    k_sg_tiny<0><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
+                                                            B->col, B->a, cnt, nullptr, nullptr, nullptr);
   // symbolic: distinct count per row (row order in the lists is arbitrary; rows are independent)
   // long B rows (mean >= KSEQ_MIN): the k-sequential kernels; short ones: flat enumeration
   const uint64_t avgB = B->rn ? B->nnz / B->rn : 0;
@@ -2188,7 +2273,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     SgBins b;
     // (k-sequential kernels take the 8192-slot table up to 75% load)
     b.lim[0] = 256; b.lim[1] = 1024; b.lim[2] = 2048; b.lim[3] = kseq ? 6144 : 4096;
-    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(cnt, rn, b, 5, 1, lists, counts);
+    k_bin_rows<<<grid_for(rn), 256, 0, s>>>(cnt, rn, b, 5, 1, lists, counts, tsk, SG_TINY);
     KCHECK();
     amgd_d2h(hn, counts, 20);
   }
@@ -2221,6 +2306,9 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
   }
   const bool rap = g_sg_slot >= 0;
+  if (ntiny)
+    k_sg_tiny<1><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
+                                                            B->col, B->a, cnt2, cnt, tcol, ta);
   const int win = kseq ? sg_win() : 0;
   // wide bins (3: block hash, 4: dense slab) split into windowed / hash rows
   uint32_t *wlists = nullptr;
