@@ -156,7 +156,11 @@ extern "C" void *amgd_alloc(size_t bytes) {
     p = g_arena + off;
   } else {                                                        // arena full: the driver
     auto t0 = std::chrono::steady_clock::now();
-    HIPCK(hipMalloc(&p, sz));
+    if (hipMalloc(&p, sz) != hipSuccess) {
+      fprintf(stderr, "omp_amg_amd: out of HBM: request %.3f GB with %.3f GB live (peak %.3f GB, "
+              "arena %.3f GB)\n", sz / 1e9, g_inuse / 1e9, g_peak / 1e9, g_arena_sz / 1e9);
+      abort();
+    }
     g_tmalloc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     g_nmalloc++;
     g_bmalloc += (double)sz;

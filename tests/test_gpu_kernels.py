@@ -21,6 +21,32 @@ def test_spgemm_short_rows(seed):
     assert refops.same(X, refops.spgemm(A, B))
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_spgemm_tiny_rows(seed):
+    """rows of <= 32 products (k_sg_tiny, one thread per row, registers): duplicate A
+    columns (last one wins), exact cancellation to zero (dropped), -0.0 products
+    (the sum starts at +0.0), empty B rows, and rows just past the limit mixed in"""
+    rng = np.random.default_rng(seed)
+    rn, kn, cn = 2000, 300, 120
+    Bro, Bcol, Ba = [0], [], []
+    for k in range(kn):
+        L = int(rng.integers(0, 9))
+        c = np.sort(rng.choice(cn, size=L, replace=False))
+        v = rng.integers(-2, 3, size=L).astype(float)
+        v[v == 0] = -0.0
+        Bcol += c.tolist(); Ba += v.tolist(); Bro.append(len(Bcol))
+    Aro, Acol, Aa = [0], [], []
+    for i in range(rn):
+        L = int(rng.integers(0, 6 if i % 7 else 40))
+        c = np.sort(rng.integers(0, kn, size=L))          # repeats: duplicate columns
+        v = rng.integers(-2, 3, size=L).astype(float)
+        v[v == 0] = -0.0
+        Acol += c.tolist(); Aa += v.tolist(); Aro.append(len(Acol))
+    A = refops.Csr(rn, kn, np.array(Aro), np.array(Acol), np.array(Aa))
+    B = refops.Csr(kn, cn, np.array(Bro), np.array(Bcol), np.array(Ba))
+    assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
+
+
 def test_spgemm_long_rows_and_cancellation():
     rng = np.random.default_rng(7)
     A = refops.rand_csr(rng, 40, 600, 0.5, ints=True)          # > 1024 products per row

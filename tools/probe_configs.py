@@ -35,6 +35,8 @@ CONFIGS = {
                lambda: problems.sem_laplacian(22, 22, 21, 7)),
     "sem1k": ("SEM Laplacian, 10x10x10 hexes, N=7",
               lambda: problems.sem_laplacian(10, 10, 10, 7)),
+    "p27_64": ("3D 27-point Poisson 64^3", lambda: problems.poisson3d(64, 27)),
+    "p27_96": ("3D 27-point Poisson 96^3", lambda: problems.poisson3d(96, 27)),
     "p27_128": ("3D 27-point Poisson 128^3", lambda: problems.poisson3d(128, 27)),
     "p27_256": ("3D 27-point Poisson 256^3", lambda: problems.poisson3d(256, 27)),
 }
