@@ -81,6 +81,7 @@ int amgd_get_exact(void);
 double amgd_dot(const double *a, const double *b, uint64_t n);
 double amgd_norm2(const double *a, uint64_t n);
 double amgd_max_first(const double *a, uint64_t n, uint64_t *idx);  /* first argmax */
+double amgd_max_first2(const double *a, const double *b, uint64_t n, uint64_t *idx, double *maxb);
 uint64_t amgd_count_gt(const double *a, uint64_t n, double thr, double *maxv);
 double amgd_fro_minus_eye(const dcsr *A);                          /* ||A - I||_F^2 */
 

@@ -1875,7 +1875,7 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
   if (srn) {
     k_rowmax<<<grid_for(srn), 256, 0, s>>>(S->ro, S->col, srn, rmax);
     k_blockmax<<<grid_for(n64), 256, 0, s>>>(rmax, srn, 6, b64, n64);
-    k_blockmax<<<grid_for(n4k), 256, 0, s>>>(rmax, srn, 12, b4k, n4k);
+    k_blockmax<<<grid_for(n4k), 256, 0, s>>>(b64, n64, 6, b4k, n4k);   // max of the 64-row maxima
   }
   const uint64_t CH = std::max<uint64_t>(1, std::min<uint64_t>(hcoff[ce] - hcoff[cb], 1ull << 26));
   uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);

@@ -1144,6 +1144,27 @@ extern "C" double amgd_max_first(const double *a, uint64_t n, uint64_t *idx) {
   return g_red_h[0];
 }
 
+// the first argmax of a and the max of b (same length) with one host round trip
+extern "C" double amgd_max_first2(const double *a, const double *b, uint64_t n, uint64_t *idx,
+                                  double *maxb) {
+  if (n == 0) { if (idx) *idx = 0; *maxb = -DBL_MAX; return -DBL_MAX; }
+  int nb = red_grid(n);
+  double *p = red_buf();
+  uint64_t *pi = (uint64_t *)(p + RED_BLOCKS);
+  for (int q = 0; q < 2; q++) {          // partials reused in stream order
+    k_argmax_partial<<<nb, RED_THREADS, 0, amgd_s()>>>(q ? b : a, nullptr, n, p, pi);
+    k_argmax_partial<<<1, RED_THREADS, 0, amgd_s()>>>(p, pi, nb, p + 2 * RED_BLOCKS + 2 * q,
+                                                      (uint64_t *)(p + 2 * RED_BLOCKS + 2 * q + 1));
+  }
+  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 32, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  uint64_t gi;
+  memcpy(&gi, &g_red_h[1], 8);
+  if (idx) *idx = gi;
+  *maxb = g_red_h[2];
+  return g_red_h[0];
+}
+
 __global__ void k_count_gt(const double *a, uint64_t n, double thr, double *pc, double *pm) {
   double c = 0.0, m = 0.0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;

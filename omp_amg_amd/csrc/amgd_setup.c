@@ -190,7 +190,8 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
     /* w = (1./w1).*w2; mask1 = w > ctol^2; x1 = mask1.*g */
     amgd_cs_w_mask1(n, w1, w2, w, ctol * ctol, g, ma, x1, rows, 4);
     uint64_t mi = 0;
-    double w1m = amgd_max_first(w1, n, &mi), wm = amgd_max_first(w, n, NULL);
+    double wm = 0;
+    double w1m = amgd_max_first2(w1, w, n, &mi, &wm);    /* max(w1) (first index), max(w) */
     double b = (w1m < wm) ? sqrt(w1m) : sqrt(wm);
     if (b <= ctol) {
       uint32_t any = 0;

@@ -887,8 +887,29 @@ __global__ void k_diag(const uint64_t *ro, const uint32_t *col, const double *a,
     D[i] = d;
   }
 }
+// long rows (coarse levels, 10^2 - 10^4 entries): one wavefront per row, the first
+// entry with col == i found 64 entries at a time by ballot (same first match)
+__global__ void k_diag_wave(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
+                            double *D) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint64_t k1 = ro[i + 1];
+    double d = 0.0;
+    for (uint64_t k0 = ro[i]; k0 < k1; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      const unsigned long long m = __ballot(k < k1 && col[k] == (uint32_t)i);
+      if (m) { d = a[k0 + __ffsll((long long)m) - 1]; break; }
+    }
+    if (lane == 0) D[i] = d;
+  }
+}
 extern "C" void amgd_diag(const dcsr *A, double *D) {
-  if (A->rn) k_diag<<<grid_for(A->rn), 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, D);
+  if (A->rn && A->nnz >= 16ull * A->rn)
+    k_diag_wave<<<grid_for((uint64_t)A->rn * 64, 256, 16384), 256, 0, amgd_s()>>>(A->ro, A->col, A->a,
+                                                                                 A->rn, D);
+  else if (A->rn)
+    k_diag<<<grid_for(A->rn), 256, 0, amgd_s()>>>(A->ro, A->col, A->a, A->rn, D);
   KCHECK();
 }
 __global__ void k_diag_op(const uint64_t *ro, const uint32_t *col, double *a, uint32_t rn,
@@ -1196,6 +1217,68 @@ __global__ void k_pointwise(const uint64_t *aro, const uint32_t *acol, const dou
     if (!FILL) cnt[i] = c;
   }
 }
+// long rows (R0 .* W_skel on coarse levels: rows of 10^2 - 10^4 entries): one
+// wavefront per row.  When both rows are strictly increasing (checked first, by the
+// whole wave) the merge's output is the intersection in A's column order, so each
+// lane locates a 64-entry chunk of A's row in B's row by bisection and the matches
+// are placed by ballot prefix counts; otherwise lane 0 runs the sequential merge.
+template <bool FILL>
+__global__ void k_pointwise_wave(const uint64_t *aro, const uint32_t *acol, const double *aa,
+                                 const uint64_t *bro, const uint32_t *bcol, const double *ba,
+                                 uint32_t rn, uint64_t *cnt, const uint64_t *xro, uint32_t *xcol,
+                                 double *xa) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint64_t a0 = aro[i], a1 = aro[i + 1], b0 = bro[i], b1 = bro[i + 1];
+    bool mono = true;
+    for (uint64_t k = a0 + 1 + lane; k < a1; k += 64) mono = mono && acol[k] > acol[k - 1];
+    for (uint64_t k = b0 + 1 + lane; k < b1; k += 64) mono = mono && bcol[k] > bcol[k - 1];
+    mono = __ballot(!mono) == 0ull;
+    uint64_t o = FILL ? xro[i] : 0, c = 0;
+    if (!mono) {
+      if (lane == 0) {
+        uint64_t ja = a0, jb = b0;
+        while (ja < a1 && jb < b1) {
+          const uint32_t ca = acol[ja], cb = bcol[jb];
+          if (ca == cb) {
+            if (FILL) { xcol[o] = ca; xa[o] = aa[ja] * ba[jb]; o++; }
+            c++; ja++; jb++;
+          } else if (ca < cb) ja++;
+          else jb++;
+        }
+        if (!FILL) cnt[i] = c;
+      }
+      continue;
+    }
+    for (uint64_t k0 = a0; k0 < a1; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      bool hit = false;
+      uint64_t jb = 0;
+      if (k < a1 && b0 < b1) {
+        const uint32_t ca = acol[k];
+        uint64_t lo = b0, hi = b1;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (bcol[mid] < ca) lo = mid + 1;
+          else hi = mid;
+        }
+        hit = lo < b1 && bcol[lo] == ca;
+        jb = lo;
+      }
+      const unsigned long long m = __ballot(hit);
+      if (FILL && hit) {
+        const uint64_t q = o + __popcll(m & below);
+        xcol[q] = acol[k];
+        xa[q] = aa[k] * ba[jb];
+      }
+      o += __popcll(m);
+      c += __popcll(m);
+    }
+    if (!FILL && lane == 0) cnt[i] = c;
+  }
+}
 extern "C" dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B) {
   if (A->rn != B->rn || A->cn != B->cn) {
     fprintf(stderr, "omp_amg_amd: mxmpoint dimension mismatch\n");
@@ -1203,7 +1286,12 @@ extern "C" dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B) {
   }
   hipStream_t s = amgd_s();
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
-  if (A->rn)
+  const bool wave = A->nnz + B->nnz >= 32ull * A->rn;
+  const int gw = grid_for((uint64_t)A->rn * 64, 256, 16384);
+  if (A->rn && wave)
+    k_pointwise_wave<false><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn, cnt,
+                                               nullptr, nullptr, nullptr);
+  else if (A->rn)
     k_pointwise<false><<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a,
                                                         A->rn, cnt, nullptr, nullptr, nullptr);
   uint64_t nz = amgd_scan_u64(cnt, A->rn);
@@ -1211,7 +1299,10 @@ extern "C" dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B) {
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
   X->a = (double *)amgd_alloc(nz * 8 + 8);
-  if (A->rn)
+  if (A->rn && wave)
+    k_pointwise_wave<true><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn,
+                                              nullptr, X->ro, X->col, X->a);
+  else if (A->rn)
     k_pointwise<true><<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a,
                                                        A->rn, nullptr, X->ro, X->col, X->a);
   KCHECK();

@@ -182,6 +182,30 @@ def test_mpm_and_mxmpoint():
     assert refops.same(oa.test_csr_op(3, A, B), refops.mxmpoint(A, B))
 
 
+def test_mxmpoint_long_rows():
+    """wave-per-row pointwise product (mean row >= 32): bisection + ballot placement on
+    strictly increasing rows, lane 0's sequential merge on rows with a repeated or an
+    unsorted column (the merge's own pairing), empty rows on either side"""
+    rng = np.random.default_rng(17)
+    rn, cn = 300, 2000
+
+    def build(dens, tweak):
+        ro, cols, vals = [0], [], []
+        for i in range(rn):
+            c = np.sort(rng.choice(cn, size=0 if i in (5, 6) and tweak == "a" else
+                                   int(rng.binomial(cn, dens)), replace=False))
+            if i == 7 and tweak == "b" and len(c) > 3:
+                c[1] = c[0]                      # repeated column
+            if i == 9 and tweak == "a" and len(c) > 3:
+                c[0], c[1] = c[1], c[0]          # unsorted pair
+            cols += c.tolist(); vals += rng.standard_normal(len(c)).tolist(); ro.append(len(cols))
+        return refops.Csr(rn, cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+    A, B = build(0.05, "a"), build(0.06, "b")
+    assert A.row_off[-1] + B.row_off[-1] >= 32 * rn
+    assert refops.same(oa.test_csr_op(3, A, B), refops.mxmpoint(A, B))
+    assert refops.same(oa.test_csr_op(3, B, A), refops.mxmpoint(B, A))
+
+
 def test_spmv_ordered():
     rng = np.random.default_rng(11)
     A = refops.rand_csr(rng, 1000, 800, 0.01)
