@@ -1553,12 +1553,17 @@ __device__ uint32_t next_row_ge(const int64_t *rmax, const int64_t *b64, const i
 __global__ void k_rowmax(const uint64_t *ro, const uint32_t *col, uint32_t n, int64_t *rmax) {
   GRID_STRIDE(r, n) rmax[r] = ro[r + 1] > ro[r] ? (int64_t)col[ro[r + 1] - 1] : -1;
 }
-__global__ void k_blockmax(const int64_t *in, uint64_t n, int shift, int64_t *out, uint64_t nout) {
-  GRID_STRIDE(b, nout) {
+// 2^shift-row maxima, one wavefront per block of rows (coalesced)
+__global__ void k_blockmax_wave(const int64_t *in, uint64_t n, int shift, int64_t *out,
+                                uint64_t nout) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t b = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; b < nout;
+       b += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
     int64_t m = -1;
-    uint64_t s0 = b << shift, s1 = min(n, (b + 1) << shift);
-    for (uint64_t q = s0; q < s1; q++) m = in[q] > m ? in[q] : m;
-    out[b] = m;
+    const uint64_t s0 = b << shift, s1 = min(n, (b + 1) << shift);
+    for (uint64_t q = s0 + lane; q < s1; q += 64) m = in[q] > m ? in[q] : m;
+    for (int o = 32; o; o >>= 1) { const int64_t y = __shfl_xor(m, o, 64); m = y > m ? y : m; }
+    if (lane == 0) out[b] = m;
   }
 }
 __global__ void k_lmop_land(const uint32_t *erow, uint64_t e0, uint64_t e1, const uint64_t *wro,
@@ -1874,8 +1879,8 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
   int64_t *b64 = (int64_t *)amgd_alloc((n64 + 1) * 8), *b4k = (int64_t *)amgd_alloc((n4k + 1) * 8);
   if (srn) {
     k_rowmax<<<grid_for(srn), 256, 0, s>>>(S->ro, S->col, srn, rmax);
-    k_blockmax<<<grid_for(n64), 256, 0, s>>>(rmax, srn, 6, b64, n64);
-    k_blockmax<<<grid_for(n4k), 256, 0, s>>>(b64, n64, 6, b4k, n4k);   // max of the 64-row maxima
+    k_blockmax_wave<<<grid_for(n64 * 64, 256, 16384), 256, 0, s>>>(rmax, srn, 6, b64, n64);
+    k_blockmax_wave<<<grid_for(n4k * 64, 256, 16384), 256, 0, s>>>(rmax, srn, 12, b4k, n4k);
   }
   const uint64_t CH = std::max<uint64_t>(1, std::min<uint64_t>(hcoff[ce] - hcoff[cb], 1ull << 26));
   uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);
@@ -2371,10 +2376,13 @@ __global__ __launch_bounds__(256) void k_expand_pick_sort(const uint64_t *ro, co
       double V = tot * 0.5;
       uint32_t c = 0;
       if (V != 0.) {
+        // kv is sorted descending and >= 0, so the running sum -- and sum - V -- never
+        // decreases: the count stops at the first prefix with sum - V >= 0
         double sum = 0.0;
         for (uint32_t p = 0; p < L; p++) {
           if (kv[p] != 0.) sum += kv[p];
           if (sum - V < 0) c++;
+          else break;
         }
       }
       uint32_t N = c + 1;
