@@ -2312,9 +2312,10 @@ __global__ __launch_bounds__(64) void k_expand_pick(const uint64_t *ro, const ui
       uint32_t c = 0;
       if (V != 0.) {
         double s = 0.0;
-        for (uint32_t p = 0; p < L; p++) {
+        for (uint32_t p = 0; p < L; p++) {      // (monotone: see k_expand_pick_sort)
           if (sval[r0 + p] != 0.) s += sval[r0 + p];
           if (s - V < 0) c++;
+          else break;
         }
       }
       uint32_t N = c + 1;

@@ -560,7 +560,12 @@ extern "C" void amgd_spmv_set_sl_min(int64_t n) { g_sl_forced = n < 0 ? -1 : n; 
 // 1024 / RW entries of each row, 16 per lane, lane L's q-th load taking flat entry
 // q*64 + L of the round (row = that / SEG): every load instruction covers whole row
 // segments of >= 128 B.
-template <bool LIST, int RW>
+template <bool NTL, typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool LIST, int RW, bool NTL = false>
 __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
@@ -601,7 +606,7 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
       v[q] = 0.0;
       if ((uint32_t)sub < rlen[w][rr]) {
         const uint64_t k = rk0[w][rr] + sub;
-        v[q] = x ? a[k] * x[col[k]] : a[k];
+        v[q] = x ? ld_stream<NTL>(a + k) * x[ld_stream<NTL>(col + k)] : ld_stream<NTL>(a + k);
       }
     }
     for (uint32_t off = 0; off < mx; off += SEG) {
@@ -625,8 +630,8 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
         cn[q] = 0;
         if (hv[q]) {
           const uint64_t k = rk0[w][rr] + en;
-          an[q] = a[k];
-          if (x) cn[q] = col[k];
+          an[q] = ld_stream<NTL>(a + k);
+          if (x) cn[q] = ld_stream<NTL>(col + k);
         }
       }
       if (lane < RW && off < len) {
@@ -666,19 +671,32 @@ static int lane_rw(uint64_t n) {
   if (g_rw_forced == 4 || g_rw_forced == 16 || g_rw_forced == 64) return (int)g_rw_forced;
   return n >= (1u << 22) ? 64 : n >= (1u << 16) ? 16 : 4;
 }
+// AMGD_SPMV_NT=1: the matrix stream (columns, values) read with nontemporal loads
+static int spmv_nt() {
+  static int v = -1;
+  if (v < 0) { const char *e = getenv("AMGD_SPMV_NT"); v = e && *e ? atoi(e) : 0; }
+  return v;
+}
+#define LANE_LAUNCH_NT(LIST, NTL, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_)              \
+  do {                                                                                        \
+    if (rw_ == 64)                                                                            \
+      k_spmv_lane<LIST, 64, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
+                                                            z_, al, y_, be, f_, ml_);         \
+    else if (rw_ == 16)                                                                       \
+      k_spmv_lane<LIST, 16, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
+                                                            z_, al, y_, be, f_, ml_);         \
+    else                                                                                      \
+      k_spmv_lane<LIST, 4, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
+                                                           z_, al, y_, be, f_, ml_);          \
+  } while (0)
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
     const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
-    if (rw_ == 64)                                                                            \
-      k_spmv_lane<LIST, 64><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
-                                                       al, y_, be, f_, ml_);                  \
-    else if (rw_ == 16)                                                                       \
-      k_spmv_lane<LIST, 16><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,  \
-                                                       al, y_, be, f_, ml_);                  \
+    if (spmv_nt())                                                                            \
+      LANE_LAUNCH_NT(LIST, true, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
     else                                                                                      \
-      k_spmv_lane<LIST, 4><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, z_,   \
-                                                      al, y_, be, f_, ml_);                   \
+      LANE_LAUNCH_NT(LIST, false, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);           \
   } while (0)
 // ordered sums (x == nullptr) or products of the listed rows only (rows longer than
 // maxlen are skipped: k_rows_exact does them)
