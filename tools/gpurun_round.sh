@@ -6,9 +6,11 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export PYTHONPATH=$PWD
 TAG=${1:-r02}
+if [ -z "$SKIP_TESTS" ]; then   # SKIP_TESTS=1: the suite already ran green on this tree
 timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/gputests_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/gputests_$TAG.log
 [ $rc -eq 0 ] || exit $rc
+fi
 t0=$(date +%s)
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo bench failed; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 echo "bench wall $(( $(date +%s) - t0 )) s"
