@@ -34,6 +34,7 @@ int amgd_rt_init(int device);            /* idempotent; 0 on success */
 const char *amgd_last_error(void);
 void *amgd_alloc(size_t bytes);          /* caching pool; aborts loudly on OOM */
 void amgd_free(void *p);
+void amgd_spmv_split_forget(const void *ro);   /* drop cached SpMV shard splits of a freed buffer */
 void amgd_rt_shutdown(void);             /* free everything; pointers become invalid */
 void amgd_pool_release(void);            /* return every cached block to the driver */
 size_t amgd_pool_bytes_in_use(void);

@@ -174,6 +174,7 @@ extern "C" void *amgd_alloc(size_t bytes) {
 
 extern "C" void amgd_free(void *p) {
   if (!p) return;
+  amgd_spmv_split_forget(p);
   auto it = g_used.find(p);
   if (it == g_used.end()) {
     fprintf(stderr, "omp_amg_amd: amgd_free of unknown pointer %p\n", p);

@@ -794,12 +794,21 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
 // one in-place allgatherv of z (8 B per row, >= 32 entries per row were read for it)
 // completes the vector on every rank.  find_support's sweeps re-multiply the same
 // pattern hundreds of times (removed entries are zeroed in place), so the split of a
-// (row offsets, rows, nnz) triple is cached: no host sync beyond the allgatherv.  A
-// stale entry (arena address reuse) still partitions [0, rn) identically on every
-// rank -- only the balance could suffer.
+// (row offsets, rows, nnz) triple is cached: no host sync beyond the allgatherv.  An
+// entry is dropped when its row-offset buffer is freed (amgd_free), so a hit is always
+// the same live matrix: every rank, running the same sequence of matrices, hits and
+// misses alike and uses the same split (each rank's arena addresses differ, so a
+// stale address match could otherwise differ between ranks and mismatch the
+// allgatherv ranges).
 #define MV_SHARD_MIN (1ull << 24)
 struct MvSplit { const uint64_t *ro; uint32_t rn; uint64_t nnz; std::vector<uint32_t> split; std::vector<uint64_t> pre; };
 static std::vector<MvSplit> g_mv_split;
+void amgd_spmv_split_forget(const void *ro) {
+  if (g_mv_split.empty()) return;
+  for (size_t q = 0; q < g_mv_split.size();)
+    if ((const void *)g_mv_split[q].ro == ro) g_mv_split.erase(g_mv_split.begin() + q);
+    else q++;
+}
 static uint64_t g_mv_shard_calls = 0;
 extern "C" uint64_t amgd_spmv_shard_calls(void) { return g_mv_shard_calls; }   // (test API)
 static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alpha, const double *y,
