@@ -15,8 +15,9 @@ value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup
           max time, scaling "weak").
 roofline: the dominant kernel by time, the long-row SpMV (k_spmv_lane<false,RW>,
           whole-matrix products: find_support's sweeps, PCG, Lanczos), event-timed
-          live on the library stream; algorithmic bytes = 12 B per entry + 8 B
-          x gather per entry + 16 B per row.
+          live on the library stream; algorithmic bytes = 12 B per entry + 8 B per
+          column (x read once) + 16 B per row; the rate with x gathered
+          once per entry and the PMC-measured HBM rate are reported beside it.
 rap_roofline: the Galerkin RAP SpGEMM numeric kernels (A_{l+1} = W'AfP + A_cf W + A_cc
           and AfP = Af W; instantiated with RAP=1 so rocprof lists them apart;
           k_sg_kseq for long B-operand rows, k_sg_row for short ones, k_sg_win
@@ -126,16 +127,36 @@ def cpu_baseline(m, reps, budget_s):
                       f"O(rows^2) and it does not terminate on many larger grids, so 256^3 is out of its reach)"}
 
 
-def pmc_traffic():
+def gpu_sample(m, reps=5):
+    """the GPU setup on the CPU baseline's own sample (7-point m^3), so the line holds a
+    same-size ratio: rows/s over `reps` device-resident setups after one warm-up"""
+    import omp_amg_amd as oa
+    from omp_amg_amd import problems
+    Ai, Aj, Av = problems.poisson3d(m, 7)
+    ds = oa.DeviceSetup(Ai, Aj, Av)
+    ds.run()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ds.run()
+    dt = time.perf_counter() - t0
+    ds.close()
+    return {"value": m ** 3 * reps / dt, "unit": "rows/s", "secs_per_setup": dt / reps,
+            "sample": f"3D 7-point Poisson {m}^3, {reps} device-resident setups on 1 MI355X"}
+
+
+def pmc_traffic(m, stencil, world):
     """HBM bytes per setup of the two roofline kernels from the committed rocprofv3
     PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass, gfx950 correction;
-    tools/gpurun_round.sh) on this same workload: (spmv, rap, source) or Nones"""
+    tools/gpurun_round.sh), only when they were measured on this same workload (grid,
+    stencil, one GPU): (spmv, rap, source) or Nones"""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_r*.json")))
-    if not files:
-        return None, None, None
-    d = json.load(open(files[-1]))
-    return d["spmv"]["hbm_bytes"], d["rap"]["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+    for f in reversed(files):
+        d = json.load(open(f))
+        w = d.get("workload", {"m": 256, "stencil": 7, "world": 1})   # r02 files: 256^3 7-point, 1 GPU
+        if (w["m"], w["stencil"], w["world"]) == (m, stencil, world):
+            return d["spmv"]["hbm_bytes"], d["rap"]["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None, None, None
 
 
 def heartbeat(period=30.0):
@@ -223,7 +244,7 @@ def main():
         t_step = time.perf_counter() - t1
         warm += 1
     barrier()
-    rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, st = 0.0, 0, 0, 0.0, 0, None
+    rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, mv_strict, st = 0.0, 0, 0, 0.0, 0, 0, None
     steps = 0
     if sharded:
         shard.stats(reset=True)
@@ -240,6 +261,7 @@ def main():
         rap_nnz += st["rap_out_nnz"]
         mv_ms += st["spmv_kernel_ms"]
         mv_bytes += st["spmv_bytes"]
+        mv_strict += st["spmv_bytes_strict"]
         if rank == 0:
             print(f"[bench] step {steps}: {t_step:.2f} s", file=sys.stderr, flush=True)
     barrier()
@@ -255,13 +277,15 @@ def main():
     comm = shard.stats() if sharded else None
 
     if rank == 0:
-        t_mv, t_rap, t_src = pmc_traffic()
+        t_mv, t_rap, t_src = pmc_traffic(args.m, args.stencil, world)
         if args.traffic is not None:
             t_mv, t_src = args.traffic, "--traffic"
         if args.rap_traffic is not None:
             t_rap = args.rap_traffic
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
-        mv_achieved = mv_bytes / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
+        mv_achieved = mv_strict / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
+        mv_gather = mv_bytes / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
+        mv_pmc = t_mv * steps / (mv_ms * 1e-3) / 1e9 if (mv_ms > 0 and t_mv) else None
         out = {
             "metric": "AMG setup rows/sec + RAP SpGEMM nnz/sec at 1/2/4/8 MI355X",
             "value": value,
@@ -297,8 +321,16 @@ def main():
                          "kernel": "k_spmv_lane<false,RW>: whole-matrix long-row SpMV (ordered row sums; "
                                    "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
                                    "HIP-event timed",
-                         "algorithmic_bytes_per_setup": mv_bytes / steps,
-                         "kernel_ms_per_setup": mv_ms / steps},
+                         "algorithmic_bytes_per_setup": mv_strict / steps,
+                         "algorithmic_bytes_def": "12 B per entry (u32 col + f64 a) + 8 B per column (x once) "
+                                                  "+ 16 B per row (row offsets, z)",
+                         "kernel_ms_per_setup": mv_ms / steps,
+                         "pmc_rate_gbs": mv_pmc,
+                         "pmc_frac": mv_pmc / HBM_PEAK_GBS if mv_pmc else None,
+                         "pmc_over_algorithmic": t_mv * steps / mv_strict if (t_mv and mv_strict) else None,
+                         "extra_per_entry_gather": {"bytes_per_setup": mv_bytes / steps, "achieved": mv_gather,
+                                                    "note": "x gathered once per entry (8 B/entry): an upper "
+                                                            "bound on gather traffic, not the roofline"}},
             "rap_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": t_rap,
@@ -315,6 +347,8 @@ def main():
                                           "bytes": comm["bytes"] / steps, "ms": comm["ms"] / steps}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.cpu_m, args.cpu_reps, args.cpu_budget_s)
+            if out["cpu_baseline"] is not None:
+                out["cpu_baseline"]["gpu_same_sample"] = gpu_sample(args.cpu_m)
         print(json.dumps(out), flush=True)
     ds.close()
     if sharded:

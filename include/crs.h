@@ -9,7 +9,12 @@
  *   they print a diagnostic and abort.
  *
  * `struct comm` is gslib's (comm.h:85-88) for a non-MPI build: {uint id, np; int c}.
- * Only np == 1 is accepted by crs_setup today (DESIGN.md "Multi-GPU").
+ * np > 1: rank comm->id passes its local rows; the library's own communicator
+ * (omp_amg_amd.h amgd_comm_init_rccl / _host, same rank and size) gathers the
+ * assembled matrix and runs the row-sharded setup (DESIGN.md "Multi-GPU").
+ * On failure (communicator mismatch, out of HBM) crs_setup returns NULL and
+ * amgd_error() holds the reason; the reference exits the process instead.
+ * amgd_crs_export (omp_amg_amd.h) copies the kept hierarchy out.
  */
 #ifndef OMP_AMG_AMD_CRS_H
 #define OMP_AMG_AMD_CRS_H

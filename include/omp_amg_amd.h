@@ -32,7 +32,8 @@ typedef struct {
   uint32_t nlevels, ub_events;   /* ub_events: inputs outside the reference's defined domain */
   size_t peak_bytes;
   double spmv_kernel_ms;         /* whole-matrix long-row SpMV kernels (k_spmv_lane), event-timed */
-  uint64_t spmv_bytes;           /* their algorithmic HBM bytes */
+  uint64_t spmv_bytes;           /* their bytes with x gathered once per entry */
+  uint64_t spmv_bytes_strict;    /* their algorithmic HBM bytes: x read once per product */
 } amgd_stats;
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */
@@ -51,6 +52,10 @@ int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj, con
 int amgd_hier_export(const amgd_hier *h, struct amg_setup_data *data);  /* D2H into the ABI struct */
 void amgd_hier_free(amgd_hier **h);
 void amgd_get_stats(amgd_stats *st);
+/* the hierarchy crs_setup (crs.h) keeps in HBM, copied into the ABI struct -- the same
+   layout amg_setup fills; free with free_data */
+struct crs_data;
+int amgd_crs_export(const struct crs_data *crs, struct amg_setup_data *data);
 /* ---- multi-GPU: row-sharded setup over the GPUs of one node (DESIGN.md "Multi-GPU") ----
    Every rank calls amgd_setup_device on the same matrix; the row-independent heavy
    kernels (SpGEMMs, Q factors) are split by work across the ranks and completed by

@@ -36,7 +36,7 @@ class AmgdStats(C.Structure):
                 ("rows0", C.c_uint64), ("nnz0", C.c_uint64),
                 ("nlevels", C.c_uint32), ("ub_events", C.c_uint32),
                 ("peak_bytes", C.c_size_t), ("spmv_kernel_ms", C.c_double),
-                ("spmv_bytes", C.c_uint64)]
+                ("spmv_bytes", C.c_uint64), ("spmv_bytes_strict", C.c_uint64)]
 
 
 class HCsr(C.Structure):
@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
+        L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
@@ -351,6 +352,19 @@ def qf_stats() -> dict:
     out = (C.c_uint64 * 3)()
     lib().amgd_test_qf_stats(out)
     return {"sparse": int(out[0]), "fallback": int(out[1]), "split": int(out[2])}
+
+
+ROUTES = ("spmv_lane", "mv_long", "sg_tiny", "sg_kseq", "sg_win", "sg_wsym", "sg_long",
+          "cs_inc", "fs_inc", "sg_row")
+
+
+def route_stats(reset: bool = True) -> dict:
+    """how often each default kernel route ran since the last reset (amgd.h AMGD_R_*):
+    lane SpMV, outlier-row SpMV, tiny / k-sequential / windowed / wide-symbolic /
+    dense-slab / flat SpGEMM, incremental coarsening and find_support sweeps"""
+    out = (C.c_uint64 * 16)()
+    lib().amgd_test_route_stats(out, int(reset))
+    return {k: int(out[i]) for i, k in enumerate(ROUTES)}
 
 
 def lmop_stats(reset: bool = True) -> dict:

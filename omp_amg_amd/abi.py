@@ -115,6 +115,8 @@ def read_csr(p) -> Csr:
 def read_setup_data(d: AmgSetupData) -> Hierarchy:
     """Copy every per-level array out of a filled `struct amg_setup_data`."""
     nl = int(d.nlevels)
+    if nl == 0:                       # failed setup (omp_amg_amd: out of HBM): empty data
+        return Hierarchy(0, 0, float(d.tolc), float(d.gamma), np.zeros(0, dtype=np.int64))
     n0 = int(d.n[0])
     h = Hierarchy(nl, int(d.nullspace), float(d.tolc), float(d.gamma),
                   _arr(d.id, n0, np.int64))
@@ -163,6 +165,59 @@ def srand(seed: int = 1) -> None:
     """Reset libc's rand() stream; the reference's Lanczos start vector is
     rand()/RAND_MAX (amg_setup.c:2447), so every parity run starts from seed 1."""
     C.CDLL(None).srand(C.c_uint(seed))
+
+
+class Comm(C.Structure):
+    # gslib comm.h:85-88 (non-MPI build), include/crs.h
+    _fields_ = [("id", amg_uint), ("np", amg_uint), ("c", C.c_int)]
+
+
+def bind_crs(lib: C.CDLL) -> C.CDLL:
+    """crs.h (reference crs.h:15-20) + the export hook of omp_amg_amd.h"""
+    lib.crs_setup.argtypes = [amg_uint, C.POINTER(C.c_ulong), amg_uint, C.POINTER(amg_uint),
+                              C.POINTER(amg_uint), C.POINTER(C.c_double), amg_uint, C.POINTER(Comm)]
+    lib.crs_setup.restype = C.c_void_p
+    lib.crs_free.argtypes = [C.c_void_p]
+    lib.crs_free.restype = None
+    lib.amgd_crs_export.argtypes = [C.c_void_p, C.POINTER(AmgSetupData)]
+    lib.amgd_crs_export.restype = C.c_int
+    return lib
+
+
+def crs_setup(lib: C.CDLL, n: int, ids, Ai, Aj, Av, null_space: int = 0, rank: int = 0,
+              np_: int = 1, *, seed: int = 1, quiet: bool = True):
+    """crs_setup(n, id, nz, Ai, Aj, A, null_space, comm) of crs.h on a local matrix
+    (local indices Ai/Aj < n, global ids `ids`, 1-based, 0 = not a dof); returns the
+    opaque handle (None where the library returned NULL)"""
+    bind_crs(lib)
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    Ai = np.ascontiguousarray(Ai, dtype=np.uint64)
+    Aj = np.ascontiguousarray(Aj, dtype=np.uint64)
+    Av = np.ascontiguousarray(Av, dtype=np.float64)
+    comm = Comm(rank, np_, 0)
+    srand(seed)
+    with quiet_stdout(quiet):
+        h = lib.crs_setup(n, ids.ctypes.data_as(C.POINTER(C.c_ulong)), len(Av),
+                          Ai.ctypes.data_as(C.POINTER(amg_uint)), Aj.ctypes.data_as(C.POINTER(amg_uint)),
+                          Av.ctypes.data_as(C.POINTER(C.c_double)), null_space, C.byref(comm))
+    return h or None
+
+
+def crs_export(lib: C.CDLL, handle) -> Hierarchy:
+    """the hierarchy crs_setup keeps in HBM (amgd_crs_export), as a host copy"""
+    bind_crs(lib)
+    bind_setup(lib)
+    libc = C.CDLL(None)
+    libc.malloc.restype = C.c_void_p
+    libc.malloc.argtypes = [C.c_size_t]
+    raw = libc.malloc(C.sizeof(AmgSetupData))
+    C.memset(raw, 0, C.sizeof(AmgSetupData))
+    dp = C.cast(raw, C.POINTER(AmgSetupData))
+    if lib.amgd_crs_export(handle, dp) != 0:
+        raise RuntimeError("amgd_crs_export failed")
+    h = read_setup_data(dp.contents)
+    lib.free_data(C.pointer(dp))
+    return h
 
 
 def bind_setup(lib: C.CDLL) -> C.CDLL:

@@ -32,7 +32,12 @@ typedef struct {
 /* ---------------- runtime (amgd_rt.hip) ---------------- */
 int amgd_rt_init(int device);            /* idempotent; 0 on success */
 const char *amgd_last_error(void);
-void *amgd_alloc(size_t bytes);          /* caching pool; aborts loudly on OOM */
+void *amgd_alloc(size_t bytes);          /* arena; out of HBM: unwinds to amgd_try, else aborts */
+void amgd_set_hbm_cap(size_t bytes);     /* cap on live bytes (tests; 0: none) */
+/* run fn(arg); if an allocation runs out of HBM inside it, every block allocated since
+   the call is released and -2 returned (amgd_last_error() has the text) */
+int amgd_try(int (*fn)(void *), void *arg);
+void amgd_spmv_split_clear(void);        /* drop every cached SpMV shard split */
 void amgd_free(void *p);
 void amgd_spmv_split_forget(const void *ro);   /* drop cached SpMV shard splits of a freed buffer */
 void amgd_rt_shutdown(void);             /* free everything; pointers become invalid */
@@ -59,6 +64,13 @@ void dcsr_free(dcsr **A);
 dcsr *dcsr_copy(const dcsr *A);
 dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
 
+/* kernel-route counters (which default paths a setup took; read by the parity tests
+   at sizes where the default routing engages) */
+enum { AMGD_R_SPMV_LANE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WIN,
+       AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW, AMGD_R_N };
+extern uint64_t amgd_route_ctr[16];
+#define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
+
 /* scans: counts[0..n-1] -> exclusive prefix in counts[0..n], returns total */
 uint64_t amgd_scan_u64(uint64_t *counts, uint64_t n);
 uint32_t amgd_scan_u32(uint32_t *counts, uint64_t n);
@@ -67,6 +79,7 @@ uint32_t amgd_mask_rank(const uint8_t *mask, uint32_t n, uint32_t *map);
 
 /* ---------------- row sharding over GPUs (amgd_comm.hip) ---------------- */
 int amgd_nshards(void);                          /* 1: sharding off */
+int amgd_comm_procs(void);                       /* processes of the communicator (sim: 1) */
 void amgd_my_shards(int *first, int *last);      /* shard ranges this process computes */
 int amgd_shard_worth(uint64_t work, uint64_t min_work);
 /* contiguous ranges of equal work: split_h[0..N] from an exclusive prefix of n+1 entries */

@@ -74,6 +74,8 @@ static int rccl_load() {
   *(void **)&R.f = dlsym(R.h, "nccl" #f);                            \
   if (!R.f) {                                                        \
     fprintf(stderr, "omp_amg_amd: librccl lacks nccl%s\n", #f);      \
+    dlclose(R.h);                                                    \
+    R = Rccl();                 /* not loaded: the next call retries */ \
     return -1;                                                       \
   }
   SYM(GetUniqueId) SYM(CommInitRank) SYM(CommDestroy) SYM(Send) SYM(Recv) SYM(GroupStart)
@@ -157,6 +159,7 @@ extern "C" API void amgd_comm_stats_reset(void) { g_calls = g_bytes = 0; g_ms = 
 
 // ---- internal API (amgd.h) ----
 int amgd_nshards(void) { return g_kind == COMM_NONE ? 1 : g_size; }
+int amgd_comm_procs(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? g_size : 1; }
 void amgd_my_shards(int *first, int *last) {
   if (g_kind == COMM_SIM) { *first = 0; *last = g_size; }
   else { *first = g_rank; *last = g_rank + 1; }

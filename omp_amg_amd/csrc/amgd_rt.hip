@@ -87,12 +87,18 @@ static size_t g_arena_sz = 0;
 static bool g_arena_tried = false;
 static std::map<size_t, size_t> g_free_off;          // offset -> size
 static std::multimap<size_t, size_t> g_free_sz;      // size -> offset
-static std::unordered_map<void *, size_t> g_used;    // live block -> size
+struct UsedBlock { size_t sz; uint64_t serial; };
+static std::unordered_map<void *, UsedBlock> g_used; // live block -> size, allocation serial
 static std::unordered_map<void *, size_t> g_direct;  // live hipMalloc fallbacks -> size
 static size_t g_inuse = 0, g_peak = 0;
+static uint64_t g_serial = 0;                         // allocations made so far
+static size_t g_cap = (size_t)-1;                    // AMGD_HBM_CAP_GB / amgd_set_hbm_cap
+static int g_cap_read = 0, g_try_depth = 0;
+struct amgd_oom_error {};
 // statistics (AMGD_PHASES report): driver allocations (arena + fallbacks), their time
 static uint64_t g_nmalloc = 0, g_nrelease = 0;
 static double g_tmalloc = 0, g_bmalloc = 0;
+extern "C" { uint64_t amgd_route_ctr[16]; }
 extern "C" void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease) {
   *nmalloc = g_nmalloc; *gbytes = g_bmalloc / 1e9; *ms = g_tmalloc * 1e3; *nrelease = g_nrelease;
 }
@@ -141,11 +147,49 @@ static void arena_init() {
   free_insert(0, want);
 }
 
+extern "C" void amgd_set_hbm_cap(size_t bytes) { g_cap = bytes ? bytes : (size_t)-1; g_cap_read = 1; }
+// Out of HBM.  Inside amgd_try (the setup entry points) the setup is unwound: every
+// block it allocated is released and the entry point returns an error with the text
+// in amgd_error().  Elsewhere there is no caller to report to: abort as before.
+static void oom(size_t sz) {
+  snprintf(g_err, sizeof g_err, "out of HBM: request %.3f GB with %.3f GB live (peak %.3f GB, arena %.3f GB%s)",
+           sz / 1e9, g_inuse / 1e9, g_peak / 1e9, g_arena_sz / 1e9,
+           g_cap != (size_t)-1 ? ", capped" : "");
+  fprintf(stderr, "omp_amg_amd: %s\n", g_err);
+  if (g_try_depth > 0) throw amgd_oom_error();
+  abort();
+}
+extern "C" int amgd_try(int (*fn)(void *), void *arg) {
+  const uint64_t mark = g_serial;
+  g_try_depth++;
+  int rc;
+  try {
+    rc = fn(arg);
+  } catch (const amgd_oom_error &) {
+    rc = -2;
+    (void)hipDeviceSynchronize();      // the side stream of the Q factors as well
+    std::vector<void *> live;
+    for (auto &u : g_used)
+      if (u.second.serial >= mark) live.push_back(u.first);
+    g_try_depth--;
+    for (void *p : live) amgd_free(p);
+    return rc;
+  }
+  g_try_depth--;
+  return rc;
+}
+
 extern "C" void *amgd_alloc(size_t bytes) {
   amgd_s();
   if (!g_arena_tried) arena_init();
+  if (!g_cap_read) {
+    g_cap_read = 1;
+    const char *e = getenv("AMGD_HBM_CAP_GB");
+    if (e && *e && atof(e) > 0) g_cap = (size_t)(atof(e) * 1073741824.0);
+  }
   size_t sz = (bytes + 255) & ~(size_t)255;
   if (sz == 0) sz = 256;
+  if (g_inuse + sz > g_cap) oom(sz);
   void *p = nullptr;
   auto it = g_free_sz.lower_bound(sz);                           // best fit
   if (it != g_free_sz.end()) {
@@ -157,16 +201,15 @@ extern "C" void *amgd_alloc(size_t bytes) {
   } else {                                                        // arena full: the driver
     auto t0 = std::chrono::steady_clock::now();
     if (hipMalloc(&p, sz) != hipSuccess) {
-      fprintf(stderr, "omp_amg_amd: out of HBM: request %.3f GB with %.3f GB live (peak %.3f GB, "
-              "arena %.3f GB)\n", sz / 1e9, g_inuse / 1e9, g_peak / 1e9, g_arena_sz / 1e9);
-      abort();
+      (void)hipGetLastError();
+      oom(sz);
     }
     g_tmalloc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     g_nmalloc++;
     g_bmalloc += (double)sz;
     g_direct[p] = sz;
   }
-  g_used[p] = sz;
+  g_used[p] = UsedBlock{sz, g_serial++};
   g_inuse += sz;
   if (g_inuse > g_peak) g_peak = g_inuse;
   return p;
@@ -180,7 +223,7 @@ extern "C" void amgd_free(void *p) {
     fprintf(stderr, "omp_amg_amd: amgd_free of unknown pointer %p\n", p);
     abort();
   }
-  const size_t sz = it->second;
+  const size_t sz = it->second.sz;
   g_used.erase(it);
   g_inuse -= sz;
   auto d = g_direct.find(p);
@@ -1223,6 +1266,7 @@ extern "C" void amgd_rt_shutdown(void) {
   for (auto &d : g_direct) (void)hipFree(d.first);
   g_direct.clear();
   g_used.clear();
+  amgd_spmv_split_clear();
   g_free_off.clear();
   g_free_sz.clear();
   if (g_arena) (void)hipFree(g_arena);

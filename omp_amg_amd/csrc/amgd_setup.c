@@ -182,6 +182,7 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
       rows_.fs = stamp;
       rows_.fb = 8u * it;
       rows = &rows_;
+      amgd_route_hit(AMGD_R_CS_INC);
     }
     amgd_cs_spmv(S, vfd, g, vf, rows, 1);          /* g   = vf.*(S*vf)  */
     amgd_cs_spmv(S, g, w1, vf, rows, 2);           /* w1  = vf.*(S*g)   */
@@ -357,6 +358,7 @@ static void chebsim(double *m, double *c, double rho, double tol) {   /* amg_set
   }
 }
 
+static double g_pcg_rho, g_pcg_stop;     /* last pcg's final rho and stop level (trace) */
 /* PCG (amg_setup.c:2242): z = M.*r, at most min(n,100) iterations; r is overwritten */
 static uint32_t pcg(double *x, const dcsr *A, double *r, const double *M, double tol, const double *b) {
   uint32_t rn = A->rn;
@@ -379,6 +381,8 @@ static uint32_t pcg(double *x, const dcsr *A, double *r, const double *M, double
     rho_old = rho;
     rho = amgd_dot(r, z, rn);
   }
+  g_pcg_rho = rho;
+  g_pcg_stop = rho_stop;
   amgd_free(p); amgd_free(z); amgd_free(w);
   return k;
 }
@@ -443,13 +447,19 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
     amgd_vcompact(lc, lam, dl, nf);
     amgd_spmv(S, lc, q, 1., rc, -1., NULL);
     amgd_vunary(dc, ncond, AMGD_V_INV);
-    pcg(xx, S, q, dc, tol, rc);
+    const uint32_t its = pcg(xx, S, q, dc, tol, rc);
+    if (verbose())
+      printf("   constraint: %lu of %u rows, pcg %u its, rho %.9e stop %.9e\n", (unsigned long)ncond, nf,
+             its, g_pcg_rho, g_pcg_stop), fflush(stdout);
     amgd_vexpand_add(lam, xx, dl, nf);
     amgd_free(rc); amgd_free(dc); amgd_free(lc);
   } else {
     amgd_spmv(S, lam, q, 1., resid, -1., NULL);       /* q = resid - S*lam */
     amgd_vunary(d, nf, AMGD_V_INV);
-    pcg(xx, S, q, d, tol, resid);
+    const uint32_t its = pcg(xx, S, q, d, tol, resid);
+    if (verbose())
+      printf("   constraint: %u of %u rows, pcg %u its, rho %.9e stop %.9e\n", nf, nf, its, g_pcg_rho,
+             g_pcg_stop), fflush(stdout);
     amgd_vop(lam, lam, xx, nf, AMGD_V_ADD);
   }
   if (S != fac->S) dcsr_free(&S);
@@ -541,6 +551,7 @@ static dcsr *find_support(const dcsr *R, double goal) {
             amgd_spmv_rows(Rl, L2, n2, w, tmp);         /* tmp on D2 */
             amgd_spmv_rows(Rt, L3, n3, tmp, w2);        /* w2 on C3 */
             done = 1;
+            amgd_route_hit(AMGD_R_FS_INC);
           }
         }
       }
@@ -649,6 +660,29 @@ static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr) 
   return R;
 }
 
+/* diagnostics only (tools/oracle_trace.py on 27-point grids, where the interpolation
+   loop does not settle): AMGD_TRACE_MAX_IT / AMGD_TRACE_MAX_S end the process cleanly
+   after that many interpolation iterations on one level / seconds since the first */
+static void trace_limit(int it) {
+  static double t_first = -1;
+  static long max_it = -2;
+  static double max_s = -2;
+  if (max_it == -2) {
+    const char *a = getenv("AMGD_TRACE_MAX_IT"), *b = getenv("AMGD_TRACE_MAX_S");
+    max_it = a && *a ? atol(a) : -1;
+    max_s = b && *b ? atof(b) : -1;
+  }
+  if (max_it < 0 && max_s < 0) return;
+  if (t_first < 0) t_first = amgd_wtime();
+  if ((max_it >= 0 && it >= max_it) || (max_s >= 0 && amgd_wtime() - t_first >= max_s)) {
+    printf("TRACE LIMIT: stopped at interpolation iteration %d after %.1f s\n", it,
+           amgd_wtime() - t_first);
+    fflush(stdout);
+    amgd_sync();
+    exit(3);
+  }
+}
+
 static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, const dcsr *Ar,
                            double gamma2, double tol) {
   uint32_t rnf = Af->rn, rnc = Ac->rn, cnc = Ac->cn, cnr = Ar->cn;
@@ -728,7 +762,8 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     double w1m = amgd_max_first(w1, cnc, NULL);
     if (verbose())
       printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)W_skel->nnz,
-             (unsigned long)n, sqrt(gamma2), sqrt(maxr));
+             (unsigned long)n, sqrt(gamma2), sqrt(maxr)), fflush(stdout);
+    trace_limit(it);
     int stalled = prev_nnz == W_skel->nnz;   /* reference would loop forever */
     if (stalled) g_ub++;
     prev_nnz = W_skel->nnz;
@@ -800,18 +835,46 @@ API void amgd_dev_upload(void *d, const void *h, size_t n) { amgd_h2d(d, h, n); 
 API void amgd_dev_download(void *h, const void *d, size_t n) { amgd_d2h(h, d, n); }
 
 extern uint64_t amgd_spmv_bytes(void);
+extern uint64_t amgd_spmv_bytes_strict(void);
 extern void amgd_spmv_bytes_reset(void);
 extern void amgd_spgemm_set_timer(int slot);
 extern void amgd_spgemm_bytes_reset(void);
 extern uint64_t amgd_spgemm_bytes(void);
 
+typedef struct {
+  uint64_t nz;
+  const uint32_t *dAi, *dAj;
+  const double *dAv;
+  amgd_hier *h;          /* the hierarchy under construction (host part freed on failure) */
+} setup_args;
+static int setup_body(void *arg);
+
+/* Out of HBM anywhere in the setup: amgd_try unwinds it, releases every device block
+   the setup had allocated, and this returns -2 with the text in amgd_error() (the
+   reference's allocator exits the process instead, fail.c); *out is left NULL. */
 API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj, const double *dAv,
                           amgd_hier **out, int flags) {
   (void)flags;
+  *out = NULL;
   if (amgd_rt_init(0) != 0) {
     fprintf(stderr, "omp_amg_amd: %s\n", amgd_last_error());
     return -1;
   }
+  setup_args a = {nz, dAi, dAj, dAv, NULL};
+  int rc = amgd_try(setup_body, &a);
+  if (rc != 0) {
+    if (a.h) { free(a.h->lv); free(a.h); }
+    return rc;
+  }
+  *out = a.h;
+  return 0;
+}
+
+static int setup_body(void *arg) {
+  setup_args *sa = (setup_args *)arg;
+  const uint64_t nz = sa->nz;
+  const uint32_t *dAi = sa->dAi, *dAj = sa->dAj;
+  const double *dAv = sa->dAv;
   memset(&g_st, 0, sizeof g_st);
   g_ub = 0;
   amgd_timer_reset();
@@ -824,6 +887,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
   const double tol = 0.5, ctol = 0.7, itol = 1e-4;
   const double gamma2 = 1. - sqrt(1. - tol), gamma = sqrt(gamma2);
   amgd_hier *h = (amgd_hier *)calloc(1, sizeof(amgd_hier));
+  sa->h = h;
   h->cap = 64;
   h->lv = (level_t *)calloc(h->cap, sizeof(level_t));
   h->tolc = ctol;
@@ -846,7 +910,7 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     L->A = A;
     ph(-1);
     if (verbose()) printf("Level %u, dim(A) = %u, nnz(A)/dim(A) = %f\n", level + 1, cn,
-                          cn ? (double)A->nnz / cn : 0.0);
+                          cn ? (double)A->nnz / cn : 0.0), fflush(stdout);
     if (cn <= 1) {
       double a0 = 0;
       if (A->nnz) amgd_d2h(&a0, A->a, 8);
@@ -932,13 +996,13 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
   g_st.rap_kernel_ms = amgd_timer_ms(0);
   g_st.spmv_kernel_ms = amgd_timer_ms(1);
   g_st.spmv_bytes = amgd_spmv_bytes();
+  g_st.spmv_bytes_strict = amgd_spmv_bytes_strict();
   amgd_spmv_bytes_reset();
   g_st.rap_bytes = amgd_spgemm_bytes();
   amgd_spgemm_bytes_reset();
   g_st.nlevels = h->nlevels;
   g_st.ub_events = (uint32_t)g_ub;
   g_st.peak_bytes = amgd_pool_peak_bytes();
-  *out = h;
   return 0;
 }
 
@@ -1048,8 +1112,14 @@ API void amg_setup(amg_uint n, const amg_uint *Ai, const amg_uint *Aj, const dou
   amgd_h2d(dv, Av, (size_t)n * 8);
   free(hi); free(hj);
   amgd_hier *h = NULL;
-  if (amgd_setup_device(n, di, dj, dv, &h, 0) != 0) abort();
+  const int rc = amgd_setup_device(n, di, dj, dv, &h, 0);
   amgd_free(di); amgd_free(dj); amgd_free(dv);
+  if (rc != 0) {
+    /* no hierarchy: data is left with nlevels = 0 and amgd_error() says why */
+    fprintf(stderr, "omp_amg_amd: amg_setup failed: %s\n", amgd_last_error());
+    memset(data, 0, sizeof *data);
+    return;
+  }
   amgd_hier_export(h, data);
   amgd_hier_free(&h);
 }
@@ -1151,12 +1221,27 @@ API void amg_export(struct amg_setup_data *data) {
 /* ------------------------------------------------------------------------ */
 struct crs_data { amgd_hier *h; amg_uint un; amg_uint null_space; };
 
+/* crs_setup (reference amg.c:475): rank comm->id of comm->np passes its local
+   matrix -- n local dofs with global ids id[0..n), nz entries in local indices.  The
+   reference hands the assembled matrix, keyed by global id (its amg_dump,
+   amg.c:1048-1072, drops entries touching id 0 and exact zeros), to the setup.  Here
+   every rank's entries are mapped to global ids on the host, uploaded, and -- for
+   np > 1 -- completed into one COO on every rank by an allgatherv over the library's
+   communicator (amgd_comm_init_rccl / _host, rank = comm->id, size = comm->np), in
+   rank order; duplicates (dofs shared between ranks) are summed by build_csr in that
+   order.  The setup then runs row-sharded over the ranks (amgd_comm.hip) and every
+   rank keeps the hierarchy.  Global ids must be 1..N (row id-1 of the assembled
+   matrix).  Returns NULL (message on stderr, amgd_error()) on a communicator that
+   does not match comm, or when the setup runs out of HBM. */
 API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz, const amg_uint *Ai,
                                const amg_uint *Aj, const double *A, amg_uint null_space,
                                const struct comm *comm) {
-  if (comm && comm->np != 1) {
-    fprintf(stderr, "omp_amg_amd: crs_setup supports np == 1 (got %lu)\n", (unsigned long)comm->np);
-    abort();
+  const int np = comm ? (int)comm->np : 1, me = comm ? (int)comm->id : 0;
+  if (np > 1 && (amgd_comm_procs() != np || amgd_comm_rank() != me)) {
+    fprintf(stderr, "omp_amg_amd: crs_setup with np = %d needs the library communicator of the same "
+            "ranks (amgd_comm_init_rccl / amgd_comm_init_host; have %d processes, rank %d)\n", np,
+            amgd_comm_procs(), amgd_comm_rank());
+    return NULL;
   }
   /* local dof k is global id[k]; entries touching id 0 are dropped (amg.c:1065) */
   amg_uint *I = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8), *J = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8);
@@ -1168,14 +1253,43 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
     I[m] = id[i] - 1; J[m] = id[j] - 1; V[m] = A[k]; m++;
   }
   struct crs_data *d = (struct crs_data *)calloc(1, sizeof *d);
-  uint32_t *di = (uint32_t *)amgd_alloc(m * 4 + 4), *dj = (uint32_t *)amgd_alloc(m * 4 + 4);
-  double *dv = dalloc(m);
+  /* entries of every rank: counts, then one allgatherv of (i, j, v) */
+  uint64_t *cnt = (uint64_t *)calloc((size_t)np + 1, 8), *pre = (uint64_t *)calloc((size_t)np + 1, 8);
+  cnt[me] = m;
+  if (np > 1) amgd_allgather_u64(cnt);
+  for (int r = 0; r < np; r++) pre[r + 1] = pre[r] + cnt[r];
+  const uint64_t M = pre[np];
+  uint32_t *di = (uint32_t *)amgd_alloc(M * 4 + 4), *dj = (uint32_t *)amgd_alloc(M * 4 + 4);
+  double *dv = dalloc(M);
   uint32_t *hi = (uint32_t *)malloc(m * 4 + 4), *hj = (uint32_t *)malloc(m * 4 + 4);
-  for (amg_uint k = 0; k < m; k++) { hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k]; }
-  amgd_h2d(di, hi, m * 4); amgd_h2d(dj, hj, m * 4); amgd_h2d(dv, V, m * 8);
+  for (amg_uint k = 0; k < m; k++) {
+    if (I[k] > 0xfffffffeul || J[k] > 0xfffffffeul) {
+      fprintf(stderr, "omp_amg_amd: crs_setup: global id %lu exceeds 32-bit range\n", (unsigned long)(I[k] + 1));
+      abort();
+    }
+    hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k];
+  }
+  amgd_h2d(di + pre[me], hi, m * 4); amgd_h2d(dj + pre[me], hj, m * 4); amgd_h2d(dv + pre[me], V, m * 8);
   free(hi); free(hj); free(I); free(J); free(V);
-  if (amgd_setup_device(m, di, dj, dv, &d->h, 0) != 0) abort();
+  if (np > 1) {
+    uint64_t *off = (uint64_t *)malloc(3 * ((size_t)np + 1) * 8);
+    void *bufs[3] = {di, dj, dv};
+    for (int r = 0; r <= np; r++) {
+      off[r] = 4 * pre[r];
+      off[(np + 1) + r] = 4 * pre[r];
+      off[2 * (np + 1) + r] = 8 * pre[r];
+    }
+    amgd_allgatherv(3, bufs, off);
+    free(off);
+  }
+  free(cnt); free(pre);
+  const int rc = amgd_setup_device(M, di, dj, dv, &d->h, 0);
   amgd_free(di); amgd_free(dj); amgd_free(dv);
+  if (rc != 0) {
+    fprintf(stderr, "omp_amg_amd: crs_setup failed: %s\n", amgd_last_error());
+    free(d);
+    return NULL;
+  }
   d->un = n;
   d->null_space = null_space;
   return d;
@@ -1187,6 +1301,10 @@ API void crs_solve(double *x, struct crs_data *data, double *b) {
 }
 API void crs_stats(struct crs_data *data) {
   printf("AMG stats: %u levels (setup %.3f ms)\n", data && data->h ? data->h->nlevels : 0, g_st.t_total_ms);
+}
+API int amgd_crs_export(const struct crs_data *data, struct amg_setup_data *out) {
+  if (!data || !data->h) return -1;
+  return amgd_hier_export(data->h, out);
 }
 API void crs_free(struct crs_data *data) {
   if (!data) return;

@@ -692,6 +692,7 @@ static int spmv_nt() {
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
+    amgd_route_hit(AMGD_R_SPMV_LANE);                                                         \
     const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
     if (spmv_nt())                                                                            \
       LANE_LAUNCH_NT(LIST, true, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
@@ -750,6 +751,7 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
     uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 16);
     unsigned *cnt = (unsigned *)(ll + n);
     amgd_memset(cnt, 0, 4);
+    amgd_route_hit(AMGD_R_MV_LONG);
     k_list_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, ml, ll, cnt);
     amgd_rows_exact(M->ro, M->col, M->a, x, ll, cnt, std::min<uint64_t>(n, M->nnz / (ml + 1) + 1),
                     M->nnz, z);
@@ -768,9 +770,12 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
                       double beta, const uint8_t *f);
 // algorithmic bytes of the event-timed (timer slot 1) lane-kernel products: each entry's
 // column + value once, x gathered once per entry, row offsets, z (and y, f) once per row
-static uint64_t g_mv_bytes = 0;
+// g_mv_bytes_strict: the same with x read once (8 B per column), the minimum any
+// kernel must move -- the roofline's algorithmic bytes
+static uint64_t g_mv_bytes = 0, g_mv_bytes_strict = 0;
 extern "C" uint64_t amgd_spmv_bytes(void) { return g_mv_bytes; }
-extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = 0; }
+extern "C" uint64_t amgd_spmv_bytes_strict(void) { return g_mv_bytes_strict; }
+extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = g_mv_bytes_strict = 0; }
 // AMGD_MVLOG=1: one line per whole-matrix SpMV (rows, nnz, kernel, time, effective GB/s)
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
@@ -809,6 +814,7 @@ void amgd_spmv_split_forget(const void *ro) {
     if ((const void *)g_mv_split[q].ro == ro) g_mv_split.erase(g_mv_split.begin() + q);
     else q++;
 }
+void amgd_spmv_split_clear(void) { g_mv_split.clear(); }
 static uint64_t g_mv_shard_calls = 0;
 extern "C" uint64_t amgd_spmv_shard_calls(void) { return g_mv_shard_calls; }   // (test API)
 static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alpha, const double *y,
@@ -838,8 +844,9 @@ static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alph
     const dcsr *M = &Ms;
     LANE_LAUNCH(false, n, (const uint32_t *)nullptr, x, z + r0, alpha, y ? y + r0 : nullptr, beta,
                 f ? f + r0 : nullptr, 0xffffffffu);
-    g_mv_bytes += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8 * (sp->pre[q + 1] - sp->pre[q]) : 0) +
-                  16ull * n + 8 + (y && alpha != 0.0 ? 8ull * n : 0) + (f ? (uint64_t)n : 0);
+    const uint64_t rest = 16ull * n + 8 + (y && alpha != 0.0 ? 8ull * n : 0) + (f ? (uint64_t)n : 0);
+    g_mv_bytes += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8 * (sp->pre[q + 1] - sp->pre[q]) : 0) + rest;
+    g_mv_bytes_strict += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8ull * M0->cn : 0) + rest;
   }
   amgd_timer_stop(1);
   KCHECK();
@@ -866,8 +873,9 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
     amgd_timer_start(1);                       // roofline: whole-matrix long-row products
     LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
     amgd_timer_stop(1);
-    g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + 16ull * M->rn + 8 +
-                  (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
+    const uint64_t rest = 16ull * M->rn + 8 + (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
+    g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
+    g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
     k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
@@ -2344,6 +2352,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     amgd_d2h(hc, counts, 24);
   }
   const unsigned ntiny = hc[5];
+  if (ntiny) amgd_route_hit(AMGD_R_SG_TINY);
   if (ntiny)
     k_sg_tiny<0><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
                                                             B->col, B->a, cnt, nullptr, nullptr, nullptr);
@@ -2362,6 +2371,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
   if (hc[1]) {
     const int wsym = kseq ? sg_wsym() : 0;
+    if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
     if (wsym == 8192)
       k_sg_wsym<8192><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
@@ -2495,6 +2505,9 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   static int nt3 = -1, nt2 = -1;
   if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 1024; }
   if (nt2 < 0) { const char *e = getenv("AMGD_SG_NT2"); nt2 = e ? atoi(e) : 512; }
+  if (hn[0] || hn[1] || hn[2] || hn[3]) amgd_route_hit(kseq ? AMGD_R_SG_KSEQ : AMGD_R_SG_ROW);
+  if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WIN);
+  if (hn[4]) amgd_route_hit(AMGD_R_SG_LONG);
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)

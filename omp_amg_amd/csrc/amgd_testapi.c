@@ -173,6 +173,14 @@ API void amgd_test_qf_stats(uint64_t *out) {
 
 /* whole-matrix SpMVs that ran row-sharded (multi-GPU) since the library loaded */
 extern uint64_t amgd_spmv_shard_calls(void);
+/* cap on live device bytes (0: none): the out-of-HBM path without filling 288 GB */
+API void amgd_test_hbm_cap(uint64_t bytes) { amgd_set_hbm_cap((size_t)bytes); }
+API uint64_t amgd_test_pool_inuse(void) { return amgd_pool_bytes_in_use(); }
+/* kernel-route counters since the last reset (out: AMGD_R_N entries) */
+API void amgd_test_route_stats(uint64_t *out, int reset) {
+  for (int r = 0; r < AMGD_R_N; r++) out[r] = amgd_route_ctr[r];
+  if (reset) memset(amgd_route_ctr, 0, sizeof amgd_route_ctr);
+}
 API uint64_t amgd_test_spmv_shard_calls(void) { return amgd_spmv_shard_calls(); }
 
 /* SpGEMM kernel family: 1 = flat-enumeration kernels only, 0 = automatic */

@@ -9,7 +9,9 @@
  * expand_support materialises dense w x nbad matrices, amg_setup.c:1034-1093).
  *
  * Pinned against the compiled reference (oracle/_ref/libref_amg.so) by
- * tests/test_oracle_vs_ref.py and against tests/golden/ fixtures.
+ * tests/golden/make_golden.py (fixtures written from the reference only where the oracle
+ * matches it bit for bit) and tests/test_oracle_golden.py (every fixture and the
+ * reference-made digests of tests/golden/digests.json).
  *
  * Deviations are confined to inputs on which the reference is undefined
  * (documented in DESIGN.md "Reference UB"):
@@ -567,6 +569,8 @@ static void chebsim(double *m, double *c, double rho, double tol) {
 }
 
 /* pcg (amg_setup.c:2242); M multiplies (z = M.*r), r is overwritten */
+static double g_pcg_rho, g_pcg_stop;     /* last pcg's final rho and stop level (trace) */
+static u64 g_offrow;                     /* sp_add landings past row j's end (trace) */
 static u32 pcg(double *x, const ocsr *A, double *r, const double *M, double tol, const double *b) {
   u32 rn = A->rn;
   for (u32 i = 0; i < rn; i++) x[i] = 0.;
@@ -594,6 +598,8 @@ static u32 pcg(double *x, const ocsr *A, double *r, const double *M, double tol,
     rho_old = rho;
     rho = vv_dot(r, z, rn);
   }
+  g_pcg_rho = rho;
+  g_pcg_stop = rho_stop;
   free(p); free(z); free(w);
   return k;
 }
@@ -702,6 +708,7 @@ static void sp_add_ref(ocsr *St, u32 j, double alpha, u32 xn, const u32 *xi, con
   for (u32 m = 0; m < xn; m++) {
     while (t < end && St->col[t] < xi[m]) t++;
     if (t >= end) { oracle_overflow_events++; return; }
+    if (t >= St->ro[j + 1]) g_offrow++;
     St->a[t] += alpha * x[m];
     t++;
   }
@@ -749,7 +756,10 @@ static void solve_constraint(double *lam, const ocsr *W_skel, const ocsr *W_skel
   ocsr *Wsk_t = transpose(W_skel);         /* mxm(S, W_skel, W_skel, 1.) = W_skel * W_skel^T */
   ocsr *S = spgemm(W_skel, Wsk_t);
   csr_free(&Wsk_t);
+  g_offrow = 0;
+  const u64 ovf0 = oracle_overflow_events;
   interp_lmop(S, Af, au2, W_skelt);
+  const u64 offrow = g_offrow, ovf = oracle_overflow_events - ovf0;
   dump_ocsr("S", S);
   double *resid = NEW(double, nf), *d = NEW(double, nf), *dl = NEW(double, nf);
   apply_M(resid, 1.0, v, -1.0, W0, u);
@@ -763,7 +773,10 @@ static void solve_constraint(double *lam, const ocsr *W_skel, const ocsr *W_skel
   double *q = NEW(double, nco ? nco : 1), *x = NEW(double, nco ? nco : 1);
   apply_M(q, 1., resid, -1., S, lc);
   for (u32 i = 0; i < nco; i++) d[i] = 1. / d[i];
-  pcg(x, S, q, d, tol, resid);
+  const u32 its = pcg(x, S, q, d, tol, resid);
+  if (getenv("ORACLE_VERBOSE"))
+    printf("   constraint: %u of %u rows, pcg %u its, rho %.9e stop %.9e, sp_add off-row %lu past-end %lu\n",
+           nco, nf, its, g_pcg_rho, g_pcg_stop, (unsigned long)offrow, (unsigned long)ovf), fflush(stdout);
   u32 t = 0;
   for (u32 i = 0; i < nf; i++) if (dl[i] != 0.) lam[i] += x[t++];
   csr_free(&S);

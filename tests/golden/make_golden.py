@@ -51,7 +51,8 @@ def candidates():
         c[f"p2d5_{m}"] = (lambda m=m: problems.poisson2d(m))
     for m in (8, 12, 16, 24):
         c[f"p2d9_{m}"] = (lambda m=m: problems.poisson2d(m, 9))
-    for (e, N) in ((2, 3), (2, 4), (3, 2), (3, 3)):
+    # configs[2] is order N = 7: e2 N7 (13^3 = 2197 rows), e3 N7 (20^3 = 8000 rows)
+    for (e, N) in ((2, 3), (2, 4), (3, 2), (3, 3), (2, 5), (2, 6), (2, 7), (3, 7)):
         c[f"sem_e{e}_N{N}"] = (lambda e=e, N=N: problems.sem_laplacian(e, e, e, N, seed=1, jitter=0.3))
     return c
 
@@ -66,7 +67,7 @@ def _run(q, so, Ai, Aj, Av, want_ub):
         q.put(("err", repr(e), (0, 0)))
 
 
-def run_isolated(so, Ai, Aj, Av, timeout=120, want_ub=False):
+def run_isolated(so, Ai, Aj, Av, timeout=int(os.environ.get("GOLDEN_TIMEOUT", "120")), want_ub=False):
     ctx = mp.get_context("fork")
     q = ctx.Queue()
     p = ctx.Process(target=_run, args=(q, so, Ai, Aj, Av, want_ub))
@@ -103,6 +104,12 @@ def asan_clean(Ai, Aj, Av, timeout=180):
 def main():
     only = set(sys.argv[1:])
     manifest = {"kept": {}, "excluded": {}}
+    mpath = os.path.join(GOLD, "MANIFEST.json")
+    if only and os.path.exists(mpath):       # partial run: update the existing manifest
+        manifest = json.load(open(mpath))
+        for k in ("kept", "excluded"):
+            for name in only:
+                manifest[k].pop(name, None)
     for name, gen in candidates().items():
         if only and name not in only:
             continue
@@ -133,8 +140,8 @@ def main():
                                   "reference_asan_clean": asan_ok, "asan": why if not asan_ok else "",
                                   "sp_add_end_overflows": ovf}
         print(f"{name:14s} kept  rows={int(rd['L0_n'])} levels={nl}", flush=True)
-    if not only:
-        with open(os.path.join(GOLD, "MANIFEST.json"), "w") as f:
+    if True:
+        with open(mpath, "w") as f:
             json.dump(manifest, f, indent=1, sort_keys=True)
 
 

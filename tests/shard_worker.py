@@ -34,7 +34,22 @@ def main():
     shard.init_host(rank, size)
     shard.set_min_work(0.0)
     shard.stats(reset=True)
-    h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    if os.environ.get("SHARD_CRS"):
+        # crs_setup (crs.h) with comm = {rank, size}: this rank passes its block of
+        # rows as a local matrix (local dof k = global id ids[k]), the library gathers
+        # the assembled matrix over its communicator and keeps the hierarchy
+        Ai64, Aj64 = np.asarray(Ai, np.int64), np.asarray(Aj, np.int64)
+        n = int(max(Ai64.max(), Aj64.max())) + 1
+        lo, hi = rank * n // size, (rank + 1) * n // size
+        sel = (Ai64 >= lo) & (Ai64 < hi)
+        ids = np.arange(1, n + 1, dtype=np.uint64)     # every rank knows every global id
+        hd = abi.crs_setup(oa.lib(), n, ids, Ai64[sel], Aj64[sel], np.asarray(Av)[sel],
+                           rank=rank, np_=size)
+        assert hd is not None, "crs_setup returned NULL"
+        h = abi.crs_export(oa.lib(), hd)
+        oa.lib().crs_free(hd)
+    else:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
     st = shard.stats()
     shard.free()
     bad = parity.compare(ref, h, exact=True)

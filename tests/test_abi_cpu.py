@@ -67,3 +67,17 @@ def test_problem_generators_are_assembled():
         for i, j, v in zip(Ai, Aj, Av):
             d[(int(i), int(j))] = v
         assert all(abs(d[(j, i)] - v) <= 1e-12 * abs(v) for (i, j), v in d.items())
+
+
+def test_crs_setup_rejects_foreign_comm_without_gpu():
+    """crs_setup with comm->np > 1 but no library communicator of those ranks returns
+    NULL before touching the device (no hang waiting for peers, no abort)"""
+    import omp_amg_amd as oa
+    from omp_amg_amd import abi
+    if not os.path.exists(oa.LIB_PATH):
+        oa.build()
+    lib = ctypes.CDLL(oa.LIB_PATH)
+    A = np.array([2, -1, -1, 0, -1, 2, 0, -1, -1, 0, 2, -1, 0, -1, -1, 2], dtype=np.float64)
+    h = abi.crs_setup(lib, 4, [1, 2, 3, 4], np.repeat(np.arange(4), 4), np.tile(np.arange(4), 4), A,
+                      rank=1, np_=2, quiet=False)
+    assert h is None

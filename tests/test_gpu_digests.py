@@ -1,0 +1,69 @@
+"""Parity at sizes where the DEFAULT kernel routing engages, with no forcing switch.
+
+tests/golden/digests.json (tests/golden/make_digests.py) holds, per case, the
+generator of the input, its SHA-256, and a SHA-256 of every array of the expected
+hierarchy -- from the reference itself (sem_e3_N7, 8 000 rows, order N = 7 as in
+BASELINE configs[2]) or from the oracle, which tests/test_oracle_golden.py pins bit
+for bit to the reference's own outputs.  Equal digests = bit-identical hierarchy
+(C/F sets, ids, every CSR pattern and every double).
+
+The GPU run also records which kernel routes ran (omp_amg_amd.route_stats), so each
+case shows that the paths the small fixtures reach only by forcing -- incremental
+coarsening and find_support sweeps, lane SpMV, windowed / k-sequential SpGEMM --
+were the ones that produced the matching bits.
+"""
+import json
+import os
+
+import pytest
+
+from conftest import GOLD
+import omp_amg_amd as oa
+from omp_amg_amd import abi
+
+DIGESTS = os.path.join(GOLD, "digests.json")
+
+
+def _db():
+    return json.load(open(DIGESTS)) if os.path.exists(DIGESTS) else {"cases": {}, "excluded": {}}
+
+
+def _mk():
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_digests
+    return make_digests
+
+
+# routes each case must have taken (kept to what its sizes guarantee by the defaults)
+EXPECT_ROUTES = {
+    "p7_48": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym"),
+    "p7_64": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym"),
+    "aniso_20": ("fs_inc", "mv_long"),
+    "aniso_24": ("fs_inc",),
+    "aniso_32": ("fs_inc", "spmv_lane"),
+    "p27_20": ("fs_inc", "spmv_lane", "sg_win", "sg_wsym"),
+    "sem_e3_N7": ("spmv_lane", "sg_wsym"),
+    "sem_e4_N7": ("spmv_lane", "sg_kseq", "sg_wsym"),
+    "sem_e5_N7": ("spmv_lane", "sg_kseq"),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", sorted(_db()["cases"]))
+def test_gpu_matches_digest_default_routing(case):
+    mk = _mk()
+    d = _db()["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    assert mk.input_digest(Ai, Aj, Av) == d["input_sha256"], "input generator drifted"
+    oa.route_stats(reset=True)
+    h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    routes = oa.route_stats(reset=True)
+    got = mk.hierarchy_digest(h)
+    exp = d["arrays"]
+    bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    assert not bad, f"{len(bad)} arrays differ from the {d['source']}: {bad[:12]} (summary {mk.summary(h)} " \
+                    f"vs {d['summary']})"
+    missing = [r for r in EXPECT_ROUTES.get(case, ()) if routes[r] == 0]
+    assert not missing, f"default routes not taken: {missing} ({routes})"
+    print(case, d["source"], d["summary"]["n"], routes)

@@ -167,12 +167,17 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("size,case", [(2, "gold:p7_12"), (2, "gold:sem_e3_N2"), (3, "gold:p27_8"),
-                                       (2, "p27:14")])
-def test_host_transport_processes(size, case):
+@pytest.mark.parametrize("size,case,crs", [(2, "gold:p7_12", ""), (2, "gold:sem_e3_N2", ""),
+                                           (3, "gold:p27_8", ""), (2, "p27:14", ""),
+                                           (2, "gold:amgdmp", "1"), (3, "gold:p7_12", "1")],
+                         ids=["p7_12x2", "sem_e3_N2x2", "p27_8x3", "p27_14x2", "crs_amgdmp_x2",
+                              "crs_p7_12x3"])
+def test_host_transport_processes(size, case, crs):
+    """crs="1": crs_setup(comm = {rank, size}) with each rank passing its own block of
+    rows; the gathered, sharded hierarchy is the reference's fixture bit for bit"""
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(size),
-               SHARD_CASE=case, PYTHONPATH=ROOT)
+               SHARD_CASE=case, SHARD_CRS=crs, PYTHONPATH=ROOT)
     ps = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "shard_worker.py")],
                            env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            text=True) for r in range(size)]

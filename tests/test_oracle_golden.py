@@ -45,3 +45,28 @@ def test_amgdmp_files_match_reference_loader():
     # assembled, symmetric pattern
     pairs = set(zip(Ai.tolist(), Aj.tolist()))
     assert all((j, i) in pairs for (i, j) in pairs)
+
+
+def _digest_cases(max_secs):
+    import json
+    p = os.path.join(GOLD, "digests.json")
+    if not os.path.exists(p):
+        return []
+    db = json.load(open(p))["cases"]
+    return sorted(k for k, v in db.items() if v["source"] == "reference" or v["secs"] <= max_secs)
+
+
+@pytest.mark.parametrize("case", _digest_cases(20.0))
+def test_oracle_matches_digest(oracle_lib, case):
+    """the oracle reproduces the digest fixtures it can redo in seconds, and the
+    reference-made ones (sem_e3_N7: SEM order 7, 8 000 rows) bit for bit"""
+    import json
+    import sys
+    sys.path.insert(0, GOLD)
+    import make_digests as mk
+    d = json.load(open(os.path.join(GOLD, "digests.json")))["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    assert mk.input_digest(Ai, Aj, Av) == d["input_sha256"]
+    got = mk.hierarchy_digest(abi.run_setup(oracle_lib, Ai, Aj, Av))
+    bad = sorted(k for k in set(got) | set(d["arrays"]) if got.get(k) != d["arrays"].get(k))
+    assert not bad, bad[:12]
