@@ -95,6 +95,7 @@ def lib() -> C.CDLL:
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
+        L.amgd_test_spgemm_wt.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
@@ -386,6 +387,12 @@ def spgemm_win(w: int) -> None:
     """wide output rows: 0 = LDS hash kernels, 4096 / 8192 / 16384 = dense-accumulator column
     windows whatever the column count, -1 = automatic (environment / default)"""
     lib().amgd_test_spgemm_win(int(w))
+
+
+def spgemm_wt(t: int) -> None:
+    """windowed SpGEMM rows per work-group: 4 / 8 = tiled kernel (union of the tile's A
+    rows in ascending k), 0 = one row per work-group, -1 = default (environment / 4)"""
+    lib().amgd_test_spgemm_wt(int(t))
 
 
 def spgemm_wsym(w: int) -> None:

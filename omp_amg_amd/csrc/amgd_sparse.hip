@@ -1945,6 +1945,239 @@ __global__ __launch_bounds__(256) void k_sg_win(const uint32_t *rows, uint32_t n
   }
 }
 
+// Tiled windowed SpGEMM: a work-group takes T consecutive rows of the windowed-row
+// list (runs of ascending row indices: neighbouring rows, whose A rows share most of
+// their k) and walks the UNION of their A entries in ascending k.  Each B row k is
+// loaded once for the tile and added into the window accumulator of every tile row
+// holding k; one barrier per distinct k of the union orders layer k before layer k'.
+// Per output row the additions still arrive one layer at a time in ascending k,
+// starting from +0 -- the reference's sum, bit for bit -- while the B-row loads and
+// the barriers (the k_sg_win cost) fall by the tile's k overlap.
+// A rows are taken in chunks of M = NT/T entries per row (one wavefront per row for
+// T = 4); each chunk's union is ordered by (k, row) with merge-path ranks (binary
+// searches in the other rows' compacted chunk), so no sort pass.  Chunks follow
+// each other in ascending k per row, which is all the per-row order needs.
+template <int W, int T, int RAP = 0>
+__global__ __launch_bounds__(256) void k_sg_wt(const uint32_t *rows, uint32_t nrows,
+                                               const uint64_t *aro, const uint32_t *acol,
+                                               const double *aa, const uint64_t *bro,
+                                               const uint32_t *bcol, const double *ba,
+                                               uint64_t *cnt2, const uint64_t *xro,
+                                               uint32_t *xcol, double *xa) {
+  constexpr int NT = 256, SPT = W / NT, M = NT / T;
+  static_assert(M == 32 || M == 64, "one or two tile rows per wavefront");
+  __shared__ double acc[T * W];
+  __shared__ uint32_t sk[T][M];           // chunk keys of each row, compacted, ascending
+  __shared__ double sa[T][M];
+  __shared__ uint32_t sn[T];
+  __shared__ uint32_t uk[NT];             // chunk union ordered by (k, row)
+  __shared__ uint8_t ut[NT];
+  __shared__ double ua[NT];
+  __shared__ uint32_t gfirst[NT + 1];     // distinct k: first union entry
+  __shared__ uint64_t gb0[NT];
+  __shared__ uint32_t glen[NT], gcur[NT];
+  __shared__ uint32_t s_ng, s_min, s_max;
+  __shared__ uint32_t wtot[NT / 64 + 1];
+  __shared__ uint32_t s_i[T], s_nout[T];
+  __shared__ uint64_t s_a0[T], s_a1[T];
+  const int t = threadIdx.x, lane = t & 63;
+  const uint32_t ntiles = (nrows + T - 1) / T;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int nt = (int)min((uint32_t)T, nrows - tile * T);
+    if (t < T) {
+      if (t < nt) {
+        const uint32_t i = rows[tile * T + t];
+        s_i[t] = i;
+        s_a0[t] = aro[i];
+        s_a1[t] = aro[i + 1];
+      } else {
+        s_i[t] = 0xffffffffu;
+        s_a0[t] = s_a1[t] = 0;
+      }
+      s_nout[t] = 0;
+    }
+    if (t == 0) { s_min = 0xffffffffu; s_max = 0; }
+    __syncthreads();
+    uint64_t maxlen = 0;
+    for (int r = 0; r < nt; r++) {                     // column range of the tile
+      const uint64_t a0 = s_a0[r], a1 = s_a1[r];
+      maxlen = max(maxlen, a1 - a0);
+      for (uint64_t ka = a0 + t; ka < a1; ka += NT) {
+        const uint32_t k = acol[ka];
+        if (ka + 1 < a1 && acol[ka + 1] == k) continue;
+        const uint64_t b0 = bro[k], b1 = bro[k + 1];
+        if (b0 < b1) {
+          atomicMin(&s_min, bcol[b0]);
+          atomicMax(&s_max, bcol[b1 - 1]);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t cmin = s_min, cmax = s_max;
+    const uint32_t nch = (uint32_t)((maxlen + M - 1) / M);
+    for (uint64_t wbl = cmin; cmin <= cmax && wbl <= (uint64_t)cmax; wbl += W) {
+      const uint32_t wb = (uint32_t)wbl;
+      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + W - 1);   // inclusive
+      for (int q = t; q < nt * W; q += NT) acc[q] = 0.0;
+      for (uint32_t c = 0; c < nch; c++) {
+        if (nch > 1 || wb == cmin) {                   // union table of this chunk
+          const int r = t / M, m = t % M;
+          bool v = false;
+          uint32_t k = 0;
+          double a = 0.0;
+          if (r < nt) {
+            const uint64_t ka = s_a0[r] + (uint64_t)c * M + m, a1 = s_a1[r];
+            if (ka < a1) {
+              k = acol[ka];
+              v = !(ka + 1 < a1 && acol[ka + 1] == k);   // duplicate columns: the last one wins
+              if (v) a = aa[ka];
+            }
+          }
+          const unsigned long long bal = __ballot(v);
+          const int sh = M == 64 ? 0 : (lane / M) * M;
+          const unsigned long long rmask = M == 64 ? ~0ull : (((1ull << M) - 1ull) << sh);
+          const uint32_t pos = (uint32_t)__popcll(bal & rmask & ((1ull << lane) - 1ull));
+          if (v) { sk[r][pos] = k; sa[r][pos] = a; }
+          if (m == 0) sn[r] = (uint32_t)__popcll(bal & rmask);
+          __syncthreads();
+          if (v) {                                      // rank in the union by (k, row)
+            uint32_t rank = pos;
+            for (int r2 = 0; r2 < nt; r2++) {
+              if (r2 == r) continue;
+              uint32_t lo = 0, hi = sn[r2];
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                const uint32_t km = sk[r2][mid];
+                if (r2 < r ? km <= k : km < k) lo = mid + 1;
+                else hi = mid;
+              }
+              rank += lo;
+            }
+            uk[rank] = k;
+            ut[rank] = (uint8_t)r;
+            ua[rank] = a;
+          }
+          uint32_t ntot = 0;
+          for (int r2 = 0; r2 < T; r2++) ntot += sn[r2];
+          __syncthreads();
+          const bool st = (uint32_t)t < ntot && (t == 0 || uk[t] != uk[t - 1]);
+          const uint32_t inc = block_incl_scan<NT>(st ? 1u : 0u, wtot);
+          if (st) {
+            const uint32_t g = inc - 1, kk = uk[t];
+            const uint64_t b0 = bro[kk];
+            const uint32_t len = (uint32_t)(bro[kk + 1] - b0);
+            uint32_t cur = 0;
+            if (wb != cmin) {                           // lower_bound(wb) in the B row
+              uint32_t lo = 0, hi = len;
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (bcol[b0 + mid] < wb) lo = mid + 1;
+                else hi = mid;
+              }
+              cur = lo;
+            }
+            gfirst[g] = (uint32_t)t;
+            gb0[g] = b0;
+            glen[g] = len;
+            gcur[g] = cur;
+          }
+          if (t == NT - 1) {
+            s_ng = inc;
+            gfirst[inc] = ntot;
+          }
+        }
+        __syncthreads();
+        const int ne = (int)s_ng;
+        auto nextg = [&](int e) {
+          e++;
+          while (e < ne && gcur[e] >= glen[e]) e++;
+          return e;
+        };
+        // the k_sg_win pipeline over distinct k: columns of group e+2 and values of group
+        // e+1 in flight while group e is added into every member row's accumulator
+        int e = nextg(-1);
+        uint32_t off = 0, col = 0xffffffffu;
+        double val = 0.0;
+        if (e < ne) {
+          off = gcur[e];
+          const uint32_t j = off + t;
+          if (j < glen[e]) {
+            col = bcol[gb0[e] + j];
+            if (col <= we) val = ba[gb0[e] + j];
+          }
+        }
+        int e2 = e < ne ? nextg(e) : ne;
+        uint32_t col2 = 0xffffffffu;
+        if (e2 < ne) {
+          const uint32_t j = gcur[e2] + t;
+          if (j < glen[e2]) col2 = bcol[gb0[e2] + j];
+        }
+        while (e < ne) {
+          const int e3 = e2 < ne ? nextg(e2) : ne;
+          double val2 = 0.0;
+          if (e2 < ne && col2 <= we) val2 = ba[gb0[e2] + gcur[e2] + t];
+          uint32_t col3 = 0xffffffffu;
+          if (e3 < ne) {
+            const uint32_t j = gcur[e3] + t;
+            if (j < glen[e3]) col3 = bcol[gb0[e3] + j];
+          }
+          const bool in = col <= we;
+          if (in) {
+            const uint32_t q = col - wb;
+            const uint32_t u1 = gfirst[e + 1];
+            for (uint32_t u = gfirst[e]; u < u1; u++) {
+              double *p = &acc[(uint32_t)ut[u] * W + q];
+              *p = *p + val * ua[u];
+            }
+          }
+          const uint32_t n = (uint32_t)__syncthreads_count(in);   // layer k before k'
+          off += n;
+          if (n == (uint32_t)NT) {                     // more of this B row in the window
+            const uint32_t j = off + t;
+            col = 0xffffffffu;
+            if (j < glen[e]) {
+              col = bcol[gb0[e] + j];
+              if (col <= we) val = ba[gb0[e] + j];
+            }
+            continue;
+          }
+          if (t == 0) gcur[e] = off;
+          e = e2;
+          if (e < ne) off = gcur[e];
+          col = col2;
+          val = val2;
+          e2 = e3;
+          col2 = col3;
+        }
+        __syncthreads();
+      }
+      // emit the window of every tile row in column order (each thread a run of SPT slots)
+      for (int r = 0; r < nt; r++) {
+        uint32_t cc = 0;
+        for (int q = 0; q < SPT; q++) cc += acc[r * W + t * SPT + q] != 0.0 ? 1u : 0u;
+        const uint32_t inc = block_incl_scan<NT>(cc, wtot);
+        uint64_t o = xro[s_i[r]] + s_nout[r] + (inc - cc);
+        for (int q = 0; q < SPT; q++) {
+          const int sl = t * SPT + q;
+          const double v = acc[r * W + sl];
+          if (v != 0.0) {
+            xcol[o] = wb + (uint32_t)sl;
+            xa[o] = v;
+            o++;
+          }
+        }
+        uint32_t tot = 0;
+        for (int w = 0; w < NT / 64; w++) tot += wtot[w];
+        __syncthreads();
+        if (t == 0) s_nout[r] += tot;
+        __syncthreads();
+      }
+    }
+    if (t < nt) cnt2[s_i[t]] = s_nout[t];
+    __syncthreads();
+  }
+}
+
 // long rows: block per row, dense slab acc[cn] + stamp[cn] per resident block
 template <int MODE, int RAP = 0>
 __global__ __launch_bounds__(256) void k_spgemm_long(
@@ -2052,6 +2285,18 @@ static int sg_wsym() {
   return g_sg_wsym;
 }
 extern "C" void amgd_spgemm_set_wsym(int w) { g_sg_wsym = w; }
+// AMGD_SG_WT: rows per tile of the tiled windowed kernel k_sg_wt (4 or 8; 0: one row per
+// work-group, k_sg_win); windows of 1024 / 2048 columns only
+static int g_sg_wt = -1;
+static int sg_wt() {
+  if (g_sg_wt < 0) {
+    const char *e = getenv("AMGD_SG_WT");
+    g_sg_wt = e && *e ? atoi(e) : 0;
+    if (g_sg_wt != 0 && g_sg_wt != 4 && g_sg_wt != 8) g_sg_wt = 4;
+  }
+  return g_sg_wt;
+}
+extern "C" void amgd_spgemm_set_wt(int t) { g_sg_wt = t < 0 ? -1 : t; }
 static uint32_t sg_win_p0() {
   static long v = -1;
   if (v < 0) { const char *e = getenv("AMGD_SG_WIN_P0"); v = e ? atol(e) : 48; }
@@ -2463,11 +2708,26 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     hn[3] = wn[1];
     hn[4] = wn[3];
   }
+#define SG_WT(W_, T_, R_)                                                                         \
+  do {                                                                                          \
+    const int gt = (int)std::min<unsigned>((nrw + T_ - 1) / T_, 16384u);                       \
+    if (rap)                                                                                    \
+      k_sg_wt<W_, T_, 1><<<gt, 256, 0, s>>>(R_, nrw,    A->ro, A->col, A->a, B->ro, B->col,     \
+                                            B->a, cnt2, cnt, tcol, ta);                         \
+    else                                                                                        \
+      k_sg_wt<W_, T_, 0><<<gt, 256, 0, s>>>(R_, nrw,    A->ro, A->col, A->a, B->ro, B->col,     \
+                                            B->a, cnt2, cnt, tcol, ta);                         \
+  } while (0)
 #define SG_WIN(nr, rows_)                                                                       \
   if (nr) {                                                                                     \
     const unsigned nrw = (nr);                                                                  \
     const int g = (int)std::min<unsigned>(nrw, 16384u);                                         \
-    if (win == 1024 && rap)                                                                     \
+    const int wt = sg_wt();                                                                     \
+    if (wt == 4 && win == 2048) SG_WT(2048, 4, rows_);                                              \
+    else if (wt == 8 && win == 2048) SG_WT(2048, 8, rows_);                                         \
+    else if (wt == 4 && win == 1024) SG_WT(1024, 4, rows_);                                         \
+    else if (wt == 8 && win == 1024) SG_WT(1024, 8, rows_);                                         \
+    else if (win == 1024 && rap)                                                                \
       k_sg_win<1024, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
                                           B->a, cnt2, cnt, tcol, ta);                           \
     else if (win == 1024)                                                                       \
@@ -2546,6 +2806,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
                                                B->a, B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);
   }
 #undef SG_WIN
+#undef SG_WT
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
   uint64_t nz = amgd_scan_u64(cnt2, rn);

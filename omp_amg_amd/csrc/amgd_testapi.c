@@ -173,6 +173,9 @@ API void amgd_test_qf_stats(uint64_t *out) {
 
 /* whole-matrix SpMVs that ran row-sharded (multi-GPU) since the library loaded */
 extern uint64_t amgd_spmv_shard_calls(void);
+void amgd_spgemm_set_wt(int t);
+/* rows per tile of the tiled windowed SpGEMM (4, 8; 0: one row per work-group; -1: default) */
+API void amgd_test_spgemm_wt(int t) { amgd_spgemm_set_wt(t); }
 /* cap on live device bytes (0: none): the out-of-HBM path without filling 288 GB */
 API void amgd_test_hbm_cap(uint64_t bytes) { amgd_set_hbm_cap((size_t)bytes); }
 API uint64_t amgd_test_pool_inuse(void) { return amgd_pool_bytes_in_use(); }

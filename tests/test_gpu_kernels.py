@@ -115,6 +115,69 @@ def test_spgemm_kseq_long_b_rows(case, win):
     assert refops.same(Y, R)
 
 
+def _banded(rng, rn, kn, cn, width, dens, blen, span, ints=True, dups=False, empty_every=0):
+    """A: row i holds k in [i*kn/rn, +width) at density dens (neighbouring rows share most
+    k, like the Galerkin products' rows); B: rows of ~blen columns in a band of `span`"""
+    ro, cols, vals = [0], [], []
+    for i in range(rn):
+        if empty_every and i % empty_every == 0:
+            ro.append(len(cols))
+            continue
+        k0 = i * kn // rn
+        ks = [k for k in range(k0, min(kn, k0 + width)) if rng.random() < dens]
+        for k in ks:
+            v = float(rng.integers(-3, 4)) if ints else rng.standard_normal()
+            cols.append(k); vals.append(v)
+            if dups and rng.random() < 0.1:          # duplicate column: the last one wins
+                cols.append(k); vals.append(v + 1.0)
+        ro.append(len(cols))
+    A = refops.Csr(rn, kn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+    ro, cols, vals = [0], [], []
+    for k in range(kn):
+        c0 = k * (cn - span) // max(1, kn - 1)
+        c = np.sort(rng.choice(span, size=min(span, blen), replace=False)) + c0
+        v = rng.integers(-3, 4, size=len(c)).astype(float) if ints else rng.standard_normal(len(c))
+        cols += c.tolist(); vals += v.tolist(); ro.append(len(cols))
+    B = refops.Csr(kn, cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+    return A, B
+
+
+@pytest.mark.parametrize("wt", [0, 4, 8])
+@pytest.mark.parametrize("win", [1024, 2048])
+@pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span"])
+def test_spgemm_tiled_windows(case, win, wt):
+    """tiled windowed kernel (k_sg_wt: T = 4 / 8 rows per work-group walking the union of
+    their A rows in ascending k) vs the one-row kernel (wt 0) vs the host restatement:
+    overlapping neighbouring rows, A rows past one chunk (several unions per window),
+    duplicate A columns, exact cancellation, empty rows inside tiles, a row count that
+    leaves a partial last tile, outputs spanning many windows"""
+    rng = np.random.default_rng({"banded": 61, "long_a": 62, "dups_cancel": 63, "ragged": 64,
+                                 "wide_span": 65}[case])
+    if case == "banded":
+        A, B = _banded(rng, 301, 400, 6000, 60, 0.7, 150, 3000, ints=False)
+    elif case == "long_a":
+        A, B = _banded(rng, 70, 900, 8000, 400, 0.8, 100, 4000)
+    elif case == "dups_cancel":
+        A, B = _banded(rng, 157, 300, 5000, 50, 0.8, 160, 2500, dups=True)
+    elif case == "ragged":
+        A, B = _banded(rng, 203, 350, 7000, 90, 0.6, 120, 3500, empty_every=5)
+    else:
+        A, B = _banded(rng, 41, 500, 60000, 200, 0.7, 90, 30000)
+    assert B.a.size >= 64 * B.rn
+    R = refops.spgemm(A, B)
+    oa.spgemm_flat(False)
+    oa.spgemm_win(win)
+    oa.spgemm_wt(wt)
+    oa.route_stats(reset=True)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_win(-1)
+        oa.spgemm_wt(-1)
+    assert oa.route_stats(reset=True)["sg_win"] > 0
+    assert refops.same(X, R)
+
+
 @pytest.mark.parametrize("wsym", [0, 32768, 65536])
 @pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
 def test_spgemm_symbolic_windows(case, wsym):

@@ -39,6 +39,10 @@ def parse(path):
 
 def main():
     a, b = parse(sys.argv[1]), parse(sys.argv[2])
+    if not any(e[0][0] == "cons" for e in a) or not any(e[0][0] == "cons" for e in b):
+        # one trace predates the constraint lines: compare levels and skeleton lines only
+        a = [e for e in a if e[0][0] != "cons"]
+        b = [e for e in b if e[0][0] != "cons"]
     out = open(sys.argv[3], "w") if len(sys.argv) > 3 else sys.stdout
     n = min(len(a), len(b))
     first = None
