@@ -96,6 +96,8 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
         L.amgd_test_spgemm_wt.argtypes = [C.c_int]
+        L.amgd_test_qf_reuse.argtypes = [C.c_int]
+        L.amgd_test_sg_pattern.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
@@ -393,6 +395,18 @@ def spgemm_wt(t: int) -> None:
     """windowed SpGEMM rows per work-group: 4 / 8 = tiled kernel (union of the tile's A
     rows in ascending k), 0 = one row per work-group, -1 = default (environment / 4)"""
     lib().amgd_test_spgemm_wt(int(t))
+
+
+def qf_reuse(on: int) -> None:
+    """Q factors of supports unchanged since the previous interpolation iteration: 1 copy
+    (default), 0 refactor every support, -1 default / AMGD_QF_REUSE.  Same bits."""
+    lib().amgd_test_qf_reuse(int(on))
+
+
+def sg_pattern(on: int) -> None:
+    """constraint pattern W_skel*W_skel': 1 pattern-only product (default), 0 the full
+    product (values discarded by interp_lmop), -1 default.  Same bits."""
+    lib().amgd_test_sg_pattern(int(on))
 
 
 def spgemm_wsym(w: int) -> None:

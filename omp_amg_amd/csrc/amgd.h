@@ -106,8 +106,12 @@ dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J, const doub
 dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *vc);
 dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out);
 dcsr *amgd_drop_zeros(const dcsr *A);                      /* exactly-zero entries removed */
-dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask);  /* rows with mask==0 emptied */  /* perm: CSC idx -> CSR idx */
+dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask);  /* rows with mask==0 emptied */
+dcsr *amgd_cols_masked(const dcsr *A, const uint8_t *mask);  /* entries with mask[col]==0 dropped */
+uint64_t *amgd_perm_inverse(const uint64_t *p, uint64_t n);  /* q[p[t]] = t */
 dcsr *amgd_spgemm(const dcsr *A, const dcsr *B);           /* A*B, reference semantics */
+/* pattern of A*B, values unspecified nonzeros (operands with all values > 0) */
+dcsr *amgd_spgemm_pattern(const dcsr *A, const dcsr *B);
 dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *B);
 dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B);
 /* z = (y ? alpha*y + beta*t : beta*t) [* f] with t = M x summed in column order */
@@ -120,9 +124,10 @@ void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
 void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */
 void amgd_diag(const dcsr *A, double *D);
 enum { AMGD_DPLUS = 0, AMGD_DMINUS = 1, AMGD_DMULT = 2, AMGD_MULTD = 3,
-       AMGD_SCALE2 = 4, AMGD_SCALE_ABS = 5, AMGD_SCALE2_ABS = 6 };
+       AMGD_SCALE2 = 4, AMGD_SCALE_ABS = 5, AMGD_SCALE2_ABS = 6, AMGD_SCALE_ABS_T = 7 };
 void amgd_diag_op(dcsr *A, const double *D, int op);
-/* fused: SCALE2 a=(a*Dl[i])*Dr[col]; SCALE_ABS a=|a*Dl[i]|*Dr[col]; SCALE2_ABS a=|(a*Dl[i])*Dr[col]| */
+/* fused: SCALE2 a=(a*Dl[i])*Dr[col]; SCALE_ABS a=|a*Dl[i]|*Dr[col]; SCALE2_ABS a=|(a*Dl[i])*Dr[col]|;
+   SCALE_ABS_T a=|a*Dl[col]|*Dr[i] (SCALE_ABS of the transpose, entry by entry) */
 void amgd_diag_op2(dcsr *A, const double *Dl, const double *Dr, int op);
 void amgd_vals_abs(dcsr *A);
 void amgd_vals_sqr(dcsr *A);
@@ -201,6 +206,11 @@ void amgd_cs_mask3(uint32_t n, const double *m2, const uint8_t *mb, uint8_t *vc,
 dcsr *amgd_min_skel(const dcsr *R);
 /* Q factors of A restricted to each row-support of Wt (packed upper triangles) */
 double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out, uint64_t *qtotal);
+/* the same, copying the factor of every support identical to the previous call's (Wp, Qp,
+   qpoff: that call's Wt, factors and offsets; NULL: factor everything) */
+double *amgd_qfactor_reuse(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out, uint64_t *qtotal,
+                           const dcsr *Wp, const double *Qp, const uint64_t *qpoff);
+void amgd_qfactor_reuse_stats(uint64_t *reused, uint64_t *factored);
 void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
                  const double *u, const double *lambda, double *out);
 /* S := interp_lmop contributions (S pattern = W_skel*W_skel'); kpos from amgd_lmop_kpos */

@@ -743,7 +743,8 @@ struct BinLim {
 };
 // (columns cb <= c < ce only: a shard's range)
 __global__ void k_bin_nz(const uint64_t *wro, uint32_t cb, uint32_t ce, BinLim lim, int nb,
-                         uint32_t *lists, unsigned *cnt, uint64_t lstride) {
+                         uint32_t *lists, unsigned *cnt, uint64_t lstride,
+                         const uint8_t *skip = nullptr) {
   const uint64_t n = ce - cb;
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t c0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -755,7 +756,7 @@ __global__ void k_bin_nz(const uint64_t *wro, uint32_t cb, uint32_t ce, BinLim l
     for (int q = nb - 2; q >= 0; q--)
       if (nz <= lim.l[q]) bin = q;
     for (int q = 0; q < nb; q++) {
-      bool take = nz != 0 && bin == q;
+      bool take = nz != 0 && bin == q && !(skip && c < ce && skip[c]);
       unsigned p = wave_append(&cnt[q], take);
       if (take) lists[(uint64_t)q * lstride + p] = (uint32_t)c;
     }
@@ -997,6 +998,46 @@ static bool qfactor_split(uint32_t c, const dcsr *Wt, const dcsr *A, uint64_t w0
   return done;
 }
 
+// Reuse of the previous skeleton's factors (amgd_qfactor_reuse): a coarse point's Q
+// depends only on its support (row of Wt) and on A, fixed over a level's interpolation
+// loop; expand_support adds entries to a minority of the supports per iteration
+// (256^3: +0.004 % to +2 % entries in the late iterations that cost most), so every
+// support identical to the previous iteration's takes its packed triangle by copy --
+// the same bits the factor kernels would write again.
+static uint8_t *g_qskip = nullptr;          // per coarse point: 1 = copy (current call)
+static const double *g_qp_q = nullptr;      // the previous call's factors
+static const uint64_t *g_qp_off = nullptr;
+static uint64_t g_qf_reused = 0, g_qf_factored = 0;
+// 1 where row c of Wt equals row c of Wp (same length, same columns): one wavefront per row
+__global__ void k_supp_same(const uint64_t *ro, const uint32_t *col, const uint64_t *pro,
+                            const uint32_t *pcol, uint32_t rn, uint8_t *same, unsigned *nsame) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < rn;
+       c += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint64_t k0 = ro[c], n = ro[c + 1] - k0, p0 = pro[c];
+    bool eq = n == pro[c + 1] - p0 && n != 0;
+    for (uint64_t k = lane; eq && k < n; k += 64) {
+      const bool d = col[k0 + k] != pcol[p0 + k];
+      if (__ballot(d)) eq = false;
+    }
+    if (lane == 0) {
+      same[c] = eq ? 1 : 0;
+      if (eq) atomicAdd(nsame, 1u);
+    }
+  }
+}
+// copy the packed triangles of the skipped supports cb <= c < ce (one block per support)
+__global__ void k_qcopy(const uint8_t *skip, const uint64_t *wro, uint32_t cb, uint32_t ce,
+                        const uint64_t *poff, const double *Qp, const uint64_t *qoff, double *Q) {
+  for (uint64_t c = cb + blockIdx.x; c < ce; c += gridDim.x) {
+    if (!skip[c]) continue;
+    const uint64_t nz = wro[c + 1] - wro[c], tn = nz * (nz + 1) / 2;
+    const double *src = Qp + poff[c];
+    double *dst = Q + qoff[c];
+    for (uint64_t t = threadIdx.x; t < tn; t += blockDim.x) dst[t] = src[t];
+  }
+}
+
 // the factors of the coarse points cb <= c < ce (all tiers), into Q at qoff
 static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, double *Q,
                           uint32_t cb, uint32_t ce, uint64_t tot) {
@@ -1009,6 +1050,8 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
   const uint64_t L = (uint64_t)rn + 1;
   // bins: LDS 32 / 64 / 128, blocked 256 / 512 / 1024, huge
   constexpr int NB = 7, HUGE = 6;
+  // (a component split of a huge support factors a sub-matrix: no reuse in there)
+  const uint8_t *skip = g_qf_split_depth == 0 ? g_qskip : nullptr;
   uint32_t *lists = (uint32_t *)amgd_alloc(NB * L * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(32);
   amgd_memset(cnt, 0, 32);
@@ -1016,7 +1059,10 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
   if (ce > cb) {
     k_bin_nz<<<grid_for(ce - cb), 256, 0, s>>>(Wt->ro, cb, ce,
                                               BinLim{{QF_T0, QF_T1, QF_T2, 256, 512, QF_T3}}, NB,
-                                              lists, cnt, L);
+                                              lists, cnt, L, skip);
+    if (skip)
+      k_qcopy<<<(int)std::min<uint32_t>(ce - cb, 16384u), 256, 0, s>>>(skip, Wt->ro, cb, ce, g_qp_off,
+                                                                      g_qp_q, qoff, Q);
     KCHECK();
     amgd_d2h(hn, cnt, NB * 4);
   }
@@ -1206,15 +1252,32 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
 // Q factors of every coarse point.  Sharded (amgd_comm.hip): coarse points split
 // into contiguous ranges of equal factor work (nz^3), each rank factors its
 // ranges into the global Q, one allgatherv of the Q segments completes it.
-__global__ void k_qcost(const uint64_t *wro, uint32_t rn, uint64_t *cost) {
+// Supports past the blocked tiers (> 1024 points: the orphan supports) are factored
+// per connected component (qfactor_split) or by the sparse kernel, far below nz^3: their
+// cost is capped at nz^2 * 1024, so one huge support no longer takes a rank's whole share.
+__global__ void k_qcost(const uint64_t *wro, uint32_t rn, uint64_t *cost, const uint8_t *skip) {
   GRID_STRIDE(c, rn) {
     uint64_t nz = wro[c + 1] - wro[c];
-    cost[c] = nz * nz * nz + 1;
+    cost[c] = (skip && skip[c] ? nz * nz / 8 : nz <= 1024 ? nz * nz * nz : nz * nz * 1024) + 1;
   }
 }
 #define QF_SHARD_MIN (1ull << 30)   // factor work (sum nz^3) below which one GPU does all
+static int g_qf_reuse = -1;     // AMGD_QF_REUSE=0 / amgd_qfactor_set_reuse(0): refactor every support
+static int qf_reuse_on() {
+  if (g_qf_reuse < 0) { const char *e = getenv("AMGD_QF_REUSE"); g_qf_reuse = e && *e ? atoi(e) : 1; }
+  return g_qf_reuse;
+}
+extern "C" void amgd_qfactor_set_reuse(int on) { g_qf_reuse = on < 0 ? -1 : on; }
+extern "C" void amgd_qfactor_reuse_stats(uint64_t *reused, uint64_t *factored) {
+  *reused = g_qf_reused; *factored = g_qf_factored;
+}
 extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
                                 uint64_t *qtotal) {
+  return amgd_qfactor_reuse(Wt, A, qoff_out, qtotal, nullptr, nullptr, nullptr);
+}
+extern "C" double *amgd_qfactor_reuse(const dcsr *Wt, const dcsr *A, uint64_t **qoff_out,
+                                      uint64_t *qtotal, const dcsr *Wp, const double *Qp,
+                                      const uint64_t *qpoff) {
   hipStream_t s = amgd_s();
   const uint32_t rn = Wt->rn;
   const uint64_t L = (uint64_t)rn + 1;
@@ -1222,12 +1285,30 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
   if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
   uint64_t tot = amgd_scan_u64(qoff, rn);
   double *Q = (double *)amgd_alloc(tot * 8 + 8);
+  if (Wp && Qp && qpoff && Wp->rn == rn && rn && qf_reuse_on()) {
+    g_qskip = (uint8_t *)amgd_alloc((size_t)rn + 1);
+    unsigned *ns = (unsigned *)amgd_alloc(16);
+    amgd_memset(ns, 0, 4);
+    k_supp_same<<<grid_for((uint64_t)rn * 64, 256, 16384), 256, 0, s>>>(Wt->ro, Wt->col, Wp->ro, Wp->col,
+                                                                       rn, g_qskip, ns);
+    KCHECK();
+    unsigned hs = 0;
+    amgd_d2h(&hs, ns, 4);
+    amgd_free(ns);
+    g_qf_reused += hs;
+    g_qf_factored += rn - hs;
+    if (hs == 0) { amgd_free(g_qskip); g_qskip = nullptr; }
+    g_qp_q = Qp;
+    g_qp_off = qpoff;
+  } else {
+    g_qf_factored += rn;
+  }
   const int N = amgd_nshards();
   uint64_t work = 0;
   uint64_t *cost = nullptr;
   if (N > 1 && rn >= (uint32_t)N) {
     cost = (uint64_t *)amgd_alloc(L * 8);
-    k_qcost<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, cost);
+    k_qcost<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, cost, g_qskip);
     KCHECK();
     work = amgd_scan_u64(cost, rn);
   }
@@ -1246,6 +1327,9 @@ extern "C" double *amgd_qfactor(const dcsr *Wt, const dcsr *A, uint64_t **qoff_o
     amgd_allgatherv(1, &b, qo.data());
   }
   if (cost) amgd_free(cost);
+  if (g_qskip) { amgd_free(g_qskip); g_qskip = nullptr; }
+  g_qp_q = nullptr;
+  g_qp_off = nullptr;
   *qoff_out = qoff;
   if (qtotal) *qtotal = tot;
   return Q;

@@ -119,6 +119,13 @@ static dcsr *spgemm_via_t(const dcsr *A, const dcsr *At, const dcsr *B, const dc
   dcsr_free(&Xt);
   return X;
 }
+/* the same choice, but the transposed product is returned as it comes (*tr = 1) for a
+   caller that can go on in transposed form */
+static dcsr *spgemm_via_t_raw(const dcsr *A, const dcsr *At, const dcsr *B, const dcsr *Bt, int *tr) {
+  const uint64_t avg_at = At && At->rn ? At->nnz / At->rn : 0, avg_b = B->rn ? B->nnz / B->rn : 0;
+  *tr = !(!At || !Bt || avg_at < 64 || avg_at < 2 * avg_b);
+  return *tr ? amgd_spgemm(Bt, At) : amgd_spgemm(A, B);
+}
 
 /* ------------------------------------------------------------------------ */
 /* coarsen (amg_setup.c:2737)                                                */
@@ -423,7 +430,9 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
        so the product of the operands without them is the same matrix, values and
        pattern -- without the orphans' dense all-zero block of products. */
     dcsr *Wn = amgd_drop_zeros(W_skel), *Wnt = amgd_drop_zeros(fac->Wt);
-    fac->S = amgd_spgemm(Wn, Wnt);
+    /* lmop overwrites every value of S (interp_lmop zeroes St first, amg_setup.c:1609): the
+       pattern is all that is needed, and the skeleton values are all 1: no sum cancels */
+    fac->S = amgd_spgemm_pattern(Wn, Wnt);
     dcsr_free(&Wn); dcsr_free(&Wnt);
     ph(PH_SPAT);
     amgd_lmop(fac->S, W_skel, fac->kpos, fac->Wt, fac->Q, fac->qoff, au2);
@@ -494,12 +503,12 @@ static void solve_weights(dcsr **W, dcsr **Wt_out, const dcsr **W0, double *lam,
 
 
 
-/* find_support (amg_setup.c:1260) */
-static dcsr *find_support(const dcsr *R, double goal) {
+/* find_support (amg_setup.c:1260).  Rt / perm: R's transpose and its CSC -> CSR map
+   when the caller already made them (taken over and freed here), else NULL. */
+static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) {
   uint32_t nf = R->rn, nc = R->cn;
   dcsr *Rl = dcsr_copy(R);
-  uint64_t *perm = NULL;
-  dcsr *Rt = amgd_transpose(R, &perm);
+  if (!Rt) Rt = amgd_transpose(R, &perm);
   double *onec = dones(nc), *rs = dalloc(nf), *w = dalloc(nc), *w2 = dalloc(nc), *tmp = dalloc(nf);
   double *vv = dalloc(nc), *sumR = dalloc(nc);
   uint64_t cap = R->nnz + nc + 16, ns = 0;
@@ -602,15 +611,22 @@ static dcsr *find_support(const dcsr *R, double goal) {
    expand_support: the product is formed for those rows alone (rows are independent, so
    they carry exactly the reference's values; the others are never read) */
 typedef struct {
-  const dcsr *Af, *W0, *W0t, *Ar;
+  const dcsr *Af, *AfT, *W0, *W0t, *Ar;
   const double *Dfsqrti, *Dcs;
 } r0_ctx;
 static dcsr *scale_abs_scale(const dcsr *X, const double *Dl, const double *Dr);
 static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
   dcsr *Afb = amgd_rows_masked(c->Af, bad);
-  dcsr *AfbT = amgd_transpose(Afb, NULL);
+  /* (Af restricted to the bad rows)' only where spgemm_via_t will use it (its mean row is
+     nnz(Afb) / cols(Af)); from Af' by a column mask when the level keeps Af' (same
+     entries in the same order as the transpose), else by a transpose */
+  const uint64_t avg_at = c->Af->cn ? Afb->nnz / c->Af->cn : 0, avg_b = c->W0->rn ? c->W0->nnz / c->W0->rn : 0;
+  dcsr *AfbT = NULL;
+  if (avg_at >= 64 && avg_at >= 2 * avg_b)
+    AfbT = c->AfT ? amgd_cols_masked(c->AfT, bad) : amgd_transpose(Afb, NULL);
   dcsr *AfW0 = spgemm_via_t(Afb, AfbT, c->W0, c->W0t);
-  dcsr_free(&Afb); dcsr_free(&AfbT);
+  dcsr_free(&Afb);
+  if (AfbT) dcsr_free(&AfbT);
   dcsr *Arb = amgd_rows_masked(c->Ar, bad);
   dcsr *Arhat0 = amgd_mpm(1., AfW0, 1., Arb);
   dcsr_free(&AfW0); dcsr_free(&Arb);
@@ -620,8 +636,9 @@ static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
 }
 
 /* expand_support (amg_setup.c:907) */
-static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, const r0_ctx *r0c, double gamma) {
-  dcsr *M = find_support(R, gamma);
+static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, dcsr *Rt, uint64_t *perm,
+                            const r0_ctx *r0c, double gamma) {
+  dcsr *M = find_support(R, Rt, perm, gamma);
   ph(PH_FS);
   if (phases_on() && verbose())
     printf("    find_support: R %u x %u nnz %lu\n", R->rn, R->cn, (unsigned long)R->nnz);
@@ -684,7 +701,7 @@ static void trace_limit(int it) {
 }
 
 static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, const dcsr *Ar,
-                           double gamma2, double tol) {
+                           const dcsr *ArT, double gamma2, double tol) {
   uint32_t rnf = Af->rn, rnc = Ac->rn, cnc = Ac->cn, cnr = Ar->cn;
   double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
   amgd_diag(Af, Df);
@@ -714,6 +731,11 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
   dcsr *W = NULL;
   uint64_t prev_nnz = (uint64_t)-1;
   int it = 0;
+  /* the previous iteration's supports and factors: supports the expansion left
+     unchanged take their factor by copy (amgd_qfactor_reuse) */
+  dcsr *prevWt = NULL;
+  double *prevQ = NULL;
+  uint64_t *prevQoff = NULL;
   ph(PH_IPRE);
   for (;;) {
     it++;
@@ -723,7 +745,8 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     fac.Wt = amgd_transpose(W_skel, &wperm);
     fac.kpos = amgd_lmop_kpos(fac.Wt, wperm);
     amgd_free(wperm);
-    fac.Q = amgd_qfactor(fac.Wt, Af, &fac.qoff, NULL);
+    fac.Q = amgd_qfactor_reuse(fac.Wt, Af, &fac.qoff, NULL, prevWt, prevQ, prevQoff);
+    if (prevWt) { dcsr_free(&prevWt); amgd_free(prevQ); amgd_free(prevQoff); prevQ = NULL; prevQoff = NULL; }
     ph(PH_QF);
     dcsr *Wtmp;
     const dcsr *W0;
@@ -736,26 +759,57 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     dump_csr("W0", W0);
     dump_csr("Wtmp", Wtmp);
     dump_dev("lam_out", lam, (size_t)rnf * 8);
-    dcsr *AfW = spgemm_via_t(Af, AfT, Wtmp, Wtmp_t);
-    dcsr *Arhat = amgd_mpm(1., AfW, 1., Ar);
-    dcsr_free(&AfW); dcsr_free(&Wtmp_t);
-    ph(PH_AFW);
-    dcsr *Arr = amgd_mpm(1.0, Arhat, 1.0, Ar);
-    dcsr *ArW = amgd_mxmpoint(Wtmp, Arr);
-    dcsr_free(&Arr);
-    dcsr *ArWt = amgd_transpose(ArW, NULL);
-    amgd_colsum(ArWt, Dcs);                          /* sum(W.*(Arhat+Ar), 1) */
-    dcsr_free(&ArW); dcsr_free(&ArWt);
-    amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
-    amgd_vunary(Dcs, cnc, AMGD_V_INV);
-    amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
-    dcsr *R = scale_abs_scale(Arhat, Dfsqrti, Dcs);  /* |Dfsqrti*Arhat|*Dcsqrti */
-    dcsr *Rt = amgd_transpose(R, NULL);
+    /* Arhat = Af*W + Ar, R = |Dfsqrti*Arhat|*Dcs and R' (with its CSC -> CSR map, for
+       find_support).  Where Af*W runs as (W'*Af')' the product comes transposed: every
+       step from Arhat to R is entry-wise (mpm, mxmpoint, the scaling) and the column sums
+       of W.*(Arhat+Ar) are the row sums of its transpose, so the chain runs on the
+       transposes as they come -- the same entries, values and orders -- and only R is
+       transposed back, instead of AfW', W.*Arr and R each being transposed once. */
+    int trp = 0;
+    dcsr *AfWx = spgemm_via_t_raw(Af, AfT, Wtmp, Wtmp_t, &trp);
+    dcsr *R, *Rt;
+    uint64_t *Rperm = NULL;
+    if (!trp) {
+      dcsr *Arhat = amgd_mpm(1., AfWx, 1., Ar);
+      dcsr_free(&AfWx); dcsr_free(&Wtmp_t);
+      ph(PH_AFW);
+      dcsr *Arr = amgd_mpm(1.0, Arhat, 1.0, Ar);
+      dcsr *ArW = amgd_mxmpoint(Wtmp, Arr);
+      dcsr_free(&Arr);
+      dcsr *ArWt = amgd_transpose(ArW, NULL);
+      amgd_colsum(ArWt, Dcs);                        /* sum(W.*(Arhat+Ar), 1) */
+      dcsr_free(&ArW); dcsr_free(&ArWt);
+      amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+      amgd_vunary(Dcs, cnc, AMGD_V_INV);
+      amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+      R = scale_abs_scale(Arhat, Dfsqrti, Dcs);      /* |Dfsqrti*Arhat|*Dcsqrti */
+      dcsr_free(&Arhat);
+      /* R' with its CSC -> CSR map: find_support (expand_support) takes both over, so R
+         is transposed once per iteration */
+      Rt = amgd_transpose(R, &Rperm);
+    } else {
+      dcsr *ArhatT = amgd_mpm(1., AfWx, 1., ArT);   /* (Af*W + Ar)' */
+      dcsr_free(&AfWx);
+      ph(PH_AFW);
+      dcsr *ArrT = amgd_mpm(1.0, ArhatT, 1.0, ArT);
+      dcsr *ArWT = amgd_mxmpoint(Wtmp_t, ArrT);      /* (W.*Arr)' */
+      dcsr_free(&ArrT); dcsr_free(&Wtmp_t);
+      amgd_colsum(ArWT, Dcs);                        /* sum(W.*(Arhat+Ar), 1) */
+      dcsr_free(&ArWT);
+      amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+      amgd_vunary(Dcs, cnc, AMGD_V_INV);
+      amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+      Rt = ArhatT;                                   /* R' = |Dfsqrti*Arhat|*Dcsqrti, transposed */
+      amgd_diag_op2(Rt, Dfsqrti, Dcs, AMGD_SCALE_ABS_T);
+      uint64_t *p = NULL;
+      R = amgd_transpose(Rt, &p);                    /* p: R position -> R' position */
+      Rperm = amgd_perm_inverse(p, R->nnz);          /* R' position -> R position */
+      amgd_free(p);
+    }
     amgd_spmv(R, onesc, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w1);                         /* w1 = ((R*1)'*R)' */
     amgd_spmv(R, w1, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w2);                         /* w2 = ((R*w1)'*R)' */
-    dcsr_free(&Rt);
     amgd_vdiv_guard(r, w2, w1, cnc);
     double maxr = 0;
     uint64_t n = amgd_count_gt(r, cnc, gamma2, &maxr);
@@ -769,6 +823,8 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     prev_nnz = W_skel->nnz;
     ph(PH_R);
     if (n == 0 || w1m <= gamma2 || stalled) {
+      dcsr_free(&Rt);
+      amgd_free(Rperm);
       /* same skeleton, alpha and u: the factor's S and W0 are reused */
       solve_weights(&W, NULL, &W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
       double *wuc = dalloc(rnf);
@@ -776,18 +832,20 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
       amgd_scale_diag_match(W, v, wuc);
       amgd_free(wuc);
       ph(PH_FINAL);
-      dcsr_free(&Wtmp); dcsr_free(&Arhat);
+      dcsr_free(&Wtmp);
       dcsr_free(&R);
       factor_free(&fac);
       break;
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
-    r0_ctx r0c = {Af, W0, fac.W0t, Ar, Dfsqrti, Dcs};
-    dcsr *nsk = expand_support(W_skel, R, &r0c, gamma2);
+    r0_ctx r0c = {Af, AfT, W0, fac.W0t, Ar, Dfsqrti, Dcs};
+    dcsr *nsk = expand_support(W_skel, R, Rt, Rperm, &r0c, gamma2);
     dcsr_free(&W_skel);
     W_skel = nsk;
-    dcsr_free(&Wtmp); dcsr_free(&Arhat);
+    dcsr_free(&Wtmp);
     dcsr_free(&R);
+    prevWt = fac.Wt; prevQ = fac.Q; prevQoff = fac.qoff;   /* kept for the next factorization */
+    fac.Wt = NULL; fac.Q = NULL; fac.qoff = NULL;
     factor_free(&fac);
   }
   dcsr_free(&W_skel); dcsr_free(&Amt);
@@ -963,7 +1021,8 @@ static int setup_body(void *arg) {
     amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, rn, L->idc, L->idf);
     /* Af' for the transposed products (only where Af's rows are long enough to pay) */
     dcsr *AfT = Af->rn && Af->nnz >= 64ull * Af->rn ? amgd_transpose(Af, NULL) : NULL;
-    dcsr *W = interpolation(Af, AfT, Ac, Afc, gamma2, itol);
+    dcsr *Acf = amgd_transpose(Afc, NULL);           /* Afc' = A(C,F): interpolation and RAP */
+    dcsr *W = interpolation(Af, AfT, Ac, Afc, Acf, gamma2, itol);
     L->W = W;
     add_time(&g_st.t_interp_ms, &t0);
     /* --- Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) --- */
@@ -974,7 +1033,6 @@ static int setup_body(void *arg) {
     dcsr_free(&AfW);
     L->AfP = AfP;
     dcsr *WtAfP = amgd_spgemm(Wt, AfP);
-    dcsr *Acf = amgd_transpose(Afc, NULL);
     dcsr *AcfW = spgemm_via_t(Acf, Afc, W, Wt);      /* Acf' = Afc exactly */
     if (AfT) dcsr_free(&AfT);
     amgd_spgemm_set_timer(-1);

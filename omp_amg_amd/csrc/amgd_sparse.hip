@@ -431,6 +431,64 @@ extern "C" dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask) {
   return X;
 }
 
+// inverse of a permutation of 0..n-1: q[p[t]] = t
+__global__ void k_perm_inv(const uint64_t *p, uint64_t n, uint64_t *q) { GRID_STRIDE(t, n) q[p[t]] = t; }
+extern "C" uint64_t *amgd_perm_inverse(const uint64_t *p, uint64_t n) {
+  uint64_t *q = (uint64_t *)amgd_alloc(n * 8 + 8);
+  if (n) k_perm_inv<<<grid_for(n), 256, 0, amgd_s()>>>(p, n, q);
+  KCHECK();
+  return q;
+}
+// entries of A kept where mask[col] != 0 (shape unchanged, order within rows kept):
+// the transpose of rows_masked(B, mask) is cols_masked(B', mask), without a sort
+__global__ void k_colmask_count(const uint64_t *ro, const uint32_t *col, uint32_t rn,
+                                const uint8_t *m, uint64_t *cnt) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    uint64_t c = 0;
+    for (uint64_t k = ro[i] + lane; k < ro[i + 1]; k += 64) c += m[col[k]] ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) cnt[i] = c;
+  }
+}
+__global__ void k_colmask_fill(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t rn,
+                               const uint8_t *m, const uint64_t *xro, uint32_t *xcol, double *xa) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < rn;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    uint64_t o = xro[i];
+    const uint64_t k1 = ro[i + 1];
+    for (uint64_t k0 = ro[i]; k0 < k1; k0 += 64) {       // uniform trip count per wave
+      const uint64_t k = k0 + lane;
+      const bool keep = k < k1 && m[col[k]];
+      const unsigned long long b = __ballot(keep);
+      if (keep) {
+        const uint64_t p = o + (uint64_t)__popcll(b & below);
+        xcol[p] = col[k];
+        xa[p] = a[k];
+      }
+      o += (uint64_t)__popcll(b);
+    }
+  }
+}
+extern "C" dcsr *amgd_cols_masked(const dcsr *A, const uint8_t *mask) {
+  hipStream_t s = amgd_s();
+  uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
+  if (A->rn) k_colmask_count<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->rn, mask, cnt);
+  uint64_t nz = amgd_scan_u64(cnt, A->rn);
+  dcsr *X = (dcsr *)malloc(sizeof(dcsr));
+  X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
+  X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
+  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  if (A->rn && nz)
+    k_colmask_fill<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, mask, X->ro, X->col, X->a);
+  KCHECK();
+  return X;
+}
+
 // ---------------------------------------------------------------------------
 // SpMV: t_i = sum_j a_ij x_col(j), left to right from +0.0 (apply_M).
 // CSR-stream: a 256-thread block owns 256 consecutive rows and walks their
@@ -984,7 +1042,7 @@ __global__ __launch_bounds__(256) void k_diag_op_g(const uint64_t *ro, const uin
         a[first] = op == AMGD_DPLUS ? a[first] + Dl[i] : a[first] - Dl[i];
       continue;
     }
-    const double di = Dl[i];
+    const double di = op == AMGD_SCALE_ABS_T ? 0.0 : Dl[i];   // (_T: Dl is per column)
     for (uint64_t k = k0 + sub; k < k1; k += G) {
       double v = a[k];
       switch (op) {
@@ -992,6 +1050,7 @@ __global__ __launch_bounds__(256) void k_diag_op_g(const uint64_t *ro, const uin
         case AMGD_MULTD: v = v * Dl[col[k]]; break;
         case AMGD_SCALE2: v = (v * di) * Dr[col[k]]; break;
         case AMGD_SCALE_ABS: v = fabs(v * di) * Dr[col[k]]; break;
+        case AMGD_SCALE_ABS_T: v = fabs(v * Dl[col[k]]) * Dr[i]; break;
         default: v = fabs((v * di) * Dr[col[k]]); break;
       }
       a[k] = v;
@@ -1592,7 +1651,7 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
             const uint32_t st = lo ? wend[lo - 1] : 0u;
             const uint64_t kb = wbst[lo] + (q - st);
             jq[u] = bcol[kb];
-            if (MODE) pq[u] = ba[kb] * wav[lo];
+            if (MODE == 1) pq[u] = ba[kb] * wav[lo];
             lq[u] = lo;
           }
         }
@@ -1636,6 +1695,8 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
                 __syncthreads();
               }
             }
+          } else if (MODE == 2) {          // pattern only: any order, a nonzero mark
+            if (v) hv[sl] = 1.0;
           }
           __syncthreads();
         }
@@ -1724,8 +1785,8 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
         const uint32_t ja = jj + t, jb = jj + NT + t;
         fa = ja < L;
         fb = jb < L;
-        if (fa) { xa_ = bcol[b0 + ja]; if (MODE) ya = ba[b0 + ja]; }
-        if (fb) { xb_ = bcol[b0 + jb]; if (MODE) yb = ba[b0 + jb]; }
+        if (fa) { xa_ = bcol[b0 + ja]; if (MODE == 1) ya = ba[b0 + ja]; }
+        if (fb) { xb_ = bcol[b0 + jb]; if (MODE == 1) yb = ba[b0 + jb]; }
       };
       auto step = [&]() {                           // the chunk after (fe, fj)
         if (fe >= ne) return;
@@ -1750,12 +1811,14 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
         const double a = MODE ? wav[ce[0]] : 0.0;
         if (va[0]) {
           const uint32_t sl = sg_insert<LG>(hk, ca[0], &nfill, MODE == 0);
-          if (MODE) hv[sl] = hv[sl] + pa[0] * a;
+          if (MODE == 1) hv[sl] = hv[sl] + pa[0] * a;
+          else if (MODE == 2) hv[sl] = 1.0;          // pattern only: a nonzero mark
           else if (sl == EMPTY_KEY) ovf = 1;
         }
         if (vb[0]) {
           const uint32_t sl = sg_insert<LG>(hk, cb[0], &nfill, MODE == 0);
-          if (MODE) hv[sl] = hv[sl] + pb[0] * a;
+          if (MODE == 1) hv[sl] = hv[sl] + pb[0] * a;
+          else if (MODE == 2) hv[sl] = 1.0;
           else if (sl == EMPTY_KEY) ovf = 1;
         }
         if (MODE == 0 && (ovf || nfill > cap)) break;   // racy LDS read: early exit only
@@ -2304,6 +2367,7 @@ static uint32_t sg_win_p0() {
 }
 static int g_sg_slot = -1;
 static uint64_t g_sg_bytes = 0;
+static int g_sg_pattern = 0;    // amgd_spgemm_pattern: hash-bin rows emit the pattern only
 extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
 extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; }
 extern "C" uint64_t amgd_spgemm_bytes(void) { return g_sg_bytes; }
@@ -2671,7 +2735,10 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
 #define SG_NUM(KER, NT, LG, bin, gmax)                                                          \
   if (hn[bin]) {                                                                                \
-    if (rap)                                                                                    \
+    if (pat)                                                                                    \
+      KER<NT, LG, 2, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
+          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
+    else if (rap)                                                                               \
       KER<NT, LG, 1, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
     else                                                                                        \
@@ -2679,6 +2746,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
           lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
   }
   const bool rap = g_sg_slot >= 0;
+  const bool pat = g_sg_pattern != 0;
   if (ntiny)
     k_sg_tiny<1><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
                                                             B->col, B->a, cnt2, cnt, tcol, ta);
@@ -2927,6 +2995,33 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   return X;
 }
 
+// Pattern of A*B with the values left unspecified (every stored value is nonzero; the
+// caller overwrites them): for operands whose stored values are all > 0 no sum can
+// cancel, so the exact-zero drop of the reference's mxm removes nothing and the
+// structural pattern IS the product's pattern.  The hash-bin rows then need no
+// ordered numeric pass: keys are inserted in any order (no per-layer barrier, no value
+// loads) and emitted sorted.  Falls back to amgd_spgemm when a value is not > 0.
+__global__ void k_allpos(const double *a, uint64_t n, unsigned *bad) {
+  GRID_STRIDE(k, n) if (!(a[k] > 0.0)) *bad = 1u;
+}
+static int g_sg_pat_on = 1;     // amgd_spgemm_set_pattern(0): full products (A/B runs)
+extern "C" void amgd_spgemm_set_pattern(int on) { g_sg_pat_on = on < 0 ? 1 : on; }
+extern "C" dcsr *amgd_spgemm_pattern(const dcsr *A, const dcsr *B) {
+  if (!g_sg_pat_on) return amgd_spgemm(A, B);
+  unsigned *bad = (unsigned *)amgd_alloc(16);
+  amgd_memset(bad, 0, 4);
+  if (A->nnz) k_allpos<<<grid_for(A->nnz), 256, 0, amgd_s()>>>(A->a, A->nnz, bad);
+  if (B->nnz) k_allpos<<<grid_for(B->nnz), 256, 0, amgd_s()>>>(B->a, B->nnz, bad);
+  KCHECK();
+  unsigned hb = 0;
+  amgd_d2h(&hb, bad, 4);
+  amgd_free(bad);
+  if (hb) return amgd_spgemm(A, B);
+  g_sg_pattern = 1;
+  dcsr *X = amgd_spgemm(A, B);
+  g_sg_pattern = 0;
+  return X;
+}
 __global__ void k_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *sa,
                                const uint64_t *dro, uint32_t rn, uint32_t *dcol, double *da) {
   GRID_STRIDE(i, rn) {

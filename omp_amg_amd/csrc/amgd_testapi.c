@@ -32,7 +32,8 @@ static void down(const dcsr *A, hcsr *H) {
   amgd_d2h(H->a, A->a, A->nnz * 8);
 }
 
-/* op: 0 spgemm(A,B)  1 transpose(A)  2 mpm(alpha,A,beta,B)  3 mxmpoint(A,B)  4 min_skel(A) */
+/* op: 0 spgemm(A,B)  1 transpose(A)  2 mpm(alpha,A,beta,B)  3 mxmpoint(A,B)  4 min_skel(A)
+       20 spgemm_pattern(A,B) */
 API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, double beta, hcsr *HX) {
   if (amgd_rt_init(0) != 0) return -1;
   dcsr *A = up(HA), *B = HB ? up(HB) : NULL, *X = NULL;
@@ -42,6 +43,7 @@ API int amgd_test_csr(int op, const hcsr *HA, const hcsr *HB, double alpha, doub
     case 2: X = amgd_mpm(alpha, A, beta, B); break;
     case 3: X = amgd_mxmpoint(A, B); break;
     case 4: X = amgd_min_skel(A); break;
+    case 20: X = amgd_spgemm_pattern(A, B); break;
     case 5: {                     /* Q factors of the supports (rows of A) on B; X.a = packed Q */
       uint64_t tot = 0, *qoff = NULL;
       double *Q = amgd_qfactor(A, B, &qoff, &tot);
@@ -176,6 +178,30 @@ extern uint64_t amgd_spmv_shard_calls(void);
 void amgd_spgemm_set_wt(int t);
 /* rows per tile of the tiled windowed SpGEMM (4, 8; 0: one row per work-group; -1: default) */
 API void amgd_test_spgemm_wt(int t) { amgd_spgemm_set_wt(t); }
+/* cols_masked(A, mask) and transpose(rows_masked(B, mask)) for the same mask: equal */
+API int amgd_test_cols_masked(const hcsr *HA, const uint8_t *hmask, hcsr *HX) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA);
+  uint8_t *m = (uint8_t *)amgd_alloc((size_t)A->cn + 1);
+  amgd_h2d(m, hmask, A->cn);
+  dcsr *X = amgd_cols_masked(A, m);
+  down(X, HX);
+  dcsr_free(&X); dcsr_free(&A);
+  amgd_free(m);
+  return 0;
+}
+void amgd_qfactor_set_reuse(int on);
+API void amgd_test_qf_reuse(int on) { amgd_qfactor_set_reuse(on); }
+void amgd_spgemm_set_pattern(int on);
+API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }
+/* Q factors taken by copy from the previous iteration / factored, since the last call */
+API void amgd_test_qf_reuse_stats(uint64_t *out) {
+  static uint64_t r0 = 0, f0 = 0;
+  uint64_t r, f;
+  amgd_qfactor_reuse_stats(&r, &f);
+  out[0] = r - r0; out[1] = f - f0;
+  r0 = r; f0 = f;
+}
 /* cap on live device bytes (0: none): the out-of-HBM path without filling 288 GB */
 API void amgd_test_hbm_cap(uint64_t bytes) { amgd_set_hbm_cap((size_t)bytes); }
 API uint64_t amgd_test_pool_inuse(void) { return amgd_pool_bytes_in_use(); }

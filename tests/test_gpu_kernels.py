@@ -178,6 +178,63 @@ def test_spgemm_tiled_windows(case, win, wt):
     assert refops.same(X, R)
 
 
+@pytest.mark.parametrize("case", ["short", "long_b", "wide", "tiny", "nonpositive"])
+def test_spgemm_pattern(case):
+    """amgd_spgemm_pattern (the constraint operator's pattern W_skel * W_skel'): operands
+    with all values > 0 give exactly mxm's pattern (no sum can cancel), every stored value
+    nonzero; any value <= 0 falls back to the full product (same bits as mxm)"""
+    rng = np.random.default_rng({"short": 71, "long_b": 72, "wide": 73, "tiny": 74, "nonpositive": 75}[case])
+    if case == "short":
+        A, B = refops.rand_csr(rng, 400, 300, 0.02), refops.rand_csr(rng, 300, 350, 0.02)
+    elif case == "long_b":
+        A, B = refops.rand_csr(rng, 300, 200, 0.03), refops.rand_csr(rng, 200, 3000, 0.04)
+    elif case == "wide":
+        A, B = refops.rand_csr(rng, 60, 300, 0.3), refops.rand_csr(rng, 300, 9000, 0.03)
+    elif case == "tiny":
+        A, B = refops.rand_csr(rng, 3000, 500, 0.002), refops.rand_csr(rng, 500, 400, 0.006)
+    else:
+        A, B = refops.rand_csr(rng, 200, 150, 0.05, ints=True), refops.rand_csr(rng, 150, 300, 0.1, ints=True)
+    if case != "nonpositive":
+        A = refops.Csr(A.rn, A.cn, A.row_off, A.col, np.ones_like(A.a))
+        B = refops.Csr(B.rn, B.cn, B.row_off, B.col, np.abs(B.a) + 0.5)
+    R = refops.spgemm(A, B)
+    X = oa.test_csr_op(20, A, B)
+    assert np.array_equal(X.row_off, R.row_off) and np.array_equal(X.col, R.col)
+    assert np.all(X.a != 0.0)
+    if case == "nonpositive":
+        assert refops.same(X, R)
+
+
+@pytest.mark.parametrize("seed", [81, 82])
+def test_cols_masked_is_transpose_of_rows_masked(seed):
+    """R0 rows (expand_support): (rows_masked(Af, bad))' is built as cols_masked(Af', bad)
+    -- the same entries in the same order as the transpose, short and long rows"""
+    import ctypes as C
+    rng = np.random.default_rng(seed)
+    B = refops.rand_csr(rng, 700, 500, 0.02 if seed == 81 else 0.3)
+    bad = (rng.random(B.rn) < 0.4).astype(np.uint8)
+    Bm = refops.Csr(B.rn, B.cn, *_rows_masked(B, bad))
+    R = refops.transpose(Bm)
+    Bt = refops.transpose(B)
+    L = oa.lib()
+    L.amgd_test_cols_masked.argtypes = [C.POINTER(oa.HCsr), C.c_void_p, C.POINTER(oa.HCsr)]
+    ha = oa._to_hcsr(Bt.row_off, Bt.col, Bt.a, Bt.rn, Bt.cn)
+    hx = oa.HCsr()
+    assert L.amgd_test_cols_masked(C.byref(ha), bad.ctypes.data, C.byref(hx)) == 0
+    X = oa._from_hcsr(hx)
+    assert refops.same(X, R)
+
+
+def _rows_masked(B, m):
+    ro, cols, vals = [0], [], []
+    for i in range(B.rn):
+        if m[i]:
+            s, e = B.row_off[i], B.row_off[i + 1]
+            cols += B.col[s:e].tolist(); vals += B.a[s:e].tolist()
+        ro.append(len(cols))
+    return np.array(ro), np.array(cols, dtype=np.int64), np.array(vals)
+
+
 @pytest.mark.parametrize("wsym", [0, 32768, 65536])
 @pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
 def test_spgemm_symbolic_windows(case, wsym):

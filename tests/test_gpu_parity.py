@@ -215,3 +215,30 @@ def test_gpu_fs_incremental_matches_full(gen, monkeypatch):
     h_full = abi.run_setup(oa.lib(), Ai, Aj, Av)
     bad = parity.compare(h_full, h_inc, exact=True)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("gen", [("p7_24", lambda: problems.poisson3d(24)),
+                                 ("p27_14", lambda: problems.poisson3d(14, 27)),
+                                 ("sem_e3_N4", lambda: problems.sem_laplacian(3, 3, 3, 4, seed=2, jitter=0.3))],
+                         ids=lambda g: g[0])
+def test_gpu_qfactor_reuse_matches_refactor(gen):
+    """Q factors of supports the skeleton expansion left unchanged are copied from the
+    previous interpolation iteration: hierarchy bit-identical to refactoring every
+    support (AMGD_QF_REUSE=0), and the copy path is taken"""
+    import ctypes as C
+    Ai, Aj, Av = gen[1]()
+    L = oa.lib()
+    L.amgd_test_qf_reuse_stats.argtypes = [C.POINTER(C.c_uint64)]
+    st = (C.c_uint64 * 2)()
+    L.amgd_test_qf_reuse_stats(st)
+    h_re = abi.run_setup(L, Ai, Aj, Av)
+    L.amgd_test_qf_reuse_stats(st)
+    assert st[0] > 0, "no factor was reused"
+    L.amgd_test_qf_reuse.argtypes = [C.c_int]
+    L.amgd_test_qf_reuse(0)
+    try:
+        h_full = abi.run_setup(L, Ai, Aj, Av)
+    finally:
+        L.amgd_test_qf_reuse(-1)
+    bad = parity.compare(h_full, h_re, exact=True)
+    assert not bad, bad
