@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_wt.argtypes = [C.c_int]
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
+        L.amgd_test_fs_fused.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
@@ -358,7 +359,7 @@ def qf_stats() -> dict:
 
 
 ROUTES = ("spmv_lane", "mv_long", "sg_tiny", "sg_kseq", "sg_win", "sg_wsym", "sg_long",
-          "cs_inc", "fs_inc", "sg_row")
+          "cs_inc", "fs_inc", "sg_row", "fs_fused", "qf_reuse")
 
 
 def route_stats(reset: bool = True) -> dict:
@@ -401,6 +402,12 @@ def qf_reuse(on: int) -> None:
     """Q factors of supports unchanged since the previous interpolation iteration: 1 copy
     (default), 0 refactor every support, -1 default / AMGD_QF_REUSE.  Same bits."""
     lib().amgd_test_qf_reuse(int(on))
+
+
+def fs_fused(on: int) -> None:
+    """find_support: 1 the sweep's w = R' rs also keeps each column's argmax for the
+    selection (default), 0 a separate selection pass, -1 default.  Same bits."""
+    lib().amgd_test_fs_fused(int(on))
 
 
 def sg_pattern(on: int) -> None:

@@ -67,7 +67,8 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
 /* kernel-route counters (which default paths a setup took; read by the parity tests
    at sizes where the default routing engages) */
 enum { AMGD_R_SPMV_LANE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WIN,
-       AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW, AMGD_R_N };
+       AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
+       AMGD_R_FS_FUSED, AMGD_R_QF_REUSE, AMGD_R_N };
 extern uint64_t amgd_route_ctr[16];
 #define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
 
@@ -119,6 +120,9 @@ void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const do
                double beta, const uint8_t *f);
 /* z[list[r]] = row list[r] of M times x (x == NULL: row sums), left to right */
 void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x, double *z);
+/* z = M x plus per row the largest product and its first entry position (amx, apos);
+   returns 0 (nothing done) where only the separate product + selection applies */
+int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos);
 /* z = M^T x, per column in ascending row order; Mt = transpose(M) */
 void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
 void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */
@@ -226,7 +230,9 @@ void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] s
    an entry */
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                         const double *w, double *sumR, double thr,
-                        uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
+                        uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved,
+                        const uint64_t *apos);   /* apos: per-column argmax of the sweep's w
+                                                    product (amgd_spmv_amax), or NULL */
 /* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
    returns the count, > cap when the list overflowed */
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,

@@ -1296,6 +1296,7 @@ extern "C" double *amgd_qfactor_reuse(const dcsr *Wt, const dcsr *A, uint64_t **
     amgd_d2h(&hs, ns, 4);
     amgd_free(ns);
     g_qf_reused += hs;
+    if (hs) amgd_route_hit(AMGD_R_QF_REUSE);
     g_qf_factored += rn - hs;
     if (hs == 0) { amgd_free(g_qskip); g_qskip = nullptr; }
     g_qp_q = Qp;
@@ -2115,6 +2116,20 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     }
   }
 }
+// the same selection from the argmax the fused product w = R' rs kept per column
+// (amgd_spmv_amax: the same products, first position of the maximum)
+__global__ void k_fs_select_cached(const uint32_t *trow, const uint64_t *perm, double *ta, double *a,
+                                   const uint64_t *apos, const uint32_t *list, const unsigned *nlist,
+                                   uint32_t *si, uint32_t *sj, unsigned *removed) {
+  const uint32_t n = *nlist;
+  GRID_STRIDE(r, n) {
+    const uint32_t c = list[r];
+    const uint64_t best = apos[c];
+    si[r] = best != ~0ull ? trow[best] : 0u;
+    sj[r] = c;
+    if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
+  }
+}
 // bad columns past fs_long() entries: one 1024-thread block each (k_fs_select skips them);
 // llist holds their slots in the bad list
 __global__ __launch_bounds__(1024) void k_fs_select_long(const uint64_t *tro, const uint32_t *trow,
@@ -2285,14 +2300,18 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
                                    double *rs, const double *w, double *sumR,
                                    double thr, uint32_t *sel_i, uint32_t *sel_j,
-                                   uint32_t *nremoved) {
+                                   uint32_t *nremoved, const uint64_t *apos) {
   hipStream_t s = amgd_s();
   const uint32_t nc = Rt->rn;
   uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(16);
   amgd_memset(cnt, 0, 16);
   uint32_t *llist = nullptr;
-  if (nc) {
+  if (nc && apos) {
+    k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
+    k_fs_select_cached<<<grid_for(nc), 256, 0, s>>>(Rt->col, perm, Rt->a, Rl->a, apos, list, cnt + 2,
+                                                    sel_i, sel_j, cnt + 1);
+  } else if (nc) {
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
     llist = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
     const uint32_t ml = fs_long(Rt);

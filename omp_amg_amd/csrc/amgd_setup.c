@@ -541,10 +541,14 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
   uint64_t prev_off = 0;
   uint32_t prev_nsel = 0;
   const int fslog = getenv("AMGD_FSLOG") != NULL;
+  /* full sweeps on long-row R': w = R'*rs keeps each column's argmax of R(i,c)*rs_i,
+     the very products the selection compares, so the selection needs no second pass */
+  double *amx = dalloc(nc);
+  uint64_t *apos = (uint64_t *)amgd_alloc((size_t)nc * 8 + 8);
   ph(PH_FS);
   for (;;) {
     it++;
-    int done = 0;
+    int done = 0, fused = 0;
     uint32_t n1 = 0, n2 = 0, n3 = 0;
     double t0 = 0, t1 = 0;
     if (fslog) { amgd_sync(); t0 = amgd_wtime(); }
@@ -566,7 +570,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
       }
     }
     if (!done) {
-      amgd_spmvt(Rt, rs, w);                              /* w = R'*rs (row order) */
+      fused = amgd_spmv_amax(Rt, rs, w, amx, apos);       /* w = R'*rs (row order) */
+      if (!fused) amgd_spmvt(Rt, rs, w);
       amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       amgd_spmvt(Rt, tmp, w2);                            /* w2 = R'*(R*w) */
     }
@@ -579,7 +584,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
-    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem,
+                                   fused ? apos : NULL);
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
@@ -602,6 +608,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
     amgd_free(st_r); amgd_free(st_c); amgd_free(L1); amgd_free(L2); amgd_free(L3);
   }
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
+  amgd_free(amx); amgd_free(apos);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);
   return Sk;

@@ -12,6 +12,7 @@
 //   * mpm / mxmpoint (amg_setup.c:1684 / 1807): sorted merges, zero-drop rule.
 // Compiled with -ffp-contract=off: no FMA contraction (the reference is ISO C).
 #include <hip/hip_runtime.h>
+#include <cfloat>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -623,13 +624,16 @@ __device__ __forceinline__ T ld_stream(const T *p) {
   if constexpr (NTL) return __builtin_nontemporal_load(p);
   else return *p;
 }
-template <bool LIST, int RW, bool NTL = false>
+// AMX: the adding lanes also keep each row's largest product and its first position
+// (find_support's selection, amg_setup.c:1343-1364, reads exactly these products)
+template <bool LIST, int RW, bool NTL = false, bool AMX = false>
 __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
                                                    double beta, const uint8_t *f,
-                                                   uint32_t maxlen = 0xffffffffu) {
+                                                   uint32_t maxlen = 0xffffffffu,
+                                                   double *amx = nullptr, uint64_t *apos = nullptr) {
   constexpr int SEG = 1024 / RW;
   __shared__ double buf[4][RW][SEG + 1];
   __shared__ uint64_t rk0[4][RW];
@@ -654,6 +658,8 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double t = 0;
+    double pmx = -DBL_MAX;           // AMX: largest product, its entry (first on ties)
+    uint64_t ppos = ~0ull;
     // round `off`'s products sit in v[]; the next round's (a, col) loads are
     // issued before the lanes add the current round, so HBM latency overlaps
     // the ordered adds (the sums and their order are unchanged)
@@ -703,9 +709,18 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
             for (int e = 0; e < 16; e++) u[e] = buf[w][lane][e0 + e];
 #pragma unroll
             for (int e = 0; e < 16; e++) t += u[e];
+            if (AMX) {
+#pragma unroll
+              for (int e = 0; e < 16; e++)
+                if (u[e] > pmx) { pmx = u[e]; ppos = rk0[w][lane] + off + e0 + e; }
+            }
           }
         } else {
-          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+          for (uint32_t e = 0; e < m; e++) {
+            const double u = buf[w][lane][e];
+            t += u;
+            if (AMX && u > pmx) { pmx = u; ppos = rk0[w][lane] + off + e; }
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -718,6 +733,7 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
+      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
     }
   }
 }
@@ -942,6 +958,38 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
     k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   }
   KCHECK();
+}
+// z = M x and, per row, the largest product M(i,k) x_k with its first entry position
+// (find_support: w = R' rs and the selection's argmax of R(i,c) rs_i per column c, in one
+// pass over R').  Only the whole-matrix lane kernel path (long rows, one GPU); returns 0
+// where that path does not apply -- the caller then multiplies and selects separately.
+static int g_fs_fused = -1;     // AMGD_FS_FUSED=0 / amgd_spmv_set_fused(0): separate selection pass
+extern "C" void amgd_spmv_set_fused(int on) { g_fs_fused = on < 0 ? -1 : on; }
+extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos) {
+  if (M->rn == 0 || amgd_nshards() > 1 || M->nnz < 32ull * M->rn || (int64_t)M->rn < sl_min_whole())
+    return 0;
+  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 1; }
+  if (!g_fs_fused) return 0;
+  const int rw_ = lane_rw(M->rn);
+  const int g_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
+  amgd_route_hit(AMGD_R_SPMV_LANE);
+  amgd_route_hit(AMGD_R_FS_FUSED);
+  amgd_timer_start(1);
+  if (rw_ == 64)
+    k_spmv_lane<false, 64, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                                0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
+  else if (rw_ == 16)
+    k_spmv_lane<false, 16, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                                0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
+  else
+    k_spmv_lane<false, 4, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
+  amgd_timer_stop(1);
+  KCHECK();
+  const uint64_t rest = 16ull * M->rn + 8;
+  g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
+  g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
+  return 1;
 }
 // rows-filtered SpMV (k_spmv arithmetic at any row length): z_i = (M x)_i * f_i on
 // the 256-row blocks holding a row i with fs[i] - fb <= fr

@@ -54,6 +54,8 @@ CASES = {
     "aniso_48": ("oracle", {"kind": "poisson3d", "m": 48, "eps": 1e-3}),
     "p27_20": ("oracle", {"kind": "poisson3d", "m": 20, "stencil": 27}),
     "p27_24": ("oracle", {"kind": "poisson3d", "m": 24, "stencil": 27}),
+    "p27_28": ("oracle", {"kind": "poisson3d", "m": 28, "stencil": 27}),
+    "p27_32": ("oracle", {"kind": "poisson3d", "m": 32, "stencil": 27}),
     "sem_e3_N7": ("reference", {"kind": "sem", "e": 3, "N": 7, "seed": 1, "jitter": 0.3}),
     "sem_e4_N7": ("oracle", {"kind": "sem", "e": 4, "N": 7, "seed": 1, "jitter": 0.3}),
     "sem_e5_N7": ("oracle", {"kind": "sem", "e": 5, "N": 7, "seed": 3, "jitter": 0.3}),

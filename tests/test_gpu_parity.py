@@ -242,3 +242,26 @@ def test_gpu_qfactor_reuse_matches_refactor(gen):
         L.amgd_test_qf_reuse(-1)
     bad = parity.compare(h_full, h_re, exact=True)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("gen", [("p7_32", lambda: problems.poisson3d(32)),
+                                 ("p27_16", lambda: problems.poisson3d(16, 27)),
+                                 ("sem_e4_N4", lambda: problems.sem_laplacian(4, 4, 4, 4, seed=5, jitter=0.3))],
+                         ids=lambda g: g[0])
+def test_gpu_fs_fused_select_matches_separate(gen):
+    """find_support's selection from the argmax kept by the fused w = R' rs product vs
+    the separate selection pass (and the lane path forced at every size): identical
+    hierarchies, and the fused path is taken"""
+    Ai, Aj, Av = gen[1]()
+    oa.spmv_sl_min(0)
+    try:
+        oa.route_stats(reset=True)
+        h_f = abi.run_setup(oa.lib(), Ai, Aj, Av)
+        assert oa.route_stats(reset=True)["fs_fused"] > 0
+        oa.fs_fused(0)
+        h_s = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.fs_fused(-1)
+        oa.spmv_sl_min(-1)
+    bad = parity.compare(h_s, h_f, exact=True)
+    assert not bad, bad

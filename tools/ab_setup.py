@@ -22,7 +22,7 @@ import omp_amg_amd as oa  # noqa: E402
 from omp_amg_amd import parity, problems  # noqa: E402
 
 HOOKS = {"wt": oa.spgemm_wt, "win": oa.spgemm_win, "wsym": oa.spgemm_wsym, "rw": oa.spmv_rw,
-         "qfr": oa.qf_reuse, "pat": oa.sg_pattern}
+         "qfr": oa.qf_reuse, "pat": oa.sg_pattern, "fused": oa.fs_fused}
 
 
 def digest(h):
