@@ -155,7 +155,7 @@ def pmc_traffic(m, stencil, world):
         d = json.load(open(f))
         w = d.get("workload", {"m": 256, "stencil": 7, "world": 1})   # r02 files: 256^3 7-point, 1 GPU
         if (w["m"], w["stencil"], w["world"]) == (m, stencil, world):
-            return d["spmv"]["hbm_bytes"], d["rap"]["hbm_bytes"], os.path.relpath(f, ROOT)
+            return d["spmv"], d["rap"], os.path.relpath(f, ROOT)
     return None, None, None
 
 
@@ -245,6 +245,7 @@ def main():
         warm += 1
     barrier()
     rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, mv_strict, st = 0.0, 0, 0, 0.0, 0, 0, None
+    mv_n, rap_n = 0, 0
     steps = 0
     if sharded:
         shard.stats(reset=True)
@@ -262,6 +263,8 @@ def main():
         mv_ms += st["spmv_kernel_ms"]
         mv_bytes += st["spmv_bytes"]
         mv_strict += st["spmv_bytes_strict"]
+        mv_n += st["spmv_launches"]
+        rap_n += st["rap_launches"]
         if rank == 0:
             print(f"[bench] step {steps}: {t_step:.2f} s", file=sys.stderr, flush=True)
     barrier()
@@ -277,11 +280,16 @@ def main():
     comm = shard.stats() if sharded else None
 
     if rank == 0:
-        t_mv, t_rap, t_src = pmc_traffic(args.m, args.stencil, world)
+        p_mv, p_rap, t_src = pmc_traffic(args.m, args.stencil, world)
+        t_mv = p_mv["hbm_bytes"] if p_mv else None          # PMC bytes per setup
+        t_rap = p_rap["hbm_bytes"] if p_rap else None
         if args.traffic is not None:
-            t_mv, t_src = args.traffic, "--traffic"
+            t_mv, t_src, p_mv = args.traffic, "--traffic", None
         if args.rap_traffic is not None:
-            t_rap = args.rap_traffic
+            t_rap, p_rap = args.rap_traffic, None
+        # per launch (the PMC run's own dispatch counts; this run's launch counts otherwise)
+        mv_lps = (p_mv or {}).get("dispatches") or (mv_n / steps if mv_n else None)
+        rap_lps = (p_rap or {}).get("dispatches") or (rap_n / steps if rap_n else None)
         achieved = rap_bytes / (rap_ms * 1e-3) / 1e9 if rap_ms > 0 else 0.0
         mv_achieved = mv_strict / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
         mv_gather = mv_bytes / (mv_ms * 1e-3) / 1e9 if mv_ms > 0 else 0.0
@@ -315,9 +323,13 @@ def main():
                                                           "t_interp_ms", "t_rap_ms")},
             "roofline": {"bound": "hbm", "achieved": mv_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": mv_achieved / HBM_PEAK_GBS,
-                         "traffic": t_mv,
-                         "traffic_unit": "bytes per setup (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic": t_mv / mv_lps if (t_mv and mv_lps) else None,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE / WRITE_SIZE, calibrated; "
+                                         "traffic_per_setup / launches_per_setup)",
+                         "traffic_per_setup": t_mv,
                          "traffic_source": t_src,
+                         "launches_per_setup": mv_n / steps,
+                         "algorithmic_bytes_per_launch": mv_strict / mv_n if mv_n else None,
                          "kernel": "k_spmv_lane<false,RW>: whole-matrix long-row SpMV (ordered row sums; "
                                    "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
                                    "HIP-event timed",
@@ -333,9 +345,12 @@ def main():
                                                             "bound on gather traffic, not the roofline"}},
             "rap_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": t_rap,
-                         "traffic_unit": "bytes per setup (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic": t_rap / rap_lps if (t_rap and rap_lps) else None,
+                         "traffic_unit": "HBM bytes per launch (PMC, calibrated; traffic_per_setup / launches)",
+                         "traffic_per_setup": t_rap,
                          "traffic_source": t_src,
+                         "traffic_over_algorithmic": t_rap * steps / rap_bytes if (t_rap and rap_bytes) else None,
+                         "launches_per_setup": rap_n / steps,
                          "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",

@@ -34,6 +34,7 @@ typedef struct {
   double spmv_kernel_ms;         /* whole-matrix long-row SpMV kernels (k_spmv_lane), event-timed */
   uint64_t spmv_bytes;           /* their bytes with x gathered once per entry */
   uint64_t spmv_bytes_strict;    /* their algorithmic HBM bytes: x read once per product */
+  uint64_t spmv_launches, rap_launches;   /* kernel launches behind spmv_/rap_kernel_ms */
 } amgd_stats;
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */

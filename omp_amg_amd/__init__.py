@@ -36,7 +36,8 @@ class AmgdStats(C.Structure):
                 ("rows0", C.c_uint64), ("nnz0", C.c_uint64),
                 ("nlevels", C.c_uint32), ("ub_events", C.c_uint32),
                 ("peak_bytes", C.c_size_t), ("spmv_kernel_ms", C.c_double),
-                ("spmv_bytes", C.c_uint64), ("spmv_bytes_strict", C.c_uint64)]
+                ("spmv_bytes", C.c_uint64), ("spmv_bytes_strict", C.c_uint64),
+                ("spmv_launches", C.c_uint64), ("rap_launches", C.c_uint64)]
 
 
 class HCsr(C.Structure):
@@ -99,6 +100,8 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
         L.amgd_test_fs_fused.argtypes = [C.c_int]
+        L.amgd_test_lmop_wave.argtypes = [C.c_int]
+        L.amgd_test_spmv_chunk.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
@@ -359,7 +362,7 @@ def qf_stats() -> dict:
 
 
 ROUTES = ("spmv_lane", "mv_long", "sg_tiny", "sg_kseq", "sg_win", "sg_wsym", "sg_long",
-          "cs_inc", "fs_inc", "sg_row", "fs_fused", "qf_reuse")
+          "cs_inc", "fs_inc", "sg_row", "fs_fused", "qf_reuse", "lmop_wave")
 
 
 def route_stats(reset: bool = True) -> dict:
@@ -404,10 +407,24 @@ def qf_reuse(on: int) -> None:
     lib().amgd_test_qf_reuse(int(on))
 
 
+def spmv_chunk(on: int) -> None:
+    """whole-matrix long-row SpMV: 1 contiguous 16-byte-load chunks (k_spmv_chunk) for
+    matrices whose mean row is < 256 entries, 2 chunks for every long-row matrix, 0 per-row
+    segments (k_spmv_lane) only (default), -1 default / AMGD_SPMV_CHUNK.  Same sums."""
+    lib().amgd_test_spmv_chunk(int(on))
+
+
 def fs_fused(on: int) -> None:
     """find_support: 1 the sweep's w = R' rs also keeps each column's argmax for the
-    selection (default), 0 a separate selection pass, -1 default.  Same bits."""
+    selection, 0 a separate selection pass (default), -1 default.  Same bits."""
     lib().amgd_test_fs_fused(int(on))
+
+
+def lmop_wave(n: int) -> None:
+    """interp_lmop general walk: chunks holding a support of >= n points replay sp_add's
+    walk one wavefront per (c, k) with 64 columns searched at once (default 64), 0 one
+    thread per (c, k) always, -1 default / AMGD_LMOP_WAVE.  Same landings."""
+    lib().amgd_test_lmop_wave(int(n))
 
 
 def sg_pattern(on: int) -> None:

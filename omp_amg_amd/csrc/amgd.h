@@ -68,7 +68,7 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
    at sizes where the default routing engages) */
 enum { AMGD_R_SPMV_LANE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WIN,
        AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
-       AMGD_R_FS_FUSED, AMGD_R_QF_REUSE, AMGD_R_N };
+       AMGD_R_FS_FUSED, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_N };
 extern uint64_t amgd_route_ctr[16];
 #define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
 

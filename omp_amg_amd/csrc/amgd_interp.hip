@@ -1012,6 +1012,7 @@ static uint64_t g_qf_reused = 0, g_qf_factored = 0;
 __global__ void k_supp_same(const uint64_t *ro, const uint32_t *col, const uint64_t *pro,
                             const uint32_t *pcol, uint32_t rn, uint8_t *same, unsigned *nsame) {
   const int lane = threadIdx.x & 63;
+  unsigned cnt = 0;
   for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < rn;
        c += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
     const uint64_t k0 = ro[c], n = ro[c + 1] - k0, p0 = pro[c];
@@ -1020,10 +1021,16 @@ __global__ void k_supp_same(const uint64_t *ro, const uint32_t *col, const uint6
       const bool d = col[k0 + k] != pcol[p0 + k];
       if (__ballot(d)) eq = false;
     }
-    if (lane == 0) {
-      same[c] = eq ? 1 : 0;
-      if (eq) atomicAdd(nsame, 1u);
-    }
+    if (lane == 0) same[c] = eq ? 1 : 0;
+    cnt += eq;
+  }
+  // one atomic per work-group (one per row serialised on a single address: ~11 ms a call)
+  __shared__ unsigned part[4];
+  if (lane == 0) part[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(nsame, t);
   }
 }
 // copy the packed triangles of the skipped supports cb <= c < ce (one block per support)
@@ -1687,6 +1694,86 @@ __global__ void k_lmop_land(const uint32_t *erow, uint64_t e0, uint64_t e1, cons
     }
   }
 }
+// The same walk, one wavefront per (c, k), for long supports (the orphan support of
+// a few thousand points: a thread's walk was a chain of nz binary searches).  The 64
+// lanes search the next 64 columns Qj[m..m+63] from the current position t at once.
+// Along a run of exact matches in the current row that IS the sequential walk: the
+// columns increase, so each earlier landing lies before the next column's position
+// and a search from t finds it.  The prefix of exact lanes is taken, then the first
+// non-exact step: its search from t equals the one from its predecessor's landing + 1
+// (everything in between is below its column) when it still lands in the row; a step
+// that leaves the row (column past the row's last) runs the row skip as before.
+__global__ __launch_bounds__(256) void k_lmop_land_wave(
+    const uint32_t *erow, uint64_t e0, uint64_t e1, const uint64_t *wro, const uint32_t *wcol,
+    const uint64_t *sro, const uint32_t *scol, uint32_t srn, uint64_t snnz, const int64_t *rmax,
+    const int64_t *b64, const int64_t *b4k, const uint64_t *coff, uint64_t cbase, uint64_t *key) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t e = e0 + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); e < e1;
+       e += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t c = erow[e];
+    const uint64_t w0 = wro[c];
+    const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t k = (uint32_t)(e - w0);
+    const uint32_t *Qj = wcol + w0;
+    const uint64_t o = coff[c] - cbase + (uint64_t)k * nz;
+    uint32_t r = Qj[k];
+    uint64_t t = sro[r];
+    bool live = sro[r + 1] != t;
+    uint32_t m = 0;
+    while (m < nz) {
+      if (!live) {
+        for (uint32_t q = m + lane; q < nz; q += 64) key[o + q] = snnz;
+        break;
+      }
+      const uint64_t end = sro[r + 1];
+      const uint32_t nv = min(64u, nz - m);
+      const bool valid = (uint32_t)lane < nv;
+      const uint32_t xm = valid ? Qj[m + lane] : 0u;
+      uint64_t L = end;
+      bool inrow = false, exact = false;
+      if (valid && t < end) {
+        L = lower_bound_u32(scol, t, end, xm);
+        inrow = L < end;                              // = rmax[r] >= xm
+        exact = inrow && scol[L] == xm;
+      }
+      const uint64_t vmask = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+      const uint64_t nonex = ~(uint64_t)__ballot(exact) & vmask;
+      const uint32_t f = nonex ? (uint32_t)(__ffsll((long long)nonex) - 1) : nv;
+      const bool finrow = f < nv && __shfl((int)inrow, (int)f, 64) != 0;
+      const uint32_t acc = f + (finrow ? 1u : 0u);
+      if ((uint32_t)lane < acc) key[o + m + lane] = L;
+      if (acc) {
+        t = __shfl((unsigned long long)L, (int)acc - 1, 64) + 1;
+        m += acc;
+      }
+      if (f < nv && !finrow) {                        // step m leaves row r (uniform)
+        const uint32_t xf = Qj[m];
+        const uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xf);
+        uint64_t land = snnz;
+        if (r2 >= srn) {
+          live = false;                               // reference runs off the end of St (UB)
+        } else {
+          r = r2;
+          land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xf);
+          t = land + 1;
+        }
+        if (lane == 0) key[o + m] = land;
+        m++;
+      }
+    }
+  }
+}
+static int g_lmop_wave = -1;          // test hook: -1 environment / default
+extern "C" void amgd_lmop_set_wave(int n) { g_lmop_wave = n; }
+static int lmop_land_wave_min() {     // support size from which the walk runs per wavefront
+  if (g_lmop_wave >= 0) return g_lmop_wave;
+  static int v = -2;
+  if (v == -2) {
+    const char *e = getenv("AMGD_LMOP_WAVE");
+    v = e && *e ? atoi(e) : 64;       // 0: never
+  }
+  return v;
+}
 // (2) values: one thread per contribution (c, k, m):
 //     u_c * sum_{t >= max(k,m)} q_t[k] * q_t[m], t ascending (QQt, amg_setup.c:1638-1642)
 __global__ void k_lmop_val(uint64_t n, uint32_t c0, uint32_t c1, const uint64_t *coff,
@@ -2009,9 +2096,19 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
     }
     uint64_t e0 = hro[c0], e1 = hro[c1];
     if (n && e1 > e0) {
-      k_lmop_land<<<grid_for(e1 - e0, 256, 65536), 256, 0, s>>>(
-          erow, e0, e1, Wt->ro, Wt->col, S->ro, S->col, srn, S->nnz, rmax, b64, b4k, coff,
-          hcoff[c0], key);
+      uint64_t maxnz = 0;
+      for (uint32_t c = c0; c < c1; c++) maxnz = std::max<uint64_t>(maxnz, hro[c + 1] - hro[c]);
+      const int wmin = lmop_land_wave_min();
+      if (wmin > 0 && maxnz >= (uint64_t)wmin) {
+        amgd_route_hit(AMGD_R_LMOP_WAVE);
+        k_lmop_land_wave<<<grid_for((e1 - e0) * 64, 256, 65536), 256, 0, s>>>(
+            erow, e0, e1, Wt->ro, Wt->col, S->ro, S->col, srn, S->nnz, rmax, b64, b4k, coff,
+            hcoff[c0], key);
+      } else {
+        k_lmop_land<<<grid_for(e1 - e0, 256, 65536), 256, 0, s>>>(
+            erow, e0, e1, Wt->ro, Wt->col, S->ro, S->col, srn, S->nnz, rmax, b64, b4k, coff,
+            hcoff[c0], key);
+      }
       k_lmop_val<<<grid_for(n, 256, 65536), 256, 0, s>>>(n, c0, c1, coff, hcoff[c0], Wt->ro, Q,
                                                           qoff, u, key, S->nnz, val);
       KCHECK();

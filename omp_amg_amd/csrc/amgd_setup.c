@@ -901,6 +901,8 @@ API void amgd_dev_download(void *h, const void *d, size_t n) { amgd_d2h(h, d, n)
 
 extern uint64_t amgd_spmv_bytes(void);
 extern uint64_t amgd_spmv_bytes_strict(void);
+extern uint64_t amgd_spmv_launches(void);
+extern uint64_t amgd_spgemm_launches(void);
 extern void amgd_spmv_bytes_reset(void);
 extern void amgd_spgemm_set_timer(int slot);
 extern void amgd_spgemm_bytes_reset(void);
@@ -1062,6 +1064,8 @@ static int setup_body(void *arg) {
   g_st.spmv_kernel_ms = amgd_timer_ms(1);
   g_st.spmv_bytes = amgd_spmv_bytes();
   g_st.spmv_bytes_strict = amgd_spmv_bytes_strict();
+  g_st.spmv_launches = amgd_spmv_launches();
+  g_st.rap_launches = amgd_spgemm_launches();
   amgd_spmv_bytes_reset();
   g_st.rap_bytes = amgd_spgemm_bytes();
   amgd_spgemm_bytes_reset();

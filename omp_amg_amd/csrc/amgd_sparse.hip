@@ -737,6 +737,120 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     }
   }
 }
+// Whole-matrix long-row SpMV over contiguous entry chunks.  A wavefront owns RW
+// consecutive rows, i.e. the contiguous entry range [ro[rb], ro[rb + RW]); each round
+// streams CH = 1024 entries of it with 16-byte loads (four columns, or two values,
+// per lane per instruction: the full-rate load width of MI355X_MICROARCH.md, where
+// k_spmv_lane's 4- / 8-byte row-segment loads run at ~0.5-0.7 of it), forms the
+// products a * x[col] into LDS in entry order, and lane r of the first RW adds row r's
+// part of the chunk, left to right -- the same row sums, from +0, as every other
+// SpMV kernel here.  The next chunk's (column, value) loads are in flight during the
+// adds.  AMX: the adding lanes also keep each row's largest product and its first
+// position (find_support's fused selection, amgd_spmv_amax).
+template <int RW, bool AMX = false>
+__global__ __launch_bounds__(256) void k_spmv_chunk(const uint64_t *ro, const uint32_t *col,
+                                                    const double *a, uint32_t n, const double *x,
+                                                    double *z, double alpha, const double *y,
+                                                    double beta, const uint8_t *f, double *amx,
+                                                    uint64_t *apos) {
+  constexpr int CH = 1024;
+  __shared__ double buf[4][CH];
+  __shared__ uint64_t rof[4][RW + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n; rb += (uint64_t)gridDim.x * 4 * RW) {
+    const uint32_t nr = (uint32_t)min((uint64_t)RW, (uint64_t)n - rb);
+    if ((uint32_t)lane < nr) rof[w][lane] = ro[rb + lane];
+    if (lane == 0) rof[w][nr] = ro[rb + nr];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t E0 = rof[w][0], E1 = rof[w][nr];
+    const bool own = (uint32_t)lane < nr;
+    const uint64_t r0 = own ? rof[w][lane] : 0, r1 = own ? rof[w][lane + 1] : 0;
+    double t = 0;
+    double pmx = -DBL_MAX;
+    uint64_t ppos = ~0ull;
+    // one chunk's loads: lane L holds entries B + 4 (L + 64 q) + j, q < 4, j < 4
+    auto load = [&](uint64_t B, uint32_t (&cq)[16], double (&aq)[16]) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint64_t e = B + 4 * (uint64_t)(lane + 64 * q);
+        if (e + 3 < E1) {
+          const double2 a0 = *(const double2 *)(a + e), a1 = *(const double2 *)(a + e + 2);
+          aq[4 * q] = a0.x; aq[4 * q + 1] = a0.y; aq[4 * q + 2] = a1.x; aq[4 * q + 3] = a1.y;
+          if (x) {
+            const uint4 c = *(const uint4 *)(col + e);
+            cq[4 * q] = c.x; cq[4 * q + 1] = c.y; cq[4 * q + 2] = c.z; cq[4 * q + 3] = c.w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            aq[4 * q + j] = e + j < E1 ? a[e + j] : 0.0;
+            cq[4 * q + j] = (x && e + j < E1) ? col[e + j] : 0u;
+          }
+        }
+      }
+    };
+    // the products of a loaded chunk, straight into LDS in entry order
+    auto form = [&](uint64_t B, const uint32_t (&cq)[16], const double (&aq)[16]) {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint64_t e = B + 4 * (uint64_t)(lane + 64 * q) + j;
+          const bool ok = e >= E0 && e < E1;
+          buf[w][4 * (lane + 64 * q) + j] = ok ? (x ? aq[4 * q + j] * x[cq[4 * q + j]] : aq[4 * q + j]) : 0.0;
+        }
+    };
+    uint64_t B = E0 & ~3ull;
+    uint32_t cq[16];
+    double aq[16];
+    if (B < E1) {
+      load(B, cq, aq);
+      form(B, cq, aq);
+    }
+    for (; B < E1; B += CH) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint64_t Bn = B + CH;
+      if (Bn < E1) load(Bn, cq, aq);                 // next chunk in flight during the adds
+      if (own) {
+        const int lo = (int)(max(r0, B) - B), hi = (int)(min(r1, Bn) - B);
+        int p = lo;
+        for (; p + 8 <= hi; p += 8) {                  // LDS reads 8 ahead of the adds
+          double u[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) u[e] = buf[w][p + e];
+#pragma unroll
+          for (int e = 0; e < 8; e++) t += u[e];
+          if (AMX) {
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+              if (u[e] > pmx) { pmx = u[e]; ppos = B + p + e; }
+          }
+        }
+        for (; p < hi; p++) {
+          const double u = buf[w][p];
+          t += u;
+          if (AMX && u > pmx) { pmx = u; ppos = B + p; }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (Bn < E1) form(Bn, cq, aq);
+    }
+    if (own) {
+      const uint64_t i = rb + lane;
+      double vz = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) vz = vz * (f[i] ? 1.0 : 0.0);
+      z[i] = vz;
+      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
+    }
+  }
+}
+
 // rows per wavefront of the lane kernel for n rows (>= ~2048 wavefronts in flight)
 static int64_t g_rw_forced = -2;     // AMGD_SL_RW / amgd_spmv_set_rw (tests): 4, 16 or 64
 extern "C" void amgd_spmv_set_rw(int rw) { g_rw_forced = rw < 0 ? -2 : rw; }
@@ -763,12 +877,41 @@ static int spmv_nt() {
       k_spmv_lane<LIST, 4, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
                                                            z_, al, y_, be, f_, ml_);          \
   } while (0)
+// AMGD_SPMV_CHUNK=0 / amgd_spmv_set_chunk(0): whole-matrix products on k_spmv_lane's
+// row segments instead of k_spmv_chunk's contiguous 16-byte-load chunks (same sums)
+static int g_spmv_chunk = -1;
+extern "C" void amgd_spmv_set_chunk(int on) { g_spmv_chunk = on < 0 ? -1 : on; }  // 2: all rows
+// Chunks win where rows are moderate (256^3: rows of ~130 entries, PCG on the level-1
+// constraint operator: 3.32 -> 2.53 ms) and lose where they are long (one lane adds a
+// whole 1024-entry chunk of one row in order: rows of 700-8000 entries 1.6-2.6x slower,
+// profiles/r03/spmv_bench_chunk_vs_segments.txt): by default rows of mean < 256.
+static bool spmv_chunk_ok(const dcsr *M) {
+  // off by default: at 256^3 the chunks lost to the per-row segments even on the moderate
+  // rows (SpMV 6245 -> 6391 ms per setup, profiles/r03/ab256_r03j_chunk_lmopwave.txt)
+  if (g_spmv_chunk < 0) { const char *e = getenv("AMGD_SPMV_CHUNK"); g_spmv_chunk = e && *e ? atoi(e) : 0; }
+  const bool moderate = M->nnz < 256ull * M->rn || g_spmv_chunk == 2;
+  return g_spmv_chunk && moderate && !((uintptr_t)M->col & 15) && !((uintptr_t)M->a & 15);
+}
+#define CHUNK_LAUNCH(AMX_, rw_, g_, n_, x_, z_, al, y_, be, f_, amx_, apos_)                  \
+  do {                                                                                        \
+    if (rw_ == 64)                                                                            \
+      k_spmv_chunk<64, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_, \
+                                                      be, f_, amx_, apos_);                   \
+    else if (rw_ == 16)                                                                       \
+      k_spmv_chunk<16, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_, \
+                                                      be, f_, amx_, apos_);                   \
+    else                                                                                      \
+      k_spmv_chunk<4, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_,  \
+                                                     be, f_, amx_, apos_);                    \
+  } while (0)
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
     amgd_route_hit(AMGD_R_SPMV_LANE);                                                         \
     const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
-    if (spmv_nt())                                                                            \
+    if (!(LIST) && spmv_chunk_ok(M))                                                          \
+      CHUNK_LAUNCH(false, rw_, g_, n_, x_, z_, al, y_, be, f_, (double *)nullptr, (uint64_t *)nullptr); \
+    else if (spmv_nt())                                                                       \
       LANE_LAUNCH_NT(LIST, true, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
     else                                                                                      \
       LANE_LAUNCH_NT(LIST, false, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);           \
@@ -846,10 +989,11 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
 // column + value once, x gathered once per entry, row offsets, z (and y, f) once per row
 // g_mv_bytes_strict: the same with x read once (8 B per column), the minimum any
 // kernel must move -- the roofline's algorithmic bytes
-static uint64_t g_mv_bytes = 0, g_mv_bytes_strict = 0;
+static uint64_t g_mv_bytes = 0, g_mv_bytes_strict = 0, g_mv_launches = 0;
 extern "C" uint64_t amgd_spmv_bytes(void) { return g_mv_bytes; }
 extern "C" uint64_t amgd_spmv_bytes_strict(void) { return g_mv_bytes_strict; }
-extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = g_mv_bytes_strict = 0; }
+extern "C" uint64_t amgd_spmv_launches(void) { return g_mv_launches; }
+extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = g_mv_bytes_strict = g_mv_launches = 0; }
 // AMGD_MVLOG=1: one line per whole-matrix SpMV (rows, nnz, kernel, time, effective GB/s)
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
@@ -921,6 +1065,7 @@ static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alph
     const uint64_t rest = 16ull * n + 8 + (y && alpha != 0.0 ? 8ull * n : 0) + (f ? (uint64_t)n : 0);
     g_mv_bytes += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8 * (sp->pre[q + 1] - sp->pre[q]) : 0) + rest;
     g_mv_bytes_strict += 12 * (sp->pre[q + 1] - sp->pre[q]) + (x ? 8ull * M0->cn : 0) + rest;
+    g_mv_launches++;
   }
   amgd_timer_stop(1);
   KCHECK();
@@ -950,6 +1095,7 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
     const uint64_t rest = 16ull * M->rn + 8 + (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
     g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
     g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
+    g_mv_launches++;
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
     k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
@@ -968,14 +1114,19 @@ extern "C" void amgd_spmv_set_fused(int on) { g_fs_fused = on < 0 ? -1 : on; }
 extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos) {
   if (M->rn == 0 || amgd_nshards() > 1 || M->nnz < 32ull * M->rn || (int64_t)M->rn < sl_min_whole())
     return 0;
-  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 1; }
+  // off by default: keeping the argmax in the ordered-add loop lengthens the adding lanes'
+  // dependent chain -- at 256^3 the SpMVs took +3.1 s against 0.7 s of selection saved
+  // (profiles/r03/ab256_r03i_chunk_fused.txt)
+  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 0; }
   if (!g_fs_fused) return 0;
   const int rw_ = lane_rw(M->rn);
   const int g_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
   amgd_route_hit(AMGD_R_SPMV_LANE);
   amgd_route_hit(AMGD_R_FS_FUSED);
   amgd_timer_start(1);
-  if (rw_ == 64)
+  if (spmv_chunk_ok(M))
+    CHUNK_LAUNCH(true, rw_, g_, M->rn, x, z, 0.0, (const double *)nullptr, 1.0, (const uint8_t *)nullptr, amx, apos);
+  else if (rw_ == 64)
     k_spmv_lane<false, 64, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
                                                                 0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
   else if (rw_ == 16)
@@ -989,6 +1140,7 @@ extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double 
   const uint64_t rest = 16ull * M->rn + 8;
   g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
   g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
+  g_mv_launches++;
   return 1;
 }
 // rows-filtered SpMV (k_spmv arithmetic at any row length): z_i = (M x)_i * f_i on
@@ -2414,10 +2566,11 @@ static uint32_t sg_win_p0() {
   return (uint32_t)v;
 }
 static int g_sg_slot = -1;
-static uint64_t g_sg_bytes = 0;
+static uint64_t g_sg_bytes = 0, g_sg_launches = 0;
+extern "C" uint64_t amgd_spgemm_launches(void) { return g_sg_launches; }
 static int g_sg_pattern = 0;    // amgd_spgemm_pattern: hash-bin rows emit the pattern only
 extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
-extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; }
+extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; g_sg_launches = 0; }
 extern "C" uint64_t amgd_spgemm_bytes(void) { return g_sg_bytes; }
 
 // Tiny rows (at most SG_TINY products: the fine levels' near-diagonal products, 10^6 -
@@ -2926,8 +3079,12 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
   uint64_t nz = amgd_scan_u64(cnt2, rn);
-  if (g_sg_slot >= 0)
+  if (g_sg_slot >= 0) {
     g_sg_bytes += 12 * (A->nnz + B->nnz + nz) + 8 * ((uint64_t)A->rn + B->rn + rn + 3);
+    // launches of the RAP-instantiated numeric kernels (the rocprof regex of tools/gpurun_pmc.sh)
+    for (int q = 0; q < 4; q++) g_sg_launches += hn[q] ? 1 : 0;
+    g_sg_launches += (hn[4] ? 1 : 0) + (win ? (wn[0] ? 1 : 0) + (wn[2] ? 1 : 0) : 0);
+  }
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = rn; X->cn = B->cn; X->nnz = nz;
   if (nz == dist) {               // no cancellation: the distinct layout is final

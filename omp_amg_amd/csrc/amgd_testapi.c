@@ -192,8 +192,12 @@ API int amgd_test_cols_masked(const hcsr *HA, const uint8_t *hmask, hcsr *HX) {
 }
 void amgd_qfactor_set_reuse(int on);
 API void amgd_test_qf_reuse(int on) { amgd_qfactor_set_reuse(on); }
+void amgd_spmv_set_chunk(int on);
+API void amgd_test_spmv_chunk(int on) { amgd_spmv_set_chunk(on); }
 void amgd_spmv_set_fused(int on);
 API void amgd_test_fs_fused(int on) { amgd_spmv_set_fused(on); }
+void amgd_lmop_set_wave(int n);
+API void amgd_test_lmop_wave(int n) { amgd_lmop_set_wave(n); }
 void amgd_spgemm_set_pattern(int on);
 API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }
 /* Q factors taken by copy from the previous iteration / factored, since the last call */

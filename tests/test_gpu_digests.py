@@ -37,10 +37,8 @@ def _mk():
 
 # routes each case must have taken (kept to what its sizes guarantee by the defaults)
 EXPECT_ROUTES = {
-    "p7_48": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "fs_fused",
-              "qf_reuse"),
-    "p7_64": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "fs_fused",
-              "qf_reuse"),
+    "p7_48": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
+    "p7_64": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
     "aniso_20": ("fs_inc", "mv_long"),
     "aniso_24": ("fs_inc",),
     "aniso_32": ("fs_inc", "spmv_lane"),

@@ -367,6 +367,15 @@ def rw(request):
     oa.spmv_rw(-1)
 
 
+@pytest.fixture(params=[2, 0], ids=["chunk", "segments"])
+def chunk(request):
+    """whole-matrix long-row products: contiguous 16-byte-load chunks (k_spmv_chunk, at
+    every row length) or per-row segments (k_spmv_lane)"""
+    oa.spmv_chunk(request.param)
+    yield request.param
+    oa.spmv_chunk(-1)
+
+
 def _adversarial_rows(rng, rn=700):
     """rows built to break a parallel ordered sum: monotone positive sums crossing many
     binades, exact ties at the running sum's half-ulp, leading / interleaved zeros and
@@ -418,7 +427,7 @@ def mv_long(request):
 
 
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_adversarial_rows(sl_min, rw, mv_long):
+def test_spmv_adversarial_rows(sl_min, rw, mv_long, chunk):
     """long-row SpMV / row sums / listed rows on adversarial rows through the wave-per-row
     and the lane-per-row kernels (every RW) and, for listed rows past the long-row
     threshold, the block-per-row binade scan, bit for bit against the sequential loop
@@ -486,7 +495,7 @@ def test_spmv_rows_multichunk_exact():
 
 
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_long_rows_ragged(sl_min, rw):
+def test_spmv_long_rows_ragged(sl_min, rw, chunk):
     """long-row SpMV kernels on ragged rows: wave-per-row (default below 2^20 rows) and
     lane-per-row (forced with the row threshold at 0), with and without y, the f row
     mask and x = NULL (ordered row sums)"""

@@ -200,6 +200,29 @@ def test_gpu_lmop_pruned_bitexact_fixture(case):
     assert not bad, bad
 
 
+# lmop: every support takes the general walk, sp_add's walk replayed one wavefront per
+# (c, k) at every support size (and one thread per (c, k)) -- against the fixtures; the
+# 27-point and anisotropic ones land contributions past their rows
+@pytest.mark.parametrize("wave", [1, 0], ids=["wave", "thread"])
+@pytest.mark.parametrize("case", ["p7_12", "p27_7", "p27_8", "aniso_12", "sem_e3_N2", "amgdmp"])
+def test_gpu_lmop_walk_wave_bitexact_fixture(case, wave):
+    z = np.load(os.path.join(GOLD, case + ".npz"))
+    ref = parity.from_npz(z)
+    oa.lmop_mode(1)
+    oa.lmop_prune(0)
+    oa.lmop_wave(wave)
+    oa.route_stats(reset=True)
+    try:
+        h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
+    finally:
+        oa.lmop_mode(0)
+        oa.lmop_prune(-1)
+        oa.lmop_wave(-1)
+    assert (oa.route_stats(reset=True)["lmop_wave"] > 0) == bool(wave)
+    bad = parity.compare(ref, h, exact=True)
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("gen", [("p7_32", "1", lambda: problems.poisson3d(32)),
                                  ("aniso_16", "2", lambda: problems.poisson3d(16, eps=1e-3)),
                                  ("p27_16", "2", lambda: problems.poisson3d(16, 27))],
@@ -255,6 +278,7 @@ def test_gpu_fs_fused_select_matches_separate(gen):
     Ai, Aj, Av = gen[1]()
     oa.spmv_sl_min(0)
     try:
+        oa.fs_fused(1)
         oa.route_stats(reset=True)
         h_f = abi.run_setup(oa.lib(), Ai, Aj, Av)
         assert oa.route_stats(reset=True)["fs_fused"] > 0

@@ -22,7 +22,8 @@ import omp_amg_amd as oa  # noqa: E402
 from omp_amg_amd import parity, problems  # noqa: E402
 
 HOOKS = {"wt": oa.spgemm_wt, "win": oa.spgemm_win, "wsym": oa.spgemm_wsym, "rw": oa.spmv_rw,
-         "qfr": oa.qf_reuse, "pat": oa.sg_pattern, "fused": oa.fs_fused}
+         "qfr": oa.qf_reuse, "pat": oa.sg_pattern, "fused": oa.fs_fused,
+         "chunk": oa.spmv_chunk, "lw": oa.lmop_wave}
 
 
 def digest(h):
@@ -64,7 +65,11 @@ def main():
             t0 = time.perf_counter()
             st = ds.run()
             ts.append(time.perf_counter() - t0)
+            print(f"# {s}: {ts[-1]:.3f} s", file=sys.stderr, flush=True)   # progress (a run
+            # that prints nothing for minutes is taken for a hang)
         apply(s, reset=True)
+        if not a.no_digest:
+            print(f"# {s}: digest ...", file=sys.stderr, flush=True)
         dg = None if a.no_digest else digest(ds.export())
         ref = ref or dg
         print(json.dumps({"setting": s, "secs": [round(t, 3) for t in ts], "rap_kernel_ms": round(st["rap_kernel_ms"], 1),
