@@ -101,6 +101,7 @@ def lib() -> C.CDLL:
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
         L.amgd_test_fs_fused.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
+        L.amgd_test_qf_colc.argtypes = [C.c_int]
         L.amgd_test_spmv_chunk.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -425,6 +426,12 @@ def lmop_wave(n: int) -> None:
     walk one wavefront per (c, k) with 64 columns searched at once (default 64), 0 one
     thread per (c, k) always, -1 default / AMGD_LMOP_WAVE.  Same landings."""
     lib().amgd_test_lmop_wave(int(n))
+
+
+def qf_colc(on: int) -> None:
+    """Q factor, 256- / 512- / 1024-point tiers: 1 the s2 pass reads a column-packed copy
+    of U (coalesced), 0 the row-packed U, -1 default / AMGD_QF_COLC.  Same bits."""
+    lib().amgd_test_qf_colc(int(on))
 
 
 def sg_pattern(on: int) -> None:

@@ -197,6 +197,8 @@ API void amgd_test_spmv_chunk(int on) { amgd_spmv_set_chunk(on); }
 void amgd_spmv_set_fused(int on);
 API void amgd_test_fs_fused(int on) { amgd_spmv_set_fused(on); }
 void amgd_lmop_set_wave(int n);
+void amgd_qfactor_set_colc(int on);
+API void amgd_test_qf_colc(int on) { amgd_qfactor_set_colc(on); }
 API void amgd_test_lmop_wave(int n) { amgd_lmop_set_wave(n); }
 void amgd_spgemm_set_pattern(int on);
 API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }

@@ -789,6 +789,24 @@ def test_qfactor_split_bitexact(structure, mode):
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
 
 
+@pytest.mark.parametrize("colc", [1, 0], ids=["colc", "rows"])
+@pytest.mark.parametrize("structure,split", [("tiers", 0), ("blocks", 1)])
+def test_qfactor_colc_bitexact(structure, split, colc):
+    """the blocked tiers (256 / 512 / 1024 points) with the s2 pass over a column-packed
+    copy of U (and over U itself), bit for bit the oracle"""
+    W, A = _qfactor_case(structure)
+    oa.qf_colc(colc)
+    oa.qf_split(split)
+    try:
+        X = oa.test_csr_op(5, W, A)
+    finally:
+        oa.qf_colc(-1)
+        oa.qf_split(-1)
+    ref = _oracle_qfactor(W, A)
+    assert X.nnz == len(ref)
+    assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
+
+
 @pytest.mark.parametrize("structure", ["tiers", "scattered"])
 def test_qapply_huge_grid_path(structure):
     """Q application of huge supports by the grid-wide kernels (threshold lowered to 600

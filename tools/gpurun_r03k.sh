@@ -1,0 +1,18 @@
+# r03 session k: full GPU suite, the driver's bench command and a rocprofv3 kernel
+# summary of a short bench run, all on the same tree
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=${1:-r03k}
+D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+rm -rf $D; mkdir -p $D
+export PYTHONPATH=$GRAFT_REPO_ROOT
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $D/gputests.log 2>&1 || { tail -30 $D/gputests.log; exit 1; }
+tail -2 $D/gputests.log
+t0=$(date +%s)
+timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench.json 2> $D/bench.err || { echo bench failed; tail -20 $D/bench.err; exit 1; }
+echo "bench wall $(( $(date +%s) - t0 )) s"
+cat $D/bench.json
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $D/prof -o bench --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 1 --warmup 1 > $D/prof_line.json 2>&1 || exit 1
+find $D -name "*kernel_trace.csv" -delete
+tail -n 1 $D/prof_line.json
