@@ -104,6 +104,8 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_colc.argtypes = [C.c_int]
         L.amgd_test_spmv_chunk.argtypes = [C.c_int]
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
+        L.amgd_test_spgemm_wwin.argtypes = [C.c_int]
+        L.amgd_test_spmv_pipe.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
@@ -438,6 +440,17 @@ def sg_pattern(on: int) -> None:
     """constraint pattern W_skel*W_skel': 1 pattern-only product (default), 0 the full
     product (values discarded by interp_lmop), -1 default.  Same bits."""
     lib().amgd_test_sg_pattern(int(on))
+
+
+def spmv_pipe(m: int) -> None:
+    """lane SpMV with the gather one round ahead (AMGD_SPMV_PIPE bits: 1 whole-matrix,
+    2 listed rows; -1: back to the env)"""
+    lib().amgd_test_spmv_pipe(int(m))
+
+
+def spgemm_wwin(m: int) -> None:
+    """wave-private windowed SpGEMM routing (AMGD_SG_WWIN bits; -1: back to the env)"""
+    lib().amgd_test_spgemm_wwin(int(m))
 
 
 def spgemm_wsym(w: int) -> None:

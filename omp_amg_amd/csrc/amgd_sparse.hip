@@ -737,6 +737,112 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
     }
   }
 }
+// k_spmv_lane with the x gather one round ahead (round 3): k_spmv_lane issues the
+// next round's (value, column) loads before its ordered adds but the gather x[col]
+// only after them, so every round waits for one full gather latency.  Here a round
+// is 512 entries (8 per lane, SEG = 512 / RW per row) and two rounds are in flight
+// during the adds of the current one: the gather of round r+1 (its columns arrived
+// during round r-1) and the (value, column) loads of round r+2.  Rows, segments and
+// the left-to-right adds from +0 are k_spmv_lane's: the same sums.
+template <bool LIST, int RW, int PER = 8>
+__global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, uint32_t n,
+                                                   const uint32_t *list, const double *x,
+                                                   double *z, double alpha, const double *y,
+                                                   double beta, const uint8_t *f,
+                                                   uint32_t maxlen = 0xffffffffu) {
+  constexpr int SEG = 64 * PER / RW;
+  __shared__ double buf[4][RW][SEG + 1];
+  __shared__ uint64_t rk0[4][RW];
+  __shared__ uint32_t rlen[4][RW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n;
+       rb += (uint64_t)gridDim.x * 4 * RW) {
+    const uint64_t r = rb + lane;
+    const bool own = lane < RW && r < n;
+    const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
+    uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    if (LIST && k1 - k0 > maxlen) k1 = k0;      // a long row: left to k_rows_exact
+    const uint32_t len = (uint32_t)(k1 - k0);
+    if (lane < RW) {
+      rk0[w][lane] = k0;
+      rlen[w][lane] = len;
+    }
+    uint32_t mx = len;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (value, column) of round `off`: lane L's q-th entry is flat entry q*64 + L
+    auto ld = [&](uint32_t off, double *av, uint32_t *cv) {
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
+        const uint32_t en = off + sub;
+        av[q] = 0.0;
+        cv[q] = 0;
+        if (en < rlen[w][rr]) {
+          const uint64_t k = rk0[w][rr] + en;
+          av[q] = a[k];
+          if (x) cv[q] = col[k];
+        }
+      }
+    };
+    double a0[PER], g0[PER], a1[PER];
+    uint32_t c0[PER], c1[PER];
+    ld(0, a0, c0);
+#pragma unroll
+    for (int q = 0; q < PER; q++) g0[q] = x ? x[c0[q]] : 0.0;
+    ld(SEG, a1, c1);
+    double t = 0;
+    for (uint32_t off = 0; off < mx; off += SEG) {
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int fl = q * 64 + lane;
+        buf[w][fl / SEG][fl % SEG] = x ? a0[q] * g0[q] : a0[q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double g1[PER], a2[PER];
+      uint32_t c2[PER];
+#pragma unroll
+      for (int q = 0; q < PER; q++) g1[q] = x ? x[c1[q]] : 0.0;   // round off + SEG
+      if (off + 2 * SEG < mx) ld(off + 2 * SEG, a2, c2);           // round off + 2 SEG
+      else {
+#pragma unroll
+        for (int q = 0; q < PER; q++) { a2[q] = 0.0; c2[q] = 0; }
+      }
+      if (lane < RW && off < len) {
+        const uint32_t m = min((uint32_t)SEG, len - off);
+        if (m == SEG) {
+          constexpr int U = SEG < 16 ? SEG : 16;
+#pragma unroll
+          for (int e0 = 0; e0 < SEG; e0 += U) {
+            double u[U];
+#pragma unroll
+            for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
+#pragma unroll
+            for (int e = 0; e < U; e++) t += u[e];
+          }
+        } else {
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < PER; q++) { a0[q] = a1[q]; g0[q] = g1[q]; a1[q] = a2[q]; c1[q] = c2[q]; }
+    }
+    if (own && (!LIST || ro[i + 1] - ro[i] <= maxlen)) {
+      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) v = v * (f[i] ? 1.0 : 0.0);
+      z[i] = v;
+    }
+  }
+}
 // Whole-matrix long-row SpMV over contiguous entry chunks.  A wavefront owns RW
 // consecutive rows, i.e. the contiguous entry range [ro[rb], ro[rb + RW]); each round
 // streams CH = 1024 entries of it with 16-byte loads (four columns, or two values,
@@ -904,6 +1010,35 @@ static bool spmv_chunk_ok(const dcsr *M) {
       k_spmv_chunk<4, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_,  \
                                                      be, f_, amx_, apos_);                    \
   } while (0)
+// AMGD_SPMV_PIPE=1 / amgd_spmv_set_pipe(1): the lane products through k_spmv_pipe
+// (gather one round ahead; same sums)
+static int g_spmv_pipe = -1;
+extern "C" void amgd_spmv_set_pipe(int on) { g_spmv_pipe = on < 0 ? -1 : on; }
+static int spmv_pipe() {
+  if (g_spmv_pipe < 0) { const char *e = getenv("AMGD_SPMV_PIPE"); g_spmv_pipe = e && *e ? atoi(e) : 0; }
+  return g_spmv_pipe;
+}
+#define PIPE_LAUNCH_P(LIST, PER_, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_)               \
+  do {                                                                                        \
+    if (rw_ == 64)                                                                            \
+      k_spmv_pipe<LIST, 64, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
+                                                             z_, al, y_, be, f_, ml_);        \
+    else if (rw_ == 16)                                                                       \
+      k_spmv_pipe<LIST, 16, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
+                                                             z_, al, y_, be, f_, ml_);        \
+    else                                                                                      \
+      k_spmv_pipe<LIST, 4, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
+                                                            z_, al, y_, be, f_, ml_);         \
+  } while (0)
+// entries per lane per round of k_spmv_pipe (AMGD_SPMV_PIPE bits 4: 4, 8: 16, 16: 12; else 8)
+#define PIPE_LAUNCH(LIST, rw_, n_, list_, x_, z_, al, y_, be, f_, ml_)                           \
+  do {                                                                                        \
+    const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
+    if (spmv_pipe() & 4) PIPE_LAUNCH_P(LIST, 4, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
+    else if (spmv_pipe() & 8) PIPE_LAUNCH_P(LIST, 16, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
+    else if (spmv_pipe() & 16) PIPE_LAUNCH_P(LIST, 12, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
+    else PIPE_LAUNCH_P(LIST, 8, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
+  } while (0)
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
@@ -911,6 +1046,8 @@ static bool spmv_chunk_ok(const dcsr *M) {
     const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
     if (!(LIST) && spmv_chunk_ok(M))                                                          \
       CHUNK_LAUNCH(false, rw_, g_, n_, x_, z_, al, y_, be, f_, (double *)nullptr, (uint64_t *)nullptr); \
+    else if (spmv_pipe() & (LIST ? 2 : 1))                                                    \
+      PIPE_LAUNCH(LIST, rw_, n_, list_, x_, z_, al, y_, be, f_, ml_);                         \
     else if (spmv_nt())                                                                       \
       LANE_LAUNCH_NT(LIST, true, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
     else                                                                                      \
@@ -2560,6 +2697,18 @@ static int sg_wt() {
   return g_sg_wt;
 }
 extern "C" void amgd_spgemm_set_wt(int t) { g_sg_wt = t < 0 ? -1 : t; }
+// AMGD_SG_WWIN bits: 1 windowed numeric rows, 2 wide symbolic rows, 4 the 4096- / 8192-slot
+// hash-bin numeric rows through the wave-private windowed kernel k_sg_wwin; 8: its numeric
+// window 1024 columns (else 2048)
+static int g_sg_wwin = -1;
+static int sg_wwin() {
+  if (g_sg_wwin < 0) {
+    const char *e = getenv("AMGD_SG_WWIN");
+    g_sg_wwin = e && *e ? atoi(e) : 0;
+  }
+  return g_sg_wwin;
+}
+extern "C" void amgd_spgemm_set_wwin(int m) { g_sg_wwin = m; }
 static uint32_t sg_win_p0() {
   static long v = -1;
   if (v < 0) { const char *e = getenv("AMGD_SG_WIN_P0"); v = e ? atol(e) : 48; }
@@ -2787,6 +2936,186 @@ __global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t 
   }
 }
 
+// Wave-private windowed SpGEMM (round 3).  k_sg_win shares one window accumulator
+// among the 256 threads of a work-group, so every layer (A entry k) costs a barrier
+// while typically only a few dozen of its B-row entries fall into the window.  Here
+// every WAVEFRONT owns a row and a private LDS window: the 64 lanes of one wavefront
+// execute a layer's additions in one instruction stream and LDS operations of one
+// wavefront complete in issue order, so layer k's additions precede layer k+1's with
+// no barrier at all.  Lane e holds the state of layer e of the current 64-layer chunk
+// (B-row start, length, cursor, A value, next column); the in-window layers are taken
+// in ascending k from a ballot mask, the next D layers' column / value loads in flight
+// while the current one is added (wave-uniform parameters by readlane).  Windows
+// start at the smallest pending column (empty column ranges are skipped); rows of
+// more than 64 layers keep their cursors in global scratch indexed by the A entry.
+// Every output is the sum, from +0 in ascending k, of its products -- mxm's order
+// (amg_setup.c:1894-1960) -- and the window is emitted in column order, coalesced.
+// MODE 0: distinct columns per row (byte map, W columns); MODE 1: values (W doubles).
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+  return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+__device__ __forceinline__ double rld(double v, int l) {
+  return __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(v), l));
+}
+template <int W, int MODE, int RAP = 0>
+__global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t nrows,
+                                                 const uint64_t *aro, const uint32_t *acol,
+                                                 const double *aa, const uint64_t *bro,
+                                                 const uint32_t *bcol, const double *ba,
+                                                 uint64_t *cnt, const uint64_t *xro,
+                                                 uint32_t *xcol, double *xa, uint32_t *curs) {
+  constexpr int NWV = 4, D = 4;
+  constexpr int WB = MODE ? W * 8 : W;              // LDS bytes per wavefront
+  constexpr uint32_t NONE = 0xffffffffu;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NWV * WB];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double *acc = (double *)(lds + wv * WB);
+  uint8_t *mp = lds + wv * WB;
+  uint32_t *mp32 = (uint32_t *)mp;
+  const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (uint32_t r = blockIdx.x * NWV + wv; r < nrows; r += gridDim.x * NWV) {
+    const uint32_t i = rows[r];
+    const uint64_t a0 = aro[i];
+    const uint32_t nl = (uint32_t)(aro[i + 1] - a0);
+    uint32_t mn = NONE, mx = 0;
+    for (uint32_t e = lane; e < nl; e += 64) {        // the row's column range
+      const uint32_t k = acol[a0 + e];
+      if (e + 1 < nl && acol[a0 + e + 1] == k) continue;
+      const uint64_t b0 = bro[k], b1 = bro[k + 1];
+      if (b0 < b1) {
+        mn = min(mn, bcol[b0]);
+        mx = max(mx, bcol[b1 - 1]);
+      }
+    }
+    for (int o = 32; o; o >>= 1) {
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    }
+    const bool single = nl <= 64;
+    uint64_t lb0 = 0;
+    uint32_t llen = 0, lcur = 0, lpk = NONE;
+    double lav = 0.0;
+    auto load_layer = [&](uint32_t c0, bool first) {
+      const uint32_t e = c0 + (uint32_t)lane;
+      lb0 = 0; llen = 0; lcur = 0; lpk = NONE; lav = 0.0;
+      if (e < nl) {
+        const uint32_t k = acol[a0 + e];
+        if (!(e + 1 < nl && acol[a0 + e + 1] == k)) {   // duplicate columns: the last one wins
+          lb0 = bro[k];
+          llen = (uint32_t)(bro[k + 1] - lb0);
+          if (MODE) lav = aa[a0 + e];
+          if (!first) lcur = curs[a0 + e];
+          if (lcur < llen) lpk = bcol[lb0 + lcur];
+        }
+      }
+    };
+    if (single) load_layer(0, true);
+    const uint64_t ob = MODE ? xro[i] : 0;
+    uint64_t nout = 0;
+    bool first = true;
+    uint32_t wb = mn;
+    while (mn <= mx) {
+      const uint32_t we = (uint32_t)min((uint64_t)mx, (uint64_t)wb + W - 1);   // inclusive
+      if (MODE) {
+        for (int q = lane; q < W; q += 64) acc[q] = 0.0;
+      } else {
+        for (int q = lane; q < W / 4; q += 64) mp32[q] = 0u;
+      }
+      uint32_t nmin = NONE;
+      for (uint32_t c0 = 0; c0 < nl; c0 += 64) {
+        if (!single) load_layer(c0, first);
+        uint64_t act = __ballot(lpk <= we);
+        int qe[D];
+        uint32_t qc[D];
+        double qv[D];
+        auto issue = [&](int s) {
+          qe[s] = -1;
+          qc[s] = NONE;
+          qv[s] = 0.0;
+          if (act) {
+            const int e = __ffsll((long long)act) - 1;
+            act &= act - 1;
+            const uint64_t b0 = rl64(lb0, e);
+            const uint32_t ln = rl32(llen, e), j = rl32(lcur, e) + (uint32_t)lane;
+            qe[s] = e;
+            if (j < ln) {
+              qc[s] = bcol[b0 + j];
+              if (MODE) qv[s] = ba[b0 + j];
+            }
+          }
+        };
+#pragma unroll
+        for (int s = 0; s < D; s++) issue(s);
+        while (qe[0] >= 0) {
+          const int e = qe[0];
+          uint32_t col = qc[0];
+          double val = qv[0];
+#pragma unroll
+          for (int s = 0; s + 1 < D; s++) { qe[s] = qe[s + 1]; qc[s] = qc[s + 1]; qv[s] = qv[s + 1]; }
+          issue(D - 1);
+          const double av = MODE ? rld(lav, e) : 0.0;
+          uint32_t cu = rl32(lcur, e);
+          for (;;) {
+            const bool in = col <= we;                 // a prefix of the lanes (sorted row)
+            if (in) {
+              if (MODE) {
+                double *p = acc + (col - wb);
+                *p = *p + val * av;
+              } else {
+                mp[col - wb] = 1;
+              }
+            }
+            const uint32_t n = (uint32_t)__popcll(__ballot(in));
+            if (n < 64) {
+              const uint32_t pk = (uint32_t)__shfl((int)col, (int)n, 64);   // first column past
+              cu += n;
+              if (lane == e) { lcur = cu; lpk = pk; }
+              break;
+            }
+            cu += 64;                                  // more of this layer in the window
+            const uint64_t b0 = rl64(lb0, e);
+            const uint32_t ln = rl32(llen, e), j = cu + (uint32_t)lane;
+            col = NONE;
+            if (j < ln) {
+              col = bcol[b0 + j];
+              if (MODE) val = ba[b0 + j];
+            }
+          }
+        }
+        uint32_t m = lpk;
+        for (int o = 32; o; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+        nmin = min(nmin, m);
+        if (!single && c0 + lane < nl) curs[a0 + c0 + lane] = lcur;
+      }
+      if (MODE) {                                      // emit in column order
+        for (int q = 0; q < W; q += 64) {
+          const double v = acc[q + lane];
+          const bool nz = v != 0.0;
+          const uint64_t bm = __ballot(nz);
+          if (nz) {
+            const uint64_t o = ob + nout + (uint64_t)__popcll(bm & ltm);
+            xcol[o] = wb + (uint32_t)(q + lane);
+            xa[o] = v;
+          }
+          nout += (uint64_t)__popcll(bm);
+        }
+      } else {
+        uint32_t c = 0;
+        for (int q = lane; q < W / 4; q += 64) c += (uint32_t)__popc(mp32[q] & 0x01010101u);
+        for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+        nout += c;
+      }
+      first = false;
+      if (nmin > mx) break;
+      wb = nmin;
+    }
+    if (lane == 0) cnt[i] = nout;
+  }
+}
+
 // wide rows -> windowed (dense accumulator) or hash kernels.  The windowed kernel
 // pays a barrier per layer per window: it is chosen when a layer brings enough
 // products into a window, i.e. products * min(W, span) / (layers * span) >= p0,
@@ -2879,10 +3208,17 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
+  const int wwin = kseq ? sg_wwin() : 0;
+  uint32_t *curs = nullptr;
+  if (wwin) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
   if (hc[1]) {
     const int wsym = kseq ? sg_wsym() : 0;
     if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
-    if (wsym == 8192)
+    if (wwin & 2)
+      k_sg_wwin<16384, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+          nullptr, curs);
+    else if (wsym == 8192)
       k_sg_wsym<8192><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
     else if (wsym == 16384)
@@ -2987,12 +3323,24 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_wt<W_, T_, 0><<<gt, 256, 0, s>>>(R_, nrw,    A->ro, A->col, A->a, B->ro, B->col,     \
                                             B->a, cnt2, cnt, tcol, ta);                         \
   } while (0)
+#define SG_WW(W_, rows_, nrw)                                                                   \
+  do {                                                                                          \
+    const int gw = (int)std::min<unsigned>((nrw + 3) / 4, 16384u);                              \
+    if (rap)                                                                                    \
+      k_sg_wwin<W_, 1, 1><<<gw, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,     \
+                                             B->a, cnt2, cnt, tcol, ta, curs);                  \
+    else                                                                                        \
+      k_sg_wwin<W_, 1, 0><<<gw, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,     \
+                                             B->a, cnt2, cnt, tcol, ta, curs);                  \
+  } while (0)
 #define SG_WIN(nr, rows_)                                                                       \
   if (nr) {                                                                                     \
     const unsigned nrw = (nr);                                                                  \
     const int g = (int)std::min<unsigned>(nrw, 16384u);                                         \
     const int wt = sg_wt();                                                                     \
-    if (wt == 4 && win == 2048) SG_WT(2048, 4, rows_);                                              \
+    if ((wwin & 1) && (wwin & 8)) SG_WW(1024, rows_, nrw);                                      \
+    else if (wwin & 1) SG_WW(2048, rows_, nrw);                                                 \
+    else if (wt == 4 && win == 2048) SG_WT(2048, 4, rows_);                                         \
     else if (wt == 8 && win == 2048) SG_WT(2048, 8, rows_);                                         \
     else if (wt == 4 && win == 1024) SG_WT(1024, 4, rows_);                                         \
     else if (wt == 8 && win == 1024) SG_WT(1024, 8, rows_);                                         \
@@ -3037,6 +3385,17 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (hn[0] || hn[1] || hn[2] || hn[3]) amgd_route_hit(kseq ? AMGD_R_SG_KSEQ : AMGD_R_SG_ROW);
   if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WIN);
   if (hn[4]) amgd_route_hit(AMGD_R_SG_LONG);
+  unsigned ww_launches = 0;
+  if (kseq && (wwin & 4)) {      // the 4096- / 8192-slot hash bins through k_sg_wwin
+    for (int q = 2; q < 4; q++) {
+      const unsigned nb = hn[q];
+      if (!nb) continue;
+      ww_launches++;
+      if (wwin & 8) SG_WW(1024, lists + q * L, nb);
+      else SG_WW(2048, lists + q * L, nb);
+      hn[q] = 0;
+    }
+  }
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
@@ -3076,6 +3435,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
 #undef SG_WIN
 #undef SG_WT
+#undef SG_WW
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
   uint64_t nz = amgd_scan_u64(cnt2, rn);
@@ -3083,7 +3443,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     g_sg_bytes += 12 * (A->nnz + B->nnz + nz) + 8 * ((uint64_t)A->rn + B->rn + rn + 3);
     // launches of the RAP-instantiated numeric kernels (the rocprof regex of tools/gpurun_pmc.sh)
     for (int q = 0; q < 4; q++) g_sg_launches += hn[q] ? 1 : 0;
-    g_sg_launches += (hn[4] ? 1 : 0) + (win ? (wn[0] ? 1 : 0) + (wn[2] ? 1 : 0) : 0);
+    g_sg_launches += (hn[4] ? 1 : 0) + (win ? (wn[0] ? 1 : 0) + (wn[2] ? 1 : 0) : 0) + ww_launches;
   }
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = rn; X->cn = B->cn; X->nnz = nz;
@@ -3099,6 +3459,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
   amgd_free(ub); amgd_free(lists); amgd_free(counts);
   if (wlists) amgd_free(wlists);
+  if (curs) amgd_free(curs);
   if (slab_v) { amgd_free(slab_v); amgd_free(slab_s); }
   if (sglog) {
     uint64_t prods = 0;

@@ -194,6 +194,8 @@ void amgd_qfactor_set_reuse(int on);
 API void amgd_test_qf_reuse(int on) { amgd_qfactor_set_reuse(on); }
 void amgd_spmv_set_chunk(int on);
 API void amgd_test_spmv_chunk(int on) { amgd_spmv_set_chunk(on); }
+void amgd_spmv_set_pipe(int on);
+API void amgd_test_spmv_pipe(int on) { amgd_spmv_set_pipe(on); }
 void amgd_spmv_set_fused(int on);
 API void amgd_test_fs_fused(int on) { amgd_spmv_set_fused(on); }
 void amgd_lmop_set_wave(int n);
@@ -244,6 +246,8 @@ API void amgd_test_spgemm_win(int w) { amgd_spgemm_set_win(w); }
 /* symbolic pass of rows with many products: 0 (LDS hash), 32768 / 65536 (byte-map windows) */
 extern void amgd_spgemm_set_wsym(int w);
 API void amgd_test_spgemm_wsym(int w) { amgd_spgemm_set_wsym(w); }
+extern void amgd_spgemm_set_wwin(int m);
+API void amgd_test_spgemm_wwin(int m) { amgd_spgemm_set_wwin(m); }
 /* SpMV: row count from which the lane-per-row kernel runs, for whole-matrix and
    listed-row products alike (0 = always, -1 = environment / default) */
 extern void amgd_spmv_set_sl_min(int64_t n);

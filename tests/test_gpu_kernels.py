@@ -178,6 +178,53 @@ def test_spgemm_tiled_windows(case, win, wt):
     assert refops.same(X, R)
 
 
+@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8])
+@pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
+                                  "huge_a", "gapped", "dense_rows"])
+def test_spgemm_wave_windows(case, wwin):
+    """wave-private windowed kernel (k_sg_wwin: one wavefront per row, its own LDS window,
+    no barrier per layer) for the symbolic counts (2) and the numeric rows of both the
+    windowed (1) and the 4096- / 8192-slot hash bins (4), windows of 2048 or 1024 (8)
+    columns: vs the host restatement, bit for bit -- rows of more than 64 layers (cursors
+    in scratch), duplicate A columns, exact cancellation, empty rows, column clusters far
+    apart (skipped windows), B-row runs past 64 entries inside one window"""
+    rng = np.random.default_rng({"banded": 91, "long_a": 92, "dups_cancel": 93, "ragged": 94,
+                                 "wide_span": 95, "huge_a": 96, "gapped": 97, "dense_rows": 98}[case])
+    if case == "banded":
+        A, B = _banded(rng, 301, 400, 6000, 60, 0.7, 150, 3000, ints=False)
+    elif case == "long_a":
+        A, B = _banded(rng, 70, 900, 8000, 400, 0.8, 100, 4000)
+    elif case == "dups_cancel":
+        A, B = _banded(rng, 157, 300, 5000, 50, 0.8, 160, 2500, dups=True)
+    elif case == "ragged":
+        A, B = _banded(rng, 203, 350, 7000, 90, 0.6, 120, 3500, empty_every=5)
+    elif case == "wide_span":
+        A, B = _banded(rng, 41, 500, 60000, 200, 0.7, 90, 30000)
+    elif case == "huge_a":          # 1100-1300 layers per row: 18-21 chunks of 64
+        A = refops.rand_csr(rng, 6, 1400, 0.85)
+        B = refops.rand_csr(rng, 1400, 3000, 0.03)
+    elif case == "gapped":
+        A = refops.rand_csr(rng, 30, 300, 0.3, ints=True)
+        B = refops.rand_csr(rng, 300, 6000, 0.02, ints=True)
+        shift = np.array([0, 70000, 250000, 1000000])[B.col // 1500]
+        B = refops.Csr(B.rn, 1006000, B.row_off, B.col + shift, B.a)
+    else:                           # dense B rows: > 64 entries of one layer per window
+        A = refops.rand_csr(rng, 20, 200, 0.3)
+        B = refops.rand_csr(rng, 200, 9000, 0.2)
+    assert B.a.size >= 64 * B.rn
+    R = refops.spgemm(A, B)
+    oa.spgemm_flat(False)
+    oa.spgemm_win(2048)
+    oa.spgemm_wwin(wwin)
+    oa.route_stats(reset=True)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_win(-1)
+        oa.spgemm_wwin(-1)
+    assert refops.same(X, R)
+
+
 @pytest.mark.parametrize("case", ["short", "long_b", "wide", "tiny", "nonpositive"])
 def test_spgemm_pattern(case):
     """amgd_spgemm_pattern (the constraint operator's pattern W_skel * W_skel'): operands
@@ -367,13 +414,16 @@ def rw(request):
     oa.spmv_rw(-1)
 
 
-@pytest.fixture(params=[2, 0], ids=["chunk", "segments"])
+@pytest.fixture(params=[2, 0, 3], ids=["chunk", "segments", "pipe"])
 def chunk(request):
     """whole-matrix long-row products: contiguous 16-byte-load chunks (k_spmv_chunk, at
-    every row length) or per-row segments (k_spmv_lane)"""
-    oa.spmv_chunk(request.param)
+    every row length), per-row segments (k_spmv_lane) or per-row segments with the gather
+    one round ahead (k_spmv_pipe, whole-matrix and listed rows)"""
+    oa.spmv_chunk(0 if request.param == 3 else request.param)
+    oa.spmv_pipe(3 if request.param == 3 else 0)
     yield request.param
     oa.spmv_chunk(-1)
+    oa.spmv_pipe(-1)
 
 
 def _adversarial_rows(rng, rn=700):
@@ -517,7 +567,7 @@ def test_spmv_long_rows_ragged(sl_min, rw, chunk):
 
 
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_rows_listed(sl_min, rw, mv_long):
+def test_spmv_rows_listed(sl_min, rw, mv_long, chunk):
     """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
     threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
     rng = np.random.default_rng(29)
