@@ -522,7 +522,26 @@ __global__ __launch_bounds__(256) void k_spmv(const uint64_t *ro, const uint32_t
     double t = 0;
     for (uint64_t c0 = b0; c0 < b1; c0 += SPMV_CH) {
       const uint64_t c1 = min(b1, c0 + SPMV_CH);
-      for (uint64_t k = c0 + tid; k < c1; k += 256) pv[k - c0] = x ? a[k] * x[col[k]] : a[k];
+      // eight (value, column) loads, then eight gathers, in flight per thread
+      for (uint64_t kb = c0 + tid; kb < c1; kb += 256 * 8) {
+        double av[8];
+        uint32_t cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint64_t k = kb + 256 * u;
+          av[u] = 0.0;
+          cv[u] = 0;
+          if (k < c1) {
+            av[u] = a[k];
+            if (x) cv[u] = col[k];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint64_t k = kb + 256 * u;
+          if (k < c1) pv[k - c0] = x ? av[u] * x[cv[u]] : av[u];
+        }
+      }
       __syncthreads();
       const uint64_t lo = max(k0, c0), hi = min(k1, c1);
 #pragma unroll 8
@@ -744,13 +763,14 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
 // during the adds of the current one: the gather of round r+1 (its columns arrived
 // during round r-1) and the (value, column) loads of round r+2.  Rows, segments and
 // the left-to-right adds from +0 are k_spmv_lane's: the same sums.
-template <bool LIST, int RW, int PER = 8>
+template <bool LIST, int RW, int PER = 8, bool AMX = false>
 __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
                                                    double beta, const uint8_t *f,
-                                                   uint32_t maxlen = 0xffffffffu) {
+                                                   uint32_t maxlen = 0xffffffffu,
+                                                   double *amx = nullptr, uint64_t *apos = nullptr) {
   constexpr int SEG = 64 * PER / RW;
   __shared__ double buf[4][RW][SEG + 1];
   __shared__ uint64_t rk0[4][RW];
@@ -796,6 +816,8 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
     for (int q = 0; q < PER; q++) g0[q] = x ? x[c0[q]] : 0.0;
     ld(SEG, a1, c1);
     double t = 0;
+    double pmx = -DBL_MAX;           // AMX: largest product, its entry (first on ties)
+    uint64_t ppos = ~0ull;
     for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
       for (int q = 0; q < PER; q++) {
@@ -825,9 +847,18 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
             for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
 #pragma unroll
             for (int e = 0; e < U; e++) t += u[e];
+            if (AMX) {
+#pragma unroll
+              for (int e = 0; e < U; e++)
+                if (u[e] > pmx) { pmx = u[e]; ppos = rk0[w][lane] + off + e0 + e; }
+            }
           }
         } else {
-          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+          for (uint32_t e = 0; e < m; e++) {
+            const double u = buf[w][lane][e];
+            t += u;
+            if (AMX && u > pmx) { pmx = u; ppos = rk0[w][lane] + off + e; }
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -840,6 +871,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
+      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
     }
   }
 }
@@ -1010,12 +1042,14 @@ static bool spmv_chunk_ok(const dcsr *M) {
       k_spmv_chunk<4, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_,  \
                                                      be, f_, amx_, apos_);                    \
   } while (0)
-// AMGD_SPMV_PIPE=1 / amgd_spmv_set_pipe(1): the lane products through k_spmv_pipe
-// (gather one round ahead; same sums)
+// AMGD_SPMV_PIPE bits / amgd_spmv_set_pipe: lane products through k_spmv_pipe (gather one
+// round ahead; same sums) -- 1 whole-matrix, 2 listed rows; entries per lane per round 8,
+// or 4 (bit 4), 16 (bit 8), 12 (bit 16).  Default 11: both, 16 per lane (256^3 SpMV
+// 6.26 -> 5.46 s; 8 per lane 5.64 s, 4: 6.98 s, 12: 7.95 s; tools/ab_setup.py, r03m)
 static int g_spmv_pipe = -1;
 extern "C" void amgd_spmv_set_pipe(int on) { g_spmv_pipe = on < 0 ? -1 : on; }
 static int spmv_pipe() {
-  if (g_spmv_pipe < 0) { const char *e = getenv("AMGD_SPMV_PIPE"); g_spmv_pipe = e && *e ? atoi(e) : 0; }
+  if (g_spmv_pipe < 0) { const char *e = getenv("AMGD_SPMV_PIPE"); g_spmv_pipe = e && *e ? atoi(e) : 11; }
   return g_spmv_pipe;
 }
 #define PIPE_LAUNCH_P(LIST, PER_, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_)               \
@@ -1263,6 +1297,15 @@ extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double 
   amgd_timer_start(1);
   if (spmv_chunk_ok(M))
     CHUNK_LAUNCH(true, rw_, g_, M->rn, x, z, 0.0, (const double *)nullptr, 1.0, (const uint8_t *)nullptr, amx, apos);
+  else if ((spmv_pipe() & 1) && rw_ == 64)
+    k_spmv_pipe<false, 64, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
+  else if ((spmv_pipe() & 1) && rw_ == 16)
+    k_spmv_pipe<false, 16, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
+  else if (spmv_pipe() & 1)
+    k_spmv_pipe<false, 4, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
+                                                              0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
   else if (rw_ == 64)
     k_spmv_lane<false, 64, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
                                                                 0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
@@ -2699,12 +2742,14 @@ static int sg_wt() {
 extern "C" void amgd_spgemm_set_wt(int t) { g_sg_wt = t < 0 ? -1 : t; }
 // AMGD_SG_WWIN bits: 1 windowed numeric rows, 2 wide symbolic rows, 4 the 4096- / 8192-slot
 // hash-bin numeric rows through the wave-private windowed kernel k_sg_wwin; 8: its numeric
-// window 1024 columns (else 2048)
+// window 1024 columns (else 2048); 16: symbolic byte windows of 4096 columns (else 16384).
+// Default 9: windowed numeric rows, 1024 columns (256^3 RAP kernels 1476 -> 1355 ms; the
+// symbolic and hash-bin routes were slower: +0.3 s / +1.5 s per setup, r03m)
 static int g_sg_wwin = -1;
 static int sg_wwin() {
   if (g_sg_wwin < 0) {
     const char *e = getenv("AMGD_SG_WWIN");
-    g_sg_wwin = e && *e ? atoi(e) : 0;
+    g_sg_wwin = e && *e ? atoi(e) : 9;
   }
   return g_sg_wwin;
 }
@@ -3214,7 +3259,11 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (hc[1]) {
     const int wsym = kseq ? sg_wsym() : 0;
     if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
-    if (wwin & 2)
+    if ((wwin & 2) && (wwin & 16))
+      k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+          nullptr, curs);
+    else if (wwin & 2)
       k_sg_wwin<16384, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
           nullptr, curs);

@@ -178,7 +178,7 @@ def test_spgemm_tiled_windows(case, win, wt):
     assert refops.same(X, R)
 
 
-@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8])
+@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8, 1 | 2 | 16])
 @pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
                                   "huge_a", "gapped", "dense_rows"])
 def test_spgemm_wave_windows(case, wwin):
@@ -420,7 +420,7 @@ def chunk(request):
     every row length), per-row segments (k_spmv_lane) or per-row segments with the gather
     one round ahead (k_spmv_pipe, whole-matrix and listed rows)"""
     oa.spmv_chunk(0 if request.param == 3 else request.param)
-    oa.spmv_pipe(3 if request.param == 3 else 0)
+    oa.spmv_pipe(11 if request.param == 3 else 0)
     yield request.param
     oa.spmv_chunk(-1)
     oa.spmv_pipe(-1)

@@ -271,12 +271,14 @@ def test_gpu_qfactor_reuse_matches_refactor(gen):
                                  ("p27_16", lambda: problems.poisson3d(16, 27)),
                                  ("sem_e4_N4", lambda: problems.sem_laplacian(4, 4, 4, 4, seed=5, jitter=0.3))],
                          ids=lambda g: g[0])
-def test_gpu_fs_fused_select_matches_separate(gen):
+@pytest.mark.parametrize("pipe", [0, 11], ids=["lane", "pipe"])
+def test_gpu_fs_fused_select_matches_separate(gen, pipe):
     """find_support's selection from the argmax kept by the fused w = R' rs product vs
-    the separate selection pass (and the lane path forced at every size): identical
-    hierarchies, and the fused path is taken"""
+    the separate selection pass (and the lane path forced at every size; k_spmv_lane or
+    k_spmv_pipe): identical hierarchies, and the fused path is taken"""
     Ai, Aj, Av = gen[1]()
     oa.spmv_sl_min(0)
+    oa.spmv_pipe(pipe)
     try:
         oa.fs_fused(1)
         oa.route_stats(reset=True)
@@ -287,5 +289,6 @@ def test_gpu_fs_fused_select_matches_separate(gen):
     finally:
         oa.fs_fused(-1)
         oa.spmv_sl_min(-1)
+        oa.spmv_pipe(-1)
     bad = parity.compare(h_s, h_f, exact=True)
     assert not bad, bad
