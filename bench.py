@@ -13,7 +13,7 @@ value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup
           allgatherv over xGMI, value = rows / max-over-ranks seconds, scaling
           "strong"; --mode replicas runs N independent setups (value = N x rows /
           max time, scaling "weak").
-roofline: the dominant kernel by time, the long-row SpMV (k_spmv_lane<false,RW>,
+roofline: the dominant kernel by time, the long-row SpMV (k_spmv_pipe<false,RW,16>,
           whole-matrix products: find_support's sweeps, PCG, Lanczos), event-timed
           live on the library stream; algorithmic bytes = 12 B per entry + 8 B per
           column (x read once) + 16 B per row; the rate with x gathered
@@ -330,7 +330,7 @@ def main():
                          "traffic_source": t_src,
                          "launches_per_setup": mv_n / steps,
                          "algorithmic_bytes_per_launch": mv_strict / mv_n if mv_n else None,
-                         "kernel": "k_spmv_lane<false,RW>: whole-matrix long-row SpMV (ordered row sums; "
+                         "kernel": "k_spmv_pipe<false,RW,16>: whole-matrix long-row SpMV (ordered row sums; "
                                    "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
                                    "HIP-event timed",
                          "algorithmic_bytes_per_setup": mv_strict / steps,
@@ -351,7 +351,7 @@ def main():
                          "traffic_source": t_src,
                          "traffic_over_algorithmic": t_rap * steps / rap_bytes if (t_rap and rap_bytes) else None,
                          "launches_per_setup": rap_n / steps,
-                         "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
+                         "kernel": "k_sg_kseq<NT,LG,1,1> + k_sg_row<NT,LG,1,1> + k_sg_wwin<W,1,1> + k_sg_win<W,1> + k_spgemm_long<1,1>: numeric "
                                    "passes of the RAP SpGEMMs (Af*W, W'*AfP, Acf*W; the first and last via their "
                                    "exact transposed products where those run faster) of every level, HIP-event timed",
                          "algorithmic_bytes_per_setup": rap_bytes / steps,

@@ -2742,14 +2742,16 @@ static int sg_wt() {
 extern "C" void amgd_spgemm_set_wt(int t) { g_sg_wt = t < 0 ? -1 : t; }
 // AMGD_SG_WWIN bits: 1 windowed numeric rows, 2 wide symbolic rows, 4 the 4096- / 8192-slot
 // hash-bin numeric rows through the wave-private windowed kernel k_sg_wwin; 8: its numeric
-// window 1024 columns (else 2048); 16: symbolic byte windows of 4096 columns (else 16384).
-// Default 9: windowed numeric rows, 1024 columns (256^3 RAP kernels 1476 -> 1355 ms; the
-// symbolic and hash-bin routes were slower: +0.3 s / +1.5 s per setup, r03m)
+// window 1024 columns (64: 512; else 2048); 16: symbolic byte windows of 4096 columns (32:
+// 2048; else 16384).
+// Default 27: windowed numeric rows at 1024 columns (256^3 RAP kernels 1476 -> 1355 ms) and
+// the wide symbolic rows at 4096-column byte windows (setup -0.2 s; 16384: +1.2 s, 2048:
+// +0.35 s); numeric 512 columns +0.3 s, hash-bin rows +1.5 s (tools/ab_setup.py, r03m)
 static int g_sg_wwin = -1;
 static int sg_wwin() {
   if (g_sg_wwin < 0) {
     const char *e = getenv("AMGD_SG_WWIN");
-    g_sg_wwin = e && *e ? atoi(e) : 9;
+    g_sg_wwin = e && *e ? atoi(e) : 27;
   }
   return g_sg_wwin;
 }
@@ -3259,7 +3261,11 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (hc[1]) {
     const int wsym = kseq ? sg_wsym() : 0;
     if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
-    if ((wwin & 2) && (wwin & 16))
+    if ((wwin & 2) && (wwin & 32))
+      k_sg_wwin<2048, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+          nullptr, curs);
+    else if ((wwin & 2) && (wwin & 16))
       k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
           nullptr, curs);
@@ -3387,7 +3393,8 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     const unsigned nrw = (nr);                                                                  \
     const int g = (int)std::min<unsigned>(nrw, 16384u);                                         \
     const int wt = sg_wt();                                                                     \
-    if ((wwin & 1) && (wwin & 8)) SG_WW(1024, rows_, nrw);                                      \
+    if ((wwin & 1) && (wwin & 64)) SG_WW(512, rows_, nrw);                                      \
+    else if ((wwin & 1) && (wwin & 8)) SG_WW(1024, rows_, nrw);                                 \
     else if (wwin & 1) SG_WW(2048, rows_, nrw);                                                 \
     else if (wt == 4 && win == 2048) SG_WT(2048, 4, rows_);                                         \
     else if (wt == 8 && win == 2048) SG_WT(2048, 8, rows_);                                         \

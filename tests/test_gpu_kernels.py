@@ -178,7 +178,7 @@ def test_spgemm_tiled_windows(case, win, wt):
     assert refops.same(X, R)
 
 
-@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8, 1 | 2 | 16])
+@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8, 1 | 2 | 16, 1 | 2 | 32 | 64])
 @pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
                                   "huge_a", "gapped", "dense_rows"])
 def test_spgemm_wave_windows(case, wwin):

@@ -1,10 +1,10 @@
 """Calibration of the PMC byte counters for the lane SpMV's own access pattern
 (MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for 16-B-per-lane streaming reads;
-"calibrate on a known byte count in your own access pattern").  Runs k_spmv_lane on a
+"calibrate on a known byte count in your own access pattern").  Runs the default long-row SpMV (k_spmv_pipe; k_spmv_lane before round 3) on a
 generated matrix far larger than the 256 MiB Infinity Cache, ordered row sums (x = NULL:
 no gather), so the bytes read are known exactly: 12 B per entry + 8 B per row offset;
 written: 8 B per row.  Run under rocprofv3 --pmc FETCH_SIZE (or WRITE_SIZE) with
---kernel-include-regex k_spmv_lane; prints the known byte counts as JSON.
+--kernel-include-regex 'k_spmv_(lane|pipe)'; prints the known byte counts as JSON.
 usage: python tools/pmc_calib.py [rows] [mean_row] [reps]"""
 import ctypes as C
 import json

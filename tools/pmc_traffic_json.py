@@ -29,13 +29,13 @@ fk, fn = counter(f"{d0}/calib_FETCH_SIZE", "FETCH_SIZE")
 wk, wn = counter(f"{d0}/calib_WRITE_SIZE", "WRITE_SIZE")
 f_fetch = cal["read_bytes_per_product"] / (fk * 1024 / fn)
 f_write = cal["write_bytes_per_product"] / (wk * 1024 / wn)
-names = {"spmv": "k_spmv_lane<false,RW> (roofline kernel)",
+names = {"spmv": "k_spmv_pipe<false,RW,16> (roofline kernel)",
          "rap": "RAP SpGEMM numeric kernels (rap_roofline)"}
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per pass (tools/gpurun_pmc.sh), "
                  f"one 256^3 setup (tools/probe_scale.py 256), tree of {tag}",
        "workload": {"m": 256, "stencil": 7, "world": 1},
        "units": "bytes per setup",
-       "calibration": {"kernel": "k_spmv_lane<false,16>, ordered row sums of a generated matrix "
+       "calibration": {"kernel": "k_spmv_pipe<false,16,16>, ordered row sums of a generated matrix "
                                  "(tools/pmc_calib.py)", **cal,
                        "FETCH_SIZE_KB_per_product": fk / fn, "WRITE_SIZE_KB_per_product": wk / wn,
                        "fetch_factor": f_fetch, "write_factor": f_write,

@@ -1,4 +1,4 @@
-"""Sum the RAP SpGEMM numeric kernels (k_sg_row / k_sg_kseq / k_sg_win / k_spgemm_long, RAP=1) in a
+"""Sum the RAP SpGEMM numeric kernels (k_sg_row / k_sg_kseq / k_sg_win / k_sg_wwin / k_spgemm_long, RAP=1) in a
 rocprofv3 --stats kernel_stats.csv, to cross-check bench.py's event-timed
 roofline.kernel_ms_per_setup.  Usage: python tools/rap_from_prof.py <kernel_stats.csv> [setups]"""
 import csv
@@ -7,7 +7,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 setups = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-pat = re.compile(r"k_sg_(row|kseq)<\d+, \d+, 1, 1>|k_sg_win<\d+, 1>|k_spgemm_long<1, 1>")
+pat = re.compile(r"k_sg_(row|kseq)<\d+, \d+, 1, 1>|k_sg_win<\d+, 1>|k_sg_wwin<\d+, 1, 1>|k_spgemm_long<1, 1>")
 tot, calls = 0.0, 0
 for r in rows:
     if pat.search(r["Name"]):
