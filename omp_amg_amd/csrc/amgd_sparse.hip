@@ -3023,6 +3023,9 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
   uint8_t *mp = lds + wv * WB;
   uint32_t *mp32 = (uint32_t *)mp;
   const uint64_t ltm = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // curs holds nnz(A) cursors from A's first entry: a row-range view of a larger matrix
+  // (sharded products) keeps absolute row offsets
+  const uint64_t cbase = aro[0];
   for (uint32_t r = blockIdx.x * NWV + wv; r < nrows; r += gridDim.x * NWV) {
     const uint32_t i = rows[r];
     const uint64_t a0 = aro[i];
@@ -3054,7 +3057,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
           lb0 = bro[k];
           llen = (uint32_t)(bro[k + 1] - lb0);
           if (MODE) lav = aa[a0 + e];
-          if (!first) lcur = curs[a0 + e];
+          if (!first) lcur = curs[a0 - cbase + e];
           if (lcur < llen) lpk = bcol[lb0 + lcur];
         }
       }
@@ -3135,7 +3138,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
         uint32_t m = lpk;
         for (int o = 32; o; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
         nmin = min(nmin, m);
-        if (!single && c0 + lane < nl) curs[a0 + c0 + lane] = lcur;
+        if (!single && c0 + lane < nl) curs[a0 - cbase + c0 + lane] = lcur;
       }
       if (MODE) {                                      // emit in column order
         for (int q = 0; q < W; q += 64) {
