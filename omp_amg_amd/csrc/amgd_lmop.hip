@@ -216,7 +216,6 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
   __shared__ uint32_t wend[NT];
   __shared__ uint64_t wtc[NT], wqq[NT];
   __shared__ double wu[NT];
-  __shared__ uint32_t wpf[NT], wj0[NT];
   __shared__ uint32_t wtot[NT / 64];
   const int t = threadIdx.x;
   for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
@@ -231,7 +230,7 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
       const uint32_t clo = cols[0], chi = cols[wn - 1];
       for (uint64_t eb = e0; eb < e1; eb += NT) {
         const uint64_t e = eb + t;
-        uint32_t len = 0, pf = 0, j0 = 0;
+        uint32_t len = 0;
         uint64_t tc = 0, qq = 0;
         double uc = 0.0;
         if (e < e1) {
@@ -249,8 +248,6 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
               tc = t0 + mlo;
               qq = qqoff[c] + (uint64_t)kpos[e] * nz + mlo;
               uc = u[c];
-              j0 = tcol[tc];
-              pf = lb_u32(cols, wn, j0);           // the layer's first position
             }
           }
         }
@@ -259,8 +256,6 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
         wtc[t] = tc;
         wqq[t] = qq;
         wu[t] = uc;
-        wpf[t] = pf;
-        wj0[t] = j0;
         __syncthreads();
         const uint32_t T = wend[NT - 1];
         for (uint32_t q0 = 0; q0 < T; q0 += NT) {
@@ -279,13 +274,7 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
             const uint32_t off = q - (l ? wend[l - 1] : 0u);
             const uint32_t j = tcol[wtc[l] + off];
             x = wu[l] * QQ[wqq[l] + off];
-            // the layer's columns ascend and, without a miss, every one is in the
-            // (strictly ascending) window: its position lies in [pf + off, pf + j - j0]
-            // (a miss anywhere makes the caller redo S exactly, so narrower bounds
-            // after a miss cannot leak into the result; a hit is always verified)
-            const uint32_t lo0 = wpf[l] + off;
-            const uint32_t hi0 = (uint32_t)min((uint64_t)wn, (uint64_t)wpf[l] + (j - wj0[l]) + 1);
-            p = lo0 < hi0 ? lo0 + lb_u32(cols + lo0, hi0 - lo0, j) : wn;
+            p = lb_u32(cols, wn, j);
             if (p >= wn || cols[p] != j) { atomicAdd(miss, 1u); p = 0xffffffffu; }
           }
           // layers of this chunk: entries [lf, ll]
