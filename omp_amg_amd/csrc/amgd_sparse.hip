@@ -3259,8 +3259,9 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
   const int wwin = kseq ? sg_wwin() : 0;
+  const int wflat = !kseq && (sg_wwin() & 128) ? sg_wwin() : 0;   // short-B-row hash bins
   uint32_t *curs = nullptr;
-  if (wwin) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
+  if (wwin || wflat) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
   if (hc[1]) {
     const int wsym = kseq ? sg_wsym() : 0;
     if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
@@ -3474,6 +3475,15 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
     else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
   } else {
+    if (wflat) {                 // AMGD_SG_WWIN bit 128: bins 1-3 through k_sg_wwin (1024 columns)
+      for (int q = 1; q < 4; q++) {
+        const unsigned nb = hn[q];
+        if (!nb) continue;
+        ww_launches++;
+        SG_WW(1024, lists + q * L, nb);
+        hn[q] = 0;
+      }
+    }
     SG_NUM(k_sg_row, 64, 9, 0, 65536u)
     SG_NUM(k_sg_row, 64, 11, 1, 65536u)
     SG_NUM(k_sg_row, 64, 12, 2, 65536u)

@@ -225,6 +225,30 @@ def test_spgemm_wave_windows(case, wwin):
     assert refops.same(X, R)
 
 
+@pytest.mark.parametrize("case", ["mid", "wide", "dups", "spread"])
+def test_spgemm_wave_windows_short_b(case):
+    """short B rows (flat products) through k_sg_wwin (AMGD_SG_WWIN bit 128: the hash bins
+    1-3 of k_sg_row): bit for bit the host restatement"""
+    rng = np.random.default_rng({"mid": 101, "wide": 102, "dups": 103, "spread": 104}[case])
+    if case == "mid":
+        A, B = refops.rand_csr(rng, 500, 400, 0.05), refops.rand_csr(rng, 400, 3000, 0.01)
+    elif case == "wide":
+        A, B = refops.rand_csr(rng, 80, 2000, 0.05), refops.rand_csr(rng, 2000, 50000, 0.0008)
+    elif case == "dups":
+        A, B = _banded(rng, 157, 300, 5000, 80, 0.8, 30, 2500, dups=True)
+    else:
+        A, B = refops.rand_csr(rng, 60, 3000, 0.05, ints=True), refops.rand_csr(rng, 3000, 900000, 0.00002, ints=True)
+    assert B.a.size < 64 * B.rn
+    R = refops.spgemm(A, B)
+    oa.spgemm_flat(False)
+    oa.spgemm_wwin(27 | 128)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.spgemm_wwin(-1)
+    assert refops.same(X, R)
+
+
 @pytest.mark.parametrize("case", ["short", "long_b", "wide", "tiny", "nonpositive"])
 def test_spgemm_pattern(case):
     """amgd_spgemm_pattern (the constraint operator's pattern W_skel * W_skel'): operands
