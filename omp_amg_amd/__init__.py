@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
         L.amgd_test_spgemm_wwin.argtypes = [C.c_int]
         L.amgd_test_spmv_pipe.argtypes = [C.c_int]
+        L.amgd_test_lmop_small.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
@@ -440,6 +441,12 @@ def sg_pattern(on: int) -> None:
     """constraint pattern W_skel*W_skel': 1 pattern-only product (default), 0 the full
     product (values discarded by interp_lmop), -1 default.  Same bits."""
     lib().amgd_test_sg_pattern(int(on))
+
+
+def lmop_small(n: int) -> None:
+    """interp_lmop row pull: S rows of <= 32 entries one thread each (n > 0) or on the
+    wavefront kernel (0); -1: back to the env (AMGD_LMOP_SMALL)"""
+    lib().amgd_test_lmop_small(int(n))
 
 
 def spmv_pipe(m: int) -> None:

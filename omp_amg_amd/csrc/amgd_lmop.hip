@@ -306,20 +306,78 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
   }
 }
 
+// S rows by length: (0, small] -> ls (thread per row), (small, lim] -> l0 (wave), > lim -> l1
 __global__ void k_srow_bins(const uint64_t *sro, uint32_t n, uint32_t lim, uint32_t *l0,
-                            uint32_t *l1, unsigned *cnt) {
+                            uint32_t *l1, unsigned *cnt, uint32_t small, uint32_t *ls) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (n + stride - 1) / stride;
   for (uint64_t it = 0; it < iters; it++) {
     uint64_t i = i0 + it * stride;
     uint64_t L = i < n ? sro[i + 1] - sro[i] : 0;
-    bool a = L > 0 && L <= lim, b = L > lim;
+    bool s = L > 0 && L <= small, a = L > small && L <= lim, b = L > lim;
     unsigned pa = wave_append(&cnt[0], a);
     unsigned pb = wave_append(&cnt[1], b);
+    unsigned ps = wave_append(&cnt[2], s);
     if (a) l0[pa] = (uint32_t)i;
     if (b) l1[pb] = (uint32_t)i;
+    if (s) ls[ps] = (uint32_t)i;
   }
+}
+// Row pull for short S rows (<= SC entries: the fine levels, 10^6 - 10^7 rows of a few
+// dozen): one THREAD per row instead of a wavefront.  The row's columns and values sit
+// in this thread's LDS column slice; its W_skel entries are taken in ascending c (the
+// layers of k_lmop_pull), and each support's columns, ascending, are matched to the
+// row's ascending columns by one forward merge pointer.  Every S entry receives its
+// contributions u_c * QQ in ascending c on top of its current value -- k_lmop_pull's
+// sums; a column missing from the row counts a miss (the caller then redoes S exactly).
+template <int SC>
+__global__ __launch_bounds__(128) void k_lmop_pull_small(
+    const uint32_t *rows, uint32_t nrows, const uint64_t *sro, const uint32_t *scol, double *sa,
+    const uint64_t *wro, const uint32_t *wcol, const uint32_t *kpos, const uint64_t *tro,
+    const uint32_t *tcol, const uint8_t *dirty, uint32_t ca, uint32_t cb, const double *u,
+    const double *QQ, const uint64_t *qqoff, unsigned *miss) {
+  __shared__ uint32_t cs[SC][128];
+  __shared__ double vs[SC][128];
+  const int t = threadIdx.x;
+  GRID_STRIDE(r, nrows) {
+    const uint32_t i = rows[r];
+    const uint64_t s0 = sro[i];
+    const uint32_t n = (uint32_t)(sro[i + 1] - s0);
+    for (uint32_t q = 0; q < n; q++) { cs[q][t] = scol[s0 + q]; vs[q][t] = sa[s0 + q]; }
+    unsigned nmiss = 0;
+    const uint64_t e1 = wro[i + 1];
+    for (uint64_t e = wro[i]; e < e1; e++) {
+      const uint32_t c = wcol[e];
+      if (c < ca || c >= cb || dirty[c]) continue;
+      const uint64_t t0 = tro[c];
+      const uint32_t nz = (uint32_t)(tro[c + 1] - t0);
+      const uint64_t qq = qqoff[c] + (uint64_t)kpos[e] * nz;
+      const double uc = u[c];
+      uint32_t p = 0;
+      for (uint32_t m = 0; m < nz; m++) {
+        const uint32_t j = tcol[t0 + m];
+        while (p < n && cs[p][t] < j) p++;
+        if (p < n && cs[p][t] == j) {
+          vs[p][t] = vs[p][t] + uc * QQ[qq + m];
+          p++;
+        } else {
+          nmiss++;
+        }
+      }
+    }
+    if (nmiss) atomicAdd(miss, nmiss);
+    for (uint32_t q = 0; q < n; q++) sa[s0 + q] = vs[q][t];
+  }
+}
+// AMGD_LMOP_SMALL=1: S rows of at most 32 entries take k_lmop_pull_small.  Off by
+// default: bit-exact (tests) but slower at 256^3 (27.64 vs 26.77 s per setup in one A/B,
+// r03r: a thread walks ~50 contributions with dependent loads at 6 waves per CU)
+static int g_lmop_small = -1;
+extern "C" void amgd_lmop_set_small(int n) { g_lmop_small = n; }
+static uint32_t lmop_small() {
+  if (g_lmop_small < 0) { const char *e = getenv("AMGD_LMOP_SMALL"); g_lmop_small = e && *e ? atoi(e) : 0; }
+  return g_lmop_small > 0 ? 32u : 0u;
 }
 
 // kpos[e] = position of the row of W_skel entry e inside its column's support
@@ -395,13 +453,14 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, cons
   }
   // S rows binned by length: wave / 1024-wide window, 256 threads / 4096-wide windows
   const uint32_t nf = S->rn;
-  uint32_t *rl = (uint32_t *)amgd_alloc(2 * ((size_t)nf + 1) * 4);
-  uint32_t *rl1 = rl + nf + 1;
-  unsigned *rc = (unsigned *)amgd_alloc(8);
-  amgd_memset(rc, 0, 8);
-  k_srow_bins<<<grid_for(nf), 256, 0, s>>>(S->ro, nf, 1024, rl, rl1, rc);
-  unsigned hrc[2];
-  amgd_d2h(hrc, rc, 8);
+  uint32_t *rl = (uint32_t *)amgd_alloc(3 * ((size_t)nf + 1) * 4);
+  uint32_t *rl1 = rl + nf + 1, *rls = rl1 + nf + 1;
+  unsigned *rc = (unsigned *)amgd_alloc(16);
+  amgd_memset(rc, 0, 12);
+  const uint32_t small = lmop_small();
+  k_srow_bins<<<grid_for(nf), 256, 0, s>>>(S->ro, nf, 1024, rl, rl1, rc, small, rls);
+  unsigned hrc[3];
+  amgd_d2h(hrc, rc, 12);
   // QQt chunks by coarse range within the memory budget
   uint64_t *sz = (uint64_t *)amgd_alloc(((size_t)nc + 1) * 8);
   k_qq_size<<<grid_for(nc), 256, 0, s>>>(Wt->ro, dirty, nc, 0, nc, sz);
@@ -437,6 +496,10 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, cons
           lc, nl, tp, ntiles, Wt->ro, Q, qoff, sz, (double *)QQb);
     }
     KCHECK();
+    if (hrc[2])
+      k_lmop_pull_small<32><<<grid_for(hrc[2], 128, 16384), 128, 0, s>>>(
+          rls, hrc[2], S->ro, S->col, S->a, Wskel->ro, Wskel->col, kpos, Wt->ro, Wt->col, dirty, ca,
+          cb, u, QQb, sz, miss);
     if (hrc[0])
       k_lmop_pull<64, 1024><<<(int)std::min<unsigned>(hrc[0], 1u << 20), 64, 0, s>>>(
           rl, hrc[0], S->ro, S->col, S->a, Wskel->ro, Wskel->col, kpos, Wt->ro, Wt->col, dirty, ca,

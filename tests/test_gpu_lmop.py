@@ -31,10 +31,17 @@ def _run(Ai, Aj, Av, mode):
     ("p2d9_40", lambda: problems.poisson2d(40, 9)),
     ("sem_e3_N3", lambda: problems.sem_laplacian(3, 3, 3, 3, seed=5, jitter=0.3)),
 ], ids=lambda g: g[0])
-def test_lmop_fast_equals_general(gen):
+@pytest.mark.parametrize("small", [1, 0], ids=["small_rows_thread", "small_rows_wave"])
+def test_lmop_fast_equals_general(gen, small):
+    """row pull (S rows of <= 32 entries one thread each, or all on wavefronts) against
+    the general walk"""
     Ai, Aj, Av = gen[1]()
     hg, sg = _run(Ai, Aj, Av, 1)
-    hf, sf = _run(Ai, Aj, Av, 0)
+    oa.lmop_small(small)
+    try:
+        hf, sf = _run(Ai, Aj, Av, 0)
+    finally:
+        oa.lmop_small(-1)
     assert sg["fast"] == 0 and sg["general"] > 0
     assert sf["fast"] > 0, sf
     assert sf["misses"] == 0, sf
