@@ -107,6 +107,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_wwin.argtypes = [C.c_int]
         L.amgd_test_spmv_pipe.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
+        L.amgd_test_spmv_sum2.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
@@ -441,6 +442,12 @@ def sg_pattern(on: int) -> None:
     """constraint pattern W_skel*W_skel': 1 pattern-only product (default), 0 the full
     product (values discarded by interp_lmop), -1 default.  Same bits."""
     lib().amgd_test_sg_pattern(int(on))
+
+
+def spmv_sum2(on: int) -> None:
+    """find_support: sumR re-summed in the full sweeps' w = R' rs pass (1) or by the listed
+    column sums after each selection (0); -1: back to the env (AMGD_SPMV_SUM2)"""
+    lib().amgd_test_spmv_sum2(int(on))
 
 
 def lmop_small(n: int) -> None:

@@ -231,8 +231,13 @@ void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] s
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                         const double *w, double *sumR, double thr,
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved,
-                        const uint64_t *apos);   /* apos: per-column argmax of the sweep's w
+                        const uint64_t *apos,    /* apos: per-column argmax of the sweep's w
                                                     product (amgd_spmv_amax), or NULL */
+                        uint32_t skip_above);    /* more selections than this: sumR is left
+                                                    to the next (full) sweep's amgd_spmv_sum2 */
+/* z = M x and z2 = M 1 from one pass (find_support's w = R' rs and sumR); 0: not taken */
+int amgd_spmv_sum2_ok(const dcsr *M);
+int amgd_spmv_sum2(const dcsr *M, const double *x, double *z, double *z2);
 /* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
    returns the count, > cap when the list overflowed */
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,

@@ -2473,7 +2473,7 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
                                    double *rs, const double *w, double *sumR,
                                    double thr, uint32_t *sel_i, uint32_t *sel_j,
-                                   uint32_t *nremoved, const uint64_t *apos) {
+                                   uint32_t *nremoved, const uint64_t *apos, uint32_t skip_above) {
   hipStream_t s = amgd_s();
   const uint32_t nc = Rt->rn;
   uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
@@ -2516,7 +2516,7 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
     const dcsr *M[2] = {Rl, Rt};
     const uint32_t *L[2] = {sel_i, sel_j};
     double *O[2] = {rs, sumR};
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < (h[0] > skip_above ? 1 : 2); q++) {
       if (M[q]->nnz <= 32ull * M[q]->rn)
         k_list_rowsum_t<<<grid_for(h[0]), 256, 0, s>>>(M[q]->ro, M[q]->a, L[q], h[0], O[q]);
       else

@@ -545,6 +545,11 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
      the very products the selection compares, so the selection needs no second pass */
   double *amx = dalloc(nc);
   uint64_t *apos = (uint64_t *)amgd_alloc((size_t)nc * 8 + 8);
+  /* full sweeps on long-row R' re-sum sumR in the w = R'*rs pass itself (the same ordered
+     row sums of R' as amgd_colsum): a sweep whose successor is certainly full (too many
+     selections for the incremental path) leaves sumR to it instead of re-summing the
+     selected columns */
+  const int sum2 = amgd_spmv_sum2_ok(Rt);
   ph(PH_FS);
   for (;;) {
     it++;
@@ -571,7 +576,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
     }
     if (!done) {
       fused = amgd_spmv_amax(Rt, rs, w, amx, apos);       /* w = R'*rs (row order) */
-      if (!fused) amgd_spmvt(Rt, rs, w);
+      if (!fused && !(sum2 && amgd_spmv_sum2(Rt, rs, w, sumR))) amgd_spmvt(Rt, rs, w);
       amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       amgd_spmvt(Rt, tmp, w2);                            /* w2 = R'*(R*w) */
     }
@@ -584,8 +589,11 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
+    /* the next sweep is full when this one selects more than the incremental path takes
+       (cap_c), or when sweeps are never incremental: then its w = R'*rs pass re-sums sumR */
+    const uint32_t skip_above = sum2 ? (fs_inc ? cap_c : 0u) : 0xffffffffu;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem,
-                                   fused ? apos : NULL);
+                                   fused ? apos : NULL, skip_above);
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;

@@ -763,16 +763,20 @@ __global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uin
 // during the adds of the current one: the gather of round r+1 (its columns arrived
 // during round r-1) and the (value, column) loads of round r+2.  Rows, segments and
 // the left-to-right adds from +0 are k_spmv_lane's: the same sums.
-template <bool LIST, int RW, int PER = 8, bool AMX = false>
+// SUM2: the same pass also writes each row's plain ordered sum of its values to z2
+// (find_support: w = R' rs and sumR = sum(R, 1) -- the column sums of R -- from one read)
+template <bool LIST, int RW, int PER = 8, bool AMX = false, bool SUM2 = false>
 __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
                                                    double beta, const uint8_t *f,
                                                    uint32_t maxlen = 0xffffffffu,
-                                                   double *amx = nullptr, uint64_t *apos = nullptr) {
+                                                   double *amx = nullptr, uint64_t *apos = nullptr,
+                                                   double *z2 = nullptr) {
   constexpr int SEG = 64 * PER / RW;
   __shared__ double buf[4][RW][SEG + 1];
+  __shared__ double buf2[SUM2 ? 4 : 1][SUM2 ? RW : 1][SUM2 ? SEG + 1 : 1];
   __shared__ uint64_t rk0[4][RW];
   __shared__ uint32_t rlen[4][RW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -815,7 +819,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
 #pragma unroll
     for (int q = 0; q < PER; q++) g0[q] = x ? x[c0[q]] : 0.0;
     ld(SEG, a1, c1);
-    double t = 0;
+    double t = 0, t2 = 0;
     double pmx = -DBL_MAX;           // AMX: largest product, its entry (first on ties)
     uint64_t ppos = ~0ull;
     for (uint32_t off = 0; off < mx; off += SEG) {
@@ -823,6 +827,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
       for (int q = 0; q < PER; q++) {
         const int fl = q * 64 + lane;
         buf[w][fl / SEG][fl % SEG] = x ? a0[q] * g0[q] : a0[q];
+        if (SUM2) buf2[w][fl / SEG][fl % SEG] = a0[q];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -845,8 +850,16 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
             double u[U];
 #pragma unroll
             for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
+            if (SUM2) {
+              double u2[U];
 #pragma unroll
-            for (int e = 0; e < U; e++) t += u[e];
+              for (int e = 0; e < U; e++) u2[e] = buf2[w][lane][e0 + e];
+#pragma unroll
+              for (int e = 0; e < U; e++) { t += u[e]; t2 += u2[e]; }
+            } else {
+#pragma unroll
+              for (int e = 0; e < U; e++) t += u[e];
+            }
             if (AMX) {
 #pragma unroll
               for (int e = 0; e < U; e++)
@@ -857,6 +870,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
           for (uint32_t e = 0; e < m; e++) {
             const double u = buf[w][lane][e];
             t += u;
+            if (SUM2) t2 += buf2[w][lane][e];
             if (AMX && u > pmx) { pmx = u; ppos = rk0[w][lane] + off + e; }
           }
         }
@@ -872,6 +886,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
       if (AMX) { amx[i] = pmx; apos[i] = ppos; }
+      if (SUM2) z2[i] = 1.0 * t2;              // amgd_colsum's beta * t
     }
   }
 }
@@ -1280,7 +1295,7 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
 // (find_support: w = R' rs and the selection's argmax of R(i,c) rs_i per column c, in one
 // pass over R').  Only the whole-matrix lane kernel path (long rows, one GPU); returns 0
 // where that path does not apply -- the caller then multiplies and selects separately.
-static int g_fs_fused = -1;     // AMGD_FS_FUSED=0 / amgd_spmv_set_fused(0): separate selection pass
+static int g_fs_fused = -1;     // AMGD_FS_FUSED=1 / amgd_spmv_set_fused(1): fused selection
 extern "C" void amgd_spmv_set_fused(int on) { g_fs_fused = on < 0 ? -1 : on; }
 extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos) {
   if (M->rn == 0 || amgd_nshards() > 1 || M->nnz < 32ull * M->rn || (int64_t)M->rn < sl_min_whole())
@@ -1318,6 +1333,40 @@ extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double 
   amgd_timer_stop(1);
   KCHECK();
   const uint64_t rest = 16ull * M->rn + 8;
+  g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
+  g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
+  g_mv_launches++;
+  return 1;
+}
+// z = M x and z2 = M 1 (each row's ordered sum of its values, amgd_colsum on M = R') from
+// one pass over M: find_support's w = R' rs and sumR.  Only where the whole-matrix
+// k_spmv_pipe path applies (long rows, one GPU, AMGD_SPMV_SUM2 not 0); returns 0 otherwise.
+static int g_spmv_sum2 = -1;
+extern "C" void amgd_spmv_set_sum2(int on) { g_spmv_sum2 = on < 0 ? -1 : on; }
+extern "C" int amgd_spmv_sum2_ok(const dcsr *M) {
+  if (g_spmv_sum2 < 0) { const char *e = getenv("AMGD_SPMV_SUM2"); g_spmv_sum2 = e && *e ? atoi(e) : 1; }
+  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 0; }
+  return g_spmv_sum2 && !g_fs_fused && M->rn && amgd_nshards() <= 1 && M->nnz >= 32ull * M->rn &&
+         (int64_t)M->rn >= sl_min_whole() && (spmv_pipe() & 1) && !spmv_chunk_ok(M);
+}
+extern "C" int amgd_spmv_sum2(const dcsr *M, const double *x, double *z, double *z2) {
+  if (!amgd_spmv_sum2_ok(M)) return 0;
+  const int rw_ = lane_rw(M->rn);
+  const int g_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
+  amgd_route_hit(AMGD_R_SPMV_LANE);
+  amgd_timer_start(1);
+  if (rw_ == 64)
+    k_spmv_pipe<false, 64, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
+        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
+  else if (rw_ == 16)
+    k_spmv_pipe<false, 16, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
+        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
+  else
+    k_spmv_pipe<false, 4, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
+        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
+  amgd_timer_stop(1);
+  KCHECK();
+  const uint64_t rest = 24ull * M->rn + 8;
   g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
   g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
   g_mv_launches++;

@@ -196,6 +196,8 @@ void amgd_spmv_set_chunk(int on);
 API void amgd_test_spmv_chunk(int on) { amgd_spmv_set_chunk(on); }
 void amgd_lmop_set_small(int n);
 API void amgd_test_lmop_small(int n) { amgd_lmop_set_small(n); }
+void amgd_spmv_set_sum2(int on);
+API void amgd_test_spmv_sum2(int on) { amgd_spmv_set_sum2(on); }
 void amgd_spmv_set_pipe(int on);
 API void amgd_test_spmv_pipe(int on) { amgd_spmv_set_pipe(on); }
 void amgd_spmv_set_fused(int on);
