@@ -370,13 +370,13 @@ __global__ __launch_bounds__(128) void k_lmop_pull_small(
     for (uint32_t q = 0; q < n; q++) sa[s0 + q] = vs[q][t];
   }
 }
-// AMGD_LMOP_SMALL=1: S rows of at most 32 entries take k_lmop_pull_small.  Off by
-// default: bit-exact (tests) but slower at 256^3 (27.64 vs 26.77 s per setup in one A/B,
-// r03r: a thread walks ~50 contributions with dependent loads at 6 waves per CU)
+// AMGD_LMOP_SMALL (default 1; 0: off): S rows of at most 32 entries take
+// k_lmop_pull_small -- 256^3 setup -0.1 to -0.2 s in interleaved A/Bs
+// (profiles/r03/ab256_r03s2_*, ab256_r03t_*)
 static int g_lmop_small = -1;
 extern "C" void amgd_lmop_set_small(int n) { g_lmop_small = n; }
 static uint32_t lmop_small() {
-  if (g_lmop_small < 0) { const char *e = getenv("AMGD_LMOP_SMALL"); g_lmop_small = e && *e ? atoi(e) : 0; }
+  if (g_lmop_small < 0) { const char *e = getenv("AMGD_LMOP_SMALL"); g_lmop_small = e && *e ? atoi(e) : 1; }
   return g_lmop_small > 0 ? 32u : 0u;
 }
 
