@@ -306,15 +306,16 @@ __global__ __launch_bounds__(NT) void k_lmop_pull(
   }
 }
 
-// S rows by length: (0, small] -> ls (thread per row), (small, lim] -> l0 (wave), > lim -> l1
-__global__ void k_srow_bins(const uint64_t *sro, uint32_t n, uint32_t lim, uint32_t *l0,
+// S rows [r0, r0 + n) by length: (0, small] -> ls (thread per row), (small, lim] -> l0
+// (wave), > lim -> l1
+__global__ void k_srow_bins(const uint64_t *sro, uint32_t r0, uint32_t n, uint32_t lim, uint32_t *l0,
                             uint32_t *l1, unsigned *cnt, uint32_t small, uint32_t *ls) {
   uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t iters = (n + stride - 1) / stride;
   for (uint64_t it = 0; it < iters; it++) {
-    uint64_t i = i0 + it * stride;
-    uint64_t L = i < n ? sro[i + 1] - sro[i] : 0;
+    uint64_t i = r0 + i0 + it * stride;
+    uint64_t L = i < (uint64_t)r0 + n ? sro[i + 1] - sro[i] : 0;
     bool s = L > 0 && L <= small, a = L > small && L <= lim, b = L > lim;
     unsigned pa = wave_append(&cnt[0], a);
     unsigned pb = wave_append(&cnt[1], b);
@@ -397,6 +398,7 @@ extern "C" uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm) {
 extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff,
                                   const double *u, uint32_t cb, uint32_t ce);
 
+#define LMOP_SHARD_MIN (1ull << 24)   // S entries below which every rank pulls all rows
 static uint64_t qq_budget() {
   static uint64_t b = 0;
   if (!b) {
@@ -451,14 +453,29 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, cons
     g_lmop_stats[2]++;
     amgd_lmop_general(S, Wt, Q, qoff, u, 0, dend);
   }
-  // S rows binned by length: wave / 1024-wide window, 256 threads / 4096-wide windows
+  // S rows binned by length: thread / wave with a 1024-wide window / 256 threads with
+  // 4096-wide windows.  Multi-GPU: S rows are independent, so each rank pulls the rows of
+  // its shards (contiguous ranges of equal S nnz) and one allgatherv of the values
+  // completes S everywhere (the dirty prefix above ran on every rank, over all rows)
   const uint32_t nf = S->rn;
+  const int N = amgd_nshards();
+  const bool sharded = N > 1 && nf >= (uint32_t)N && amgd_shard_worth(S->nnz, LMOP_SHARD_MIN);
+  std::vector<uint32_t> split(N + 1, 0);
+  int sf = 0, sl = 1;
+  uint32_t r0 = 0, r1 = nf;
+  if (sharded) {
+    amgd_shard_split(S->ro, nf, split.data());
+    amgd_my_shards(&sf, &sl);
+    r0 = split[sf];
+    r1 = split[sl];
+  }
   uint32_t *rl = (uint32_t *)amgd_alloc(3 * ((size_t)nf + 1) * 4);
   uint32_t *rl1 = rl + nf + 1, *rls = rl1 + nf + 1;
   unsigned *rc = (unsigned *)amgd_alloc(16);
   amgd_memset(rc, 0, 12);
   const uint32_t small = lmop_small();
-  k_srow_bins<<<grid_for(nf), 256, 0, s>>>(S->ro, nf, 1024, rl, rl1, rc, small, rls);
+  if (r1 > r0)
+    k_srow_bins<<<grid_for(r1 - r0), 256, 0, s>>>(S->ro, r0, r1 - r0, 1024, rl, rl1, rc, small, rls);
   unsigned hrc[3];
   amgd_d2h(hrc, rc, 12);
   // QQt chunks by coarse range within the memory budget
@@ -514,6 +531,23 @@ extern "C" void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, cons
   }
   unsigned hm = 0;
   amgd_d2h(&hm, miss, 4);
+  if (sharded) {
+    // every rank holds its rows' values; a miss on any rank sends all of them to the
+    // exact walk (the counts are summed over the ranks first)
+    std::vector<uint64_t> mv(N, 0);
+    for (int q = sf; q < sl; q++) mv[q] = q == sf ? hm : 0;
+    amgd_allgather_u64(mv.data());
+    uint64_t tot = 0;
+    for (int q = 0; q < N; q++) tot += mv[q];
+    hm = (unsigned)std::min<uint64_t>(tot, 0xffffffffu);
+    if (!hm) {
+      std::vector<uint64_t> pre(N + 1), off(N + 1);
+      amgd_gather_u64_at(S->ro, split.data(), N + 1, pre.data());
+      for (int q = 0; q <= N; q++) off[q] = 8 * pre[q];
+      void *b = S->a;
+      amgd_allgatherv(1, &b, off.data());
+    }
+  }
   if (hm) {
     // a clean contribution missed its column: S is not W_skel*W_skel' -- redo exactly
     g_lmop_stats[3] += hm;
