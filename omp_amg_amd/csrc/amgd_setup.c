@@ -503,9 +503,13 @@ static void solve_weights(dcsr **W, dcsr **Wt_out, const dcsr **W0, double *lam,
 
 
 
+/* the first sweep's products when the caller already formed them from the same R
+   (interpolation's w1 / w2 test, amg_setup.c:870-880: rs = R*1, w = R'rs, tmp = R w,
+   w2 = R' tmp -- the same ordered sums), else NULL */
+typedef struct { const double *rs, *w, *tmp, *w2; } fs_first;
 /* find_support (amg_setup.c:1260).  Rt / perm: R's transpose and its CSC -> CSR map
    when the caller already made them (taken over and freed here), else NULL. */
-static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) {
+static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, const fs_first *f1) {
   uint32_t nf = R->rn, nc = R->cn;
   dcsr *Rl = dcsr_copy(R);
   if (!Rt) Rt = amgd_transpose(R, &perm);
@@ -517,7 +521,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
   int it = 0;
   /* rs = R*1 and sumR = sum(R,1) change only where a sweep removed an entry:
      computed in full once, then re-summed for those rows / columns (amgd_fs_select) */
-  amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);            /* rs = R*1 */
+  if (f1) amgd_d2d(rs, f1->rs, (size_t)nf * 8);
+  else amgd_spmv(Rl, onec, rs, 0., NULL, 1., NULL);       /* rs = R*1 */
   amgd_colsum(Rt, sumR);
   /* Incremental sweeps: a sweep that removed few entries changes rs only on their
      rows D; w = R'rs then changes on the columns C1 of D, tmp = R w on the rows D2
@@ -573,6 +578,12 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal) 
           }
         }
       }
+    }
+    if (!done && it == 1 && f1) {                         /* the caller's products */
+      amgd_d2d(w, f1->w, (size_t)nc * 8);
+      amgd_d2d(tmp, f1->tmp, (size_t)nf * 8);
+      amgd_d2d(w2, f1->w2, (size_t)nc * 8);
+      done = 1;
     }
     if (!done) {
       fused = amgd_spmv_amax(Rt, rs, w, amx, apos);       /* w = R'*rs (row order) */
@@ -652,8 +663,8 @@ static dcsr *r0_rows(const r0_ctx *c, const uint8_t *bad) {
 
 /* expand_support (amg_setup.c:907) */
 static dcsr *expand_support(const dcsr *W_skel, const dcsr *R, dcsr *Rt, uint64_t *perm,
-                            const r0_ctx *r0c, double gamma) {
-  dcsr *M = find_support(R, Rt, perm, gamma);
+                            const r0_ctx *r0c, double gamma, const fs_first *f1) {
+  dcsr *M = find_support(R, Rt, perm, gamma, f1);
   ph(PH_FS);
   if (phases_on() && verbose())
     printf("    find_support: R %u x %u nnz %lu\n", R->rn, R->cn, (unsigned long)R->nnz);
@@ -743,6 +754,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
   dcsr *Amt = amgd_transpose(Ar, NULL);              /* -Ar' */
   amgd_vals_scale(Amt, -1.0);
   double *Dcs = dalloc(cnc), *w1 = dalloc(cnc), *w2 = dalloc(cnc), *onesc = dones(cnc), *r = dalloc(cnc);
+  double *rs1 = dalloc(rnf);
   dcsr *W = NULL;
   uint64_t prev_nnz = (uint64_t)-1;
   int it = 0;
@@ -821,8 +833,8 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
       Rperm = amgd_perm_inverse(p, R->nnz);          /* R' position -> R position */
       amgd_free(p);
     }
-    amgd_spmv(R, onesc, tmp, 0., NULL, 1., NULL);
-    amgd_spmvt(Rt, tmp, w1);                         /* w1 = ((R*1)'*R)' */
+    amgd_spmv(R, onesc, rs1, 0., NULL, 1., NULL);
+    amgd_spmvt(Rt, rs1, w1);                         /* w1 = ((R*1)'*R)' */
     amgd_spmv(R, w1, tmp, 0., NULL, 1., NULL);
     amgd_spmvt(Rt, tmp, w2);                         /* w2 = ((R*w1)'*R)' */
     amgd_vdiv_guard(r, w2, w1, cnc);
@@ -854,7 +866,8 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
     r0_ctx r0c = {Af, AfT, W0, fac.W0t, Ar, Dfsqrti, Dcs};
-    dcsr *nsk = expand_support(W_skel, R, Rt, Rperm, &r0c, gamma2);
+    const fs_first f1 = {rs1, w1, tmp, w2};          /* find_support's first sweep */
+    dcsr *nsk = expand_support(W_skel, R, Rt, Rperm, &r0c, gamma2, &f1);
     dcsr_free(&W_skel);
     W_skel = nsk;
     dcsr_free(&Wtmp);
@@ -866,7 +879,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
   dcsr_free(&W_skel); dcsr_free(&Amt);
   amgd_free(Df); amgd_free(Dfinv); amgd_free(uc); amgd_free(tmp); amgd_free(v); amgd_free(b);
   amgd_free(Dc); amgd_free(Dcinv); amgd_free(lam); amgd_free(alpha); amgd_free(Dcs);
-  amgd_free(w1); amgd_free(w2); amgd_free(onesc); amgd_free(r);
+  amgd_free(w1); amgd_free(w2); amgd_free(onesc); amgd_free(r); amgd_free(rs1);
   return W;
 }
 
