@@ -1340,11 +1340,14 @@ extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double 
 }
 // z = M x and z2 = M 1 (each row's ordered sum of its values, amgd_colsum on M = R') from
 // one pass over M: find_support's w = R' rs and sumR.  Only where the whole-matrix
-// k_spmv_pipe path applies (long rows, one GPU, AMGD_SPMV_SUM2 not 0); returns 0 otherwise.
+// k_spmv_pipe path applies (long rows, one GPU, AMGD_SPMV_SUM2=1); returns 0 otherwise.
+// Off by default: bit-exact (tests), but the second ordered chain costs the SpMV about
+// what the skipped column re-sums save (256^3: SpMV +0.38 s, setup -0.07 s in an
+// interleaved A/B, profiles/r03/ab256_r03s2_sum2_lmopsmall.txt).
 static int g_spmv_sum2 = -1;
 extern "C" void amgd_spmv_set_sum2(int on) { g_spmv_sum2 = on < 0 ? -1 : on; }
 extern "C" int amgd_spmv_sum2_ok(const dcsr *M) {
-  if (g_spmv_sum2 < 0) { const char *e = getenv("AMGD_SPMV_SUM2"); g_spmv_sum2 = e && *e ? atoi(e) : 1; }
+  if (g_spmv_sum2 < 0) { const char *e = getenv("AMGD_SPMV_SUM2"); g_spmv_sum2 = e && *e ? atoi(e) : 0; }
   if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 0; }
   return g_spmv_sum2 && !g_fs_fused && M->rn && amgd_nshards() <= 1 && M->nnz >= 32ull * M->rn &&
          (int64_t)M->rn >= sl_min_whole() && (spmv_pipe() & 1) && !spmv_chunk_ok(M);
