@@ -96,18 +96,10 @@ def lib() -> C.CDLL:
         L.amgd_test_lmop_mode.argtypes = [C.c_int]
         L.amgd_test_spgemm_flat.argtypes = [C.c_int]
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
-        L.amgd_test_spgemm_wt.argtypes = [C.c_int]
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
-        L.amgd_test_fs_fused.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
-        L.amgd_test_qf_colc.argtypes = [C.c_int]
-        L.amgd_test_spmv_chunk.argtypes = [C.c_int]
-        L.amgd_test_spgemm_wsym.argtypes = [C.c_int]
-        L.amgd_test_spgemm_wwin.argtypes = [C.c_int]
-        L.amgd_test_spmv_pipe.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
-        L.amgd_test_spmv_sum2.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
         L.amgd_test_lmop_prune.argtypes = [C.c_int]
         L.amgd_test_qf_sparse.argtypes = [C.c_int]
@@ -367,14 +359,15 @@ def qf_stats() -> dict:
 
 
 ROUTES = ("spmv_lane", "mv_long", "sg_tiny", "sg_kseq", "sg_win", "sg_wsym", "sg_long",
-          "cs_inc", "fs_inc", "sg_row", "fs_fused", "qf_reuse", "lmop_wave")
+          "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
+          "qf_t512", "qf_t1024")
 
 
 def route_stats(reset: bool = True) -> dict:
     """how often each default kernel route ran since the last reset (amgd.h AMGD_R_*):
     lane SpMV, outlier-row SpMV, tiny / k-sequential / windowed / wide-symbolic /
     dense-slab / flat SpGEMM, incremental coarsening and find_support sweeps"""
-    out = (C.c_uint64 * 16)()
+    out = (C.c_uint64 * 32)()
     lib().amgd_test_route_stats(out, int(reset))
     return {k: int(out[i]) for i, k in enumerate(ROUTES)}
 
@@ -395,34 +388,15 @@ def lmop_prune(n: int) -> None:
 
 
 def spgemm_win(w: int) -> None:
-    """wide output rows: 0 = LDS hash kernels, 4096 / 8192 / 16384 = dense-accumulator column
-    windows whatever the column count, -1 = automatic (environment / default)"""
+    """wide output rows: 0 = LDS hash kernels only, 1024..16384 = every wide row through the
+    wave-private windowed kernel (k_sg_wwin) whatever the column count, -1 = automatic"""
     lib().amgd_test_spgemm_win(int(w))
-
-
-def spgemm_wt(t: int) -> None:
-    """windowed SpGEMM rows per work-group: 4 / 8 = tiled kernel (union of the tile's A
-    rows in ascending k), 0 = one row per work-group, -1 = default (environment / 4)"""
-    lib().amgd_test_spgemm_wt(int(t))
 
 
 def qf_reuse(on: int) -> None:
     """Q factors of supports unchanged since the previous interpolation iteration: 1 copy
     (default), 0 refactor every support, -1 default / AMGD_QF_REUSE.  Same bits."""
     lib().amgd_test_qf_reuse(int(on))
-
-
-def spmv_chunk(on: int) -> None:
-    """whole-matrix long-row SpMV: 1 contiguous 16-byte-load chunks (k_spmv_chunk) for
-    matrices whose mean row is < 256 entries, 2 chunks for every long-row matrix, 0 per-row
-    segments (k_spmv_lane) only (default), -1 default / AMGD_SPMV_CHUNK.  Same sums."""
-    lib().amgd_test_spmv_chunk(int(on))
-
-
-def fs_fused(on: int) -> None:
-    """find_support: 1 the sweep's w = R' rs also keeps each column's argmax for the
-    selection, 0 a separate selection pass (default), -1 default.  Same bits."""
-    lib().amgd_test_fs_fused(int(on))
 
 
 def lmop_wave(n: int) -> None:
@@ -432,45 +406,16 @@ def lmop_wave(n: int) -> None:
     lib().amgd_test_lmop_wave(int(n))
 
 
-def qf_colc(on: int) -> None:
-    """Q factor, 256- / 512- / 1024-point tiers: 1 the s2 pass reads a column-packed copy
-    of U (coalesced), 0 the row-packed U, -1 default / AMGD_QF_COLC.  Same bits."""
-    lib().amgd_test_qf_colc(int(on))
-
-
 def sg_pattern(on: int) -> None:
     """constraint pattern W_skel*W_skel': 1 pattern-only product (default), 0 the full
     product (values discarded by interp_lmop), -1 default.  Same bits."""
     lib().amgd_test_sg_pattern(int(on))
 
 
-def spmv_sum2(on: int) -> None:
-    """find_support: sumR re-summed in the full sweeps' w = R' rs pass (1) or by the listed
-    column sums after each selection (0); -1: back to the env (AMGD_SPMV_SUM2)"""
-    lib().amgd_test_spmv_sum2(int(on))
-
-
 def lmop_small(n: int) -> None:
     """interp_lmop row pull: S rows of <= 32 entries one thread each (n > 0) or on the
     wavefront kernel (0); -1: back to the env (AMGD_LMOP_SMALL)"""
     lib().amgd_test_lmop_small(int(n))
-
-
-def spmv_pipe(m: int) -> None:
-    """lane SpMV with the gather one round ahead (AMGD_SPMV_PIPE bits: 1 whole-matrix,
-    2 listed rows; -1: back to the env)"""
-    lib().amgd_test_spmv_pipe(int(m))
-
-
-def spgemm_wwin(m: int) -> None:
-    """wave-private windowed SpGEMM routing (AMGD_SG_WWIN bits; -1: back to the env)"""
-    lib().amgd_test_spgemm_wwin(int(m))
-
-
-def spgemm_wsym(w: int) -> None:
-    """symbolic pass of rows with many products: 0 = LDS hash, 32768 / 65536 = byte-map
-    column windows, -1 = automatic (environment / default)"""
-    lib().amgd_test_spgemm_wsym(int(w))
 
 
 def spgemm_flat(on: bool) -> None:

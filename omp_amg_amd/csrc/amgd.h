@@ -32,18 +32,26 @@ typedef struct {
 /* ---------------- runtime (amgd_rt.hip) ---------------- */
 int amgd_rt_init(int device);            /* idempotent; 0 on success */
 const char *amgd_last_error(void);
+void amgd_set_error(const char *msg);
 void *amgd_alloc(size_t bytes);          /* arena; out of HBM: unwinds to amgd_try, else aborts */
 void amgd_set_hbm_cap(size_t bytes);     /* cap on live bytes (tests; 0: none) */
 /* run fn(arg); if an allocation runs out of HBM inside it, every block allocated since
    the call is released and -2 returned (amgd_last_error() has the text) */
 int amgd_try(int (*fn)(void *), void *arg);
 void amgd_spmv_split_clear(void);        /* drop every cached SpMV shard split */
+/* reset the per-call module state a setup sets and clears around its kernels (SpGEMM
+   pattern mode / timer slot, Q-factor reuse pointers, component-split depth): called at the
+   start of every setup and after an unwound one */
+void amgd_reset_call_state(void);
+void amgd_sparse_reset_state(void);
+void amgd_interp_reset_state(void);
 void amgd_free(void *p);
 void amgd_spmv_split_forget(const void *ro);   /* drop cached SpMV shard splits of a freed buffer */
 void amgd_rt_shutdown(void);             /* free everything; pointers become invalid */
 void amgd_pool_release(void);            /* return every cached block to the driver */
 size_t amgd_pool_bytes_in_use(void);
 size_t amgd_pool_peak_bytes(void);
+void amgd_pool_peak_reset(void);          /* peak := bytes in use now (start of a setup) */
 void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease);
 void amgd_h2d(void *d, const void *h, size_t n);
 void amgd_d2h(void *h, const void *d, size_t n);
@@ -68,8 +76,9 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
    at sizes where the default routing engages) */
 enum { AMGD_R_SPMV_LANE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WIN,
        AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
-       AMGD_R_FS_FUSED, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_N };
-extern uint64_t amgd_route_ctr[16];
+       AMGD_R_MV_RW4, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_MV_RW16, AMGD_R_MV_RW64,
+       AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_N };
+extern uint64_t amgd_route_ctr[32];
 #define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
 
 /* scans: counts[0..n-1] -> exclusive prefix in counts[0..n], returns total */
@@ -120,9 +129,6 @@ void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const do
                double beta, const uint8_t *f);
 /* z[list[r]] = row list[r] of M times x (x == NULL: row sums), left to right */
 void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, const double *x, double *z);
-/* z = M x plus per row the largest product and its first entry position (amx, apos);
-   returns 0 (nothing done) where only the separate product + selection applies */
-int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos);
 /* z = M^T x, per column in ascending row order; Mt = transpose(M) */
 void amgd_spmvt(const dcsr *Mt, const double *x, double *z);
 void amgd_colsum(const dcsr *Mt, double *z);   /* sum(M,1) via Mt */
@@ -230,14 +236,7 @@ void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] s
    an entry */
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                         const double *w, double *sumR, double thr,
-                        uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved,
-                        const uint64_t *apos,    /* apos: per-column argmax of the sweep's w
-                                                    product (amgd_spmv_amax), or NULL */
-                        uint32_t skip_above);    /* more selections than this: sumR is left
-                                                    to the next (full) sweep's amgd_spmv_sum2 */
-/* z = M x and z2 = M 1 from one pass (find_support's w = R' rs and sumR); 0: not taken */
-int amgd_spmv_sum2_ok(const dcsr *M);
-int amgd_spmv_sum2(const dcsr *M, const double *x, double *z, double *z2);
+                        uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
 /* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
    returns the count, > cap when the list overflowed */
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,

@@ -289,19 +289,12 @@ __global__ __launch_bounds__(256) void k_qfactor_mid(const uint32_t *rows, uint3
 // s2_{k'}[k] of the later steps of the block on lanes of wave 0.  U is read twice per
 // B steps instead of twice per step; every sum keeps the reference's order.
 #define QB2 16
-// COLC: a column-packed copy of U in per-block scratch (Ucs + blockIdx.x * ucap; column j
-// holds U[j..nz-1][j] at ctri(j) = sum_{j'<j} (nz - j')), so the s2 pass -- lane i walking
-// row i of U -- reads one coalesced run per step instead of 64 rows' worth of lines
-__device__ __forceinline__ uint64_t ctri(uint32_t j, uint32_t nz) {
-  return (uint64_t)j * nz - (uint64_t)j * (j - 1) / 2;
-}
-template <int NZMAX, int B, int NTT = 256, bool COLC = false>
+template <int NZMAX, int B, int NTT = 256>
 __global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint32_t nrows,
                                                      const uint64_t *wro, const uint32_t *wcol,
                                                      const uint64_t *aro, const uint32_t *acol,
                                                      const double *aa, const uint64_t *qoff,
-                                                     double *Q, double *Ucs = nullptr,
-                                                     uint64_t ucap = 0) {
+                                                     double *Q) {
   constexpr uint32_t NT = NTT, RPT = (NZMAX + NT - 1) / NT, PAD = NZMAX + 16;
   __shared__ uint32_t Qs[NZMAX];
   __shared__ double S1[B * PAD], S2[B * PAD], qk[PAD];
@@ -313,7 +306,6 @@ __global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint3
     const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
     for (uint32_t m = t; m < nz; m += NT) Qs[m] = wcol[w0 + m];
     double *U = Q + qoff[c];
-    double *Uc = COLC ? Ucs + (uint64_t)blockIdx.x * ucap : nullptr;
     __syncthreads();
     for (uint32_t k0 = 0; k0 < nz; k0 += B) {
       const uint32_t bn = min((uint32_t)B, nz - k0);
@@ -370,39 +362,7 @@ __global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint3
       }
       __syncthreads();
       // s2_k[i], i < k0, for every step of the block: one pass over rows i
-      if (COLC) {
-#pragma unroll
-        for (uint32_t rr = 0; rr < RPT; rr++) {
-          const uint32_t ib = (t - lane) + rr * NT, i = ib + lane;
-          if (ib >= k0) break;                          // uniform per wavefront
-          double acc[B];
-#pragma unroll
-          for (int b = 0; b < B; b++) acc[b] = 0.0;
-          const uint32_t jend = min(ib + 63, k0 - 1);   // last column any lane needs
-          uint64_t cj = 0;                              // ctri(j0)
-          for (uint32_t j0 = 0; j0 <= jend; j0 += QB2) {
-            double u[QB2];
-#pragma unroll
-            for (int q = 0; q < QB2; q++) {
-              const uint32_t j = j0 + q;
-              u[q] = (j <= i && i < k0) ? Uc[cj + (i - j)] : 0.0;
-              cj += nz - j;
-            }
-#pragma unroll
-            for (int q = 0; q < QB2; q++)
-              if (j0 + q <= i && i < k0) {
-#pragma unroll
-                for (int b = 0; b < B; b++) acc[b] += u[q] * S1[b * PAD + j0 + q];
-              }
-          }
-          if (i < k0) {
-#pragma unroll
-            for (int b = 0; b < B; b++)
-              if ((uint32_t)b < bn) S2[b * PAD + i] = acc[b];
-          }
-        }
-      }
-      for (uint32_t i = t; !COLC && i < k0; i += NT) {
+      for (uint32_t i = t; i < k0; i += NT) {
         double acc[B];
 #pragma unroll
         for (int b = 0; b < B; b++) acc[b] = 0.0;
@@ -479,14 +439,8 @@ __global__ __launch_bounds__(NTT) void k_qfactor_blk(const uint32_t *rows, uint3
           __syncthreads();
           const double al = sh_al;
           double *out = U + tri(k);
-          for (uint32_t i = t; i < k; i += NT) {
-            out[i] = qk[i] * al;
-            if (COLC) Uc[ctri(i, nz) + (k - i)] = qk[i] * al;
-          }
-          if (t == 0) {
-            out[k] = -al;
-            if (COLC) Uc[ctri(k, nz)] = -al;
-          }
+          for (uint32_t i = t; i < k; i += NT) out[i] = qk[i] * al;
+          if (t == 0) out[k] = -al;
           // s2_{k'}[k] for the later steps k' of the block, one chain per lane of wave 0
           if (t < bn - 1 - b) {
             const double *s1 = S1 + (b + 1 + t) * PAD;
@@ -860,14 +814,6 @@ static int qf_blocked() {
   }
   return b;
 }
-static int g_qf_colc = -1;     // column-packed U copy for the 256 / 512 / 1024 tiers
-extern "C" void amgd_qfactor_set_colc(int on) { g_qf_colc = on; }
-static int qf_colc() {
-  if (g_qf_colc >= 0) return g_qf_colc;
-  static int v = -1;
-  if (v < 0) { const char *e = getenv("AMGD_QF_COLC"); v = e && *e ? atoi(e) : 0; }
-  return v;
-}
 static uint32_t g_coop_lds_max = QF_COOP_MAX;   // tests: smaller forces the global-memory variant
 extern "C" void amgd_qfactor_set_coop_lds(int m) { g_coop_lds_max = m < 0 ? QF_COOP_MAX : (uint32_t)m; }
 static unsigned long g_qf_stats[3];   // huge supports factored sparse / sent to the dense kernel / split
@@ -1061,6 +1007,14 @@ static bool qfactor_split(uint32_t c, const dcsr *Wt, const dcsr *A, uint64_t w0
 static uint8_t *g_qskip = nullptr;          // per coarse point: 1 = copy (current call)
 static const double *g_qp_q = nullptr;      // the previous call's factors
 static const uint64_t *g_qp_off = nullptr;
+// after an unwound setup g_qskip points into a block the rollback already released:
+// forget it (never free it again)
+extern "C" void amgd_interp_reset_state(void) {
+  g_qskip = nullptr;
+  g_qp_q = nullptr;
+  g_qp_off = nullptr;
+  g_qf_split_depth = 0;
+}
 static uint64_t g_qf_reused = 0, g_qf_factored = 0;
 // 1 where row c of Wt equals row c of Wp (same length, same columns): one wavefront per row
 __global__ void k_supp_same(const uint64_t *ro, const uint32_t *col, const uint64_t *pro,
@@ -1264,38 +1218,18 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
     // (512 tier, 47782-column call at 256^3: B 8 -> 4: 419 -> 318 ms)
     static int v256 = -1;   // AMGD_QF_B256: steps per pass of the 256-point tier (4 or 8)
     if (v256 < 0) v256 = getenv("AMGD_QF_B256") ? atoi(getenv("AMGD_QF_B256")) : 4;
-    const int colc = qf_colc();
-    // column copies: one triangle of scratch per resident work-group (grid capped)
-    auto ucs = [&](unsigned n, unsigned gmax, uint64_t cap) {
-      const unsigned g = std::min(n, gmax);
-      return std::make_pair(g, (double *)amgd_alloc((size_t)g * cap * 8 + 8));
-    };
-    constexpr uint64_t C256 = 256ull * 257 / 2, C512 = 512ull * 513 / 2, C1K = 1024ull * 1025 / 2;
-    if (hn[3] && colc) {
-      auto g = ucs(hn[3], 4096u, C256);
-      k_qfactor_blk<256, 4, 256, true><<<(int)g.first, 256, 0, s>>>(
-          lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q, g.second, C256);
-      amgd_free(g.second);
-    } else if (hn[3] && v256 == 8)
+    if (hn[3] && v256 == 8)
       k_qfactor_blk<256, 8><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
           lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
     else if (hn[3])
       k_qfactor_blk<256, 4><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
           lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-    if (hn[4] && colc) {
-      auto g = ucs(hn[4], 2048u, C512);
-      k_qfactor_blk<512, 4, 256, true><<<(int)g.first, 256, 0, s>>>(
-          lists + 4 * L, hn[4], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q, g.second, C512);
-      amgd_free(g.second);
-    } else if (hn[4])
+    if (hn[4]) amgd_route_hit(AMGD_R_QF_T512);
+    if (hn[5]) amgd_route_hit(AMGD_R_QF_T1024);
+    if (hn[4])
       k_qfactor_blk<512, 4><<<(int)std::min<unsigned>(hn[4], 8192u), 256, 0, s>>>(
           lists + 4 * L, hn[4], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-    if (hn[5] && colc) {
-      auto g = ucs(hn[5], 1024u, C1K);
-      k_qfactor_blk<QF_T3, 4, 256, true><<<(int)g.first, 256, 0, s>>>(
-          lists + 5 * L, hn[5], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q, g.second, C1K);
-      amgd_free(g.second);
-    } else if (hn[5])
+    if (hn[5])
       k_qfactor_blk<QF_T3, 4><<<(int)std::min<unsigned>(hn[5], 8192u), 256, 0, s>>>(
           lists + 5 * L, hn[5], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   } else {
@@ -2289,20 +2223,6 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     }
   }
 }
-// the same selection from the argmax the fused product w = R' rs kept per column
-// (amgd_spmv_amax: the same products, first position of the maximum)
-__global__ void k_fs_select_cached(const uint32_t *trow, const uint64_t *perm, double *ta, double *a,
-                                   const uint64_t *apos, const uint32_t *list, const unsigned *nlist,
-                                   uint32_t *si, uint32_t *sj, unsigned *removed) {
-  const uint32_t n = *nlist;
-  GRID_STRIDE(r, n) {
-    const uint32_t c = list[r];
-    const uint64_t best = apos[c];
-    si[r] = best != ~0ull ? trow[best] : 0u;
-    sj[r] = c;
-    if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
-  }
-}
 // bad columns past fs_long() entries: one 1024-thread block each (k_fs_select skips them);
 // llist holds their slots in the bad list
 __global__ __launch_bounds__(1024) void k_fs_select_long(const uint64_t *tro, const uint32_t *trow,
@@ -2473,18 +2393,14 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
                                    double *rs, const double *w, double *sumR,
                                    double thr, uint32_t *sel_i, uint32_t *sel_j,
-                                   uint32_t *nremoved, const uint64_t *apos, uint32_t skip_above) {
+                                   uint32_t *nremoved) {
   hipStream_t s = amgd_s();
   const uint32_t nc = Rt->rn;
   uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
   unsigned *cnt = (unsigned *)amgd_alloc(16);
   amgd_memset(cnt, 0, 16);
   uint32_t *llist = nullptr;
-  if (nc && apos) {
-    k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
-    k_fs_select_cached<<<grid_for(nc), 256, 0, s>>>(Rt->col, perm, Rt->a, Rl->a, apos, list, cnt + 2,
-                                                    sel_i, sel_j, cnt + 1);
-  } else if (nc) {
+  if (nc) {
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
     llist = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
     const uint32_t ml = fs_long(Rt);
@@ -2516,7 +2432,7 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
     const dcsr *M[2] = {Rl, Rt};
     const uint32_t *L[2] = {sel_i, sel_j};
     double *O[2] = {rs, sumR};
-    for (int q = 0; q < (h[0] > skip_above ? 1 : 2); q++) {
+    for (int q = 0; q < 2; q++) {
       if (M[q]->nnz <= 32ull * M[q]->rn)
         k_list_rowsum_t<<<grid_for(h[0]), 256, 0, s>>>(M[q]->ro, M[q]->a, L[q], h[0], O[q]);
       else

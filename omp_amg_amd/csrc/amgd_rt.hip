@@ -35,6 +35,7 @@ void amgd_check(hipError_t e, const char *what, const char *file, int line) {
 }
 
 extern "C" const char *amgd_last_error(void) { return g_err; }
+extern "C" void amgd_set_error(const char *msg) { snprintf(g_err, sizeof g_err, "%s", msg); }
 
 // The reference's Lanczos start vector comes from the process-wide libc rand()
 // stream (amg_setup.c:2447).  The HIP runtime may draw from that stream while it
@@ -98,7 +99,7 @@ struct amgd_oom_error {};
 // statistics (AMGD_PHASES report): driver allocations (arena + fallbacks), their time
 static uint64_t g_nmalloc = 0, g_nrelease = 0;
 static double g_tmalloc = 0, g_bmalloc = 0;
-extern "C" { uint64_t amgd_route_ctr[16]; }
+extern "C" { uint64_t amgd_route_ctr[32]; }
 extern "C" void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease) {
   *nmalloc = g_nmalloc; *gbytes = g_bmalloc / 1e9; *ms = g_tmalloc * 1e3; *nrelease = g_nrelease;
 }
@@ -156,7 +157,9 @@ static void oom(size_t sz) {
            sz / 1e9, g_inuse / 1e9, g_peak / 1e9, g_arena_sz / 1e9,
            g_cap != (size_t)-1 ? ", capped" : "");
   fprintf(stderr, "omp_amg_amd: %s\n", g_err);
-  if (g_try_depth > 0) throw amgd_oom_error();
+  // One rank unwinding alone would leave its peers blocked in the next collective:
+  // with a multi-process communicator out of HBM stays fatal.
+  if (g_try_depth > 0 && amgd_comm_procs() <= 1) throw amgd_oom_error();
   abort();
 }
 extern "C" int amgd_try(int (*fn)(void *), void *arg) {
@@ -173,6 +176,7 @@ extern "C" int amgd_try(int (*fn)(void *), void *arg) {
       if (u.second.serial >= mark) live.push_back(u.first);
     g_try_depth--;
     for (void *p : live) amgd_free(p);
+    amgd_reset_call_state();           // per-call flags the unwound frames had set
     return rc;
   }
   g_try_depth--;
@@ -244,6 +248,7 @@ extern "C" void amgd_pool_release(void) {
 }
 extern "C" size_t amgd_pool_bytes_in_use(void) { return g_inuse; }
 extern "C" size_t amgd_pool_peak_bytes(void) { return g_peak; }
+extern "C" void amgd_pool_peak_reset(void) { g_peak = g_inuse; }
 
 extern "C" void amgd_h2d(void *d, const void *h, size_t n) {
   if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, amgd_s()));

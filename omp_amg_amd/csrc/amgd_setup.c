@@ -546,19 +546,10 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
   uint64_t prev_off = 0;
   uint32_t prev_nsel = 0;
   const int fslog = getenv("AMGD_FSLOG") != NULL;
-  /* full sweeps on long-row R': w = R'*rs keeps each column's argmax of R(i,c)*rs_i,
-     the very products the selection compares, so the selection needs no second pass */
-  double *amx = dalloc(nc);
-  uint64_t *apos = (uint64_t *)amgd_alloc((size_t)nc * 8 + 8);
-  /* full sweeps on long-row R' re-sum sumR in the w = R'*rs pass itself (the same ordered
-     row sums of R' as amgd_colsum): a sweep whose successor is certainly full (too many
-     selections for the incremental path) leaves sumR to it instead of re-summing the
-     selected columns */
-  const int sum2 = amgd_spmv_sum2_ok(Rt);
   ph(PH_FS);
   for (;;) {
     it++;
-    int done = 0, fused = 0;
+    int done = 0;
     uint32_t n1 = 0, n2 = 0, n3 = 0;
     double t0 = 0, t1 = 0;
     if (fslog) { amgd_sync(); t0 = amgd_wtime(); }
@@ -586,8 +577,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
       done = 1;
     }
     if (!done) {
-      fused = amgd_spmv_amax(Rt, rs, w, amx, apos);       /* w = R'*rs (row order) */
-      if (!fused && !(sum2 && amgd_spmv_sum2(Rt, rs, w, sumR))) amgd_spmvt(Rt, rs, w);
+      amgd_spmvt(Rt, rs, w);                              /* w = R'*rs (row order) */
       amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       amgd_spmvt(Rt, tmp, w2);                            /* w2 = R'*(R*w) */
     }
@@ -600,11 +590,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
     if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
     if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
-    /* the next sweep is full when this one selects more than the incremental path takes
-       (cap_c), or when sweeps are never incremental: then its w = R'*rs pass re-sums sumR */
-    const uint32_t skip_above = sum2 ? (fs_inc ? cap_c : 0u) : 0xffffffffu;
-    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem,
-                                   fused ? apos : NULL, skip_above);
+    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
@@ -627,7 +613,6 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
     amgd_free(st_r); amgd_free(st_c); amgd_free(L1); amgd_free(L2); amgd_free(L3);
   }
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
-  amgd_free(amx); amgd_free(apos);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);
   return Sk;
@@ -965,6 +950,8 @@ static int setup_body(void *arg) {
   const double *dAv = sa->dAv;
   memset(&g_st, 0, sizeof g_st);
   g_ub = 0;
+  amgd_reset_call_state();
+  amgd_pool_peak_reset();               /* amgd_stats.peak_bytes: this setup's peak */
   amgd_timer_reset();
   amgd_spmv_bytes_reset();
   amgd_sync();
@@ -1333,32 +1320,40 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
             amgd_comm_procs(), amgd_comm_rank());
     return NULL;
   }
-  /* local dof k is global id[k]; entries touching id 0 are dropped (amg.c:1065) */
+  /* local dof k is global id[k]; entries touching id 0 are dropped (amg.c:1065).  Local
+     indices must be < n and ids < 2^32 (the device CSR keeps u32 columns): a violation on
+     any rank makes every rank return NULL (the flag travels with the entry counts, so no
+     rank is left waiting in a collective) */
   amg_uint *I = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8), *J = (amg_uint *)malloc(nz * sizeof(amg_uint) + 8);
   double *V = (double *)malloc(nz * sizeof(double) + 8);
   amg_uint m = 0;
-  for (amg_uint k = 0; k < nz; k++) {
+  const char *why = NULL;
+  for (amg_uint k = 0; k < nz && !why; k++) {
     amg_uint i = Ai[k], j = Aj[k];
-    if (i >= n || j >= n || id[i] == 0 || id[j] == 0 || A[k] == 0) continue;
+    if (i >= n || j >= n) { why = "local index >= n"; break; }
+    if (id[i] == 0 || id[j] == 0 || A[k] == 0) continue;
+    if (id[i] - 1 > 0xfffffffeul || id[j] - 1 > 0xfffffffeul) { why = "global id exceeds the 32-bit range"; break; }
     I[m] = id[i] - 1; J[m] = id[j] - 1; V[m] = A[k]; m++;
   }
-  struct crs_data *d = (struct crs_data *)calloc(1, sizeof *d);
-  /* entries of every rank: counts, then one allgatherv of (i, j, v) */
   uint64_t *cnt = (uint64_t *)calloc((size_t)np + 1, 8), *pre = (uint64_t *)calloc((size_t)np + 1, 8);
-  cnt[me] = m;
+  cnt[me] = why ? ~0ull : m;
   if (np > 1) amgd_allgather_u64(cnt);
+  int bad_rank = -1;
+  for (int r = 0; r < np; r++) if (cnt[r] == ~0ull && bad_rank < 0) bad_rank = r;
+  if (bad_rank >= 0) {
+    amgd_set_error(why ? why : "invalid input on another rank");
+    fprintf(stderr, "omp_amg_amd: crs_setup: rank %d: %s\n", bad_rank, why ? why : "(see that rank)");
+    free(cnt); free(pre); free(I); free(J); free(V);
+    return NULL;
+  }
+  struct crs_data *d = (struct crs_data *)calloc(1, sizeof *d);
+  /* entries of every rank: counts (above), then one allgatherv of (i, j, v) */
   for (int r = 0; r < np; r++) pre[r + 1] = pre[r] + cnt[r];
   const uint64_t M = pre[np];
   uint32_t *di = (uint32_t *)amgd_alloc(M * 4 + 4), *dj = (uint32_t *)amgd_alloc(M * 4 + 4);
   double *dv = dalloc(M);
   uint32_t *hi = (uint32_t *)malloc(m * 4 + 4), *hj = (uint32_t *)malloc(m * 4 + 4);
-  for (amg_uint k = 0; k < m; k++) {
-    if (I[k] > 0xfffffffeul || J[k] > 0xfffffffeul) {
-      fprintf(stderr, "omp_amg_amd: crs_setup: global id %lu exceeds 32-bit range\n", (unsigned long)(I[k] + 1));
-      abort();
-    }
-    hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k];
-  }
+  for (amg_uint k = 0; k < m; k++) { hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k]; }
   amgd_h2d(di + pre[me], hi, m * 4); amgd_h2d(dj + pre[me], hj, m * 4); amgd_h2d(dv + pre[me], V, m * 8);
   free(hi); free(hj); free(I); free(J); free(V);
   if (np > 1) {

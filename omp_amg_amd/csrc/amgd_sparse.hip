@@ -634,149 +634,24 @@ static int64_t sl_min_whole() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("
 static int64_t sl_min_list() { return g_sl_forced >= 0 ? g_sl_forced : sl_env("AMGD_SL_LIST_MIN_ROWS", 4096); }
 extern "C" void amgd_spmv_set_sl_min(int64_t n) { g_sl_forced = n < 0 ? -1 : n; }
 // RW rows per wavefront (64: one row per lane; 16 / 4 for matrices with fewer, longer
-// rows -- more wavefronts in flight, the first RW lanes add): a round loads SEG =
-// 1024 / RW entries of each row, 16 per lane, lane L's q-th load taking flat entry
-// q*64 + L of the round (row = that / SEG): every load instruction covers whole row
-// segments of >= 128 B.
-template <bool NTL, typename T>
-__device__ __forceinline__ T ld_stream(const T *p) {
-  if constexpr (NTL) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-// AMX: the adding lanes also keep each row's largest product and its first position
-// (find_support's selection, amg_setup.c:1343-1364, reads exactly these products)
-template <bool LIST, int RW, bool NTL = false, bool AMX = false>
-__global__ __launch_bounds__(256) void k_spmv_lane(const uint64_t *ro, const uint32_t *col,
-                                                   const double *a, uint32_t n,
-                                                   const uint32_t *list, const double *x,
-                                                   double *z, double alpha, const double *y,
-                                                   double beta, const uint8_t *f,
-                                                   uint32_t maxlen = 0xffffffffu,
-                                                   double *amx = nullptr, uint64_t *apos = nullptr) {
-  constexpr int SEG = 1024 / RW;
-  __shared__ double buf[4][RW][SEG + 1];
-  __shared__ uint64_t rk0[4][RW];
-  __shared__ uint32_t rlen[4][RW];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n;
-       rb += (uint64_t)gridDim.x * 4 * RW) {
-    const uint64_t r = rb + lane;
-    const bool own = lane < RW && r < n;
-    const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
-    uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
-    if (LIST && k1 - k0 > maxlen) k1 = k0;      // a long row: left to k_rows_exact
-    const uint32_t len = (uint32_t)(k1 - k0);
-    if (lane < RW) {
-      rk0[w][lane] = k0;
-      rlen[w][lane] = len;
-    }
-    uint32_t mx = len;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double t = 0;
-    double pmx = -DBL_MAX;           // AMX: largest product, its entry (first on ties)
-    uint64_t ppos = ~0ull;
-    // round `off`'s products sit in v[]; the next round's (a, col) loads are
-    // issued before the lanes add the current round, so HBM latency overlaps
-    // the ordered adds (the sums and their order are unchanged)
-    double v[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
-      v[q] = 0.0;
-      if ((uint32_t)sub < rlen[w][rr]) {
-        const uint64_t k = rk0[w][rr] + sub;
-        v[q] = x ? ld_stream<NTL>(a + k) * x[ld_stream<NTL>(col + k)] : ld_stream<NTL>(a + k);
-      }
-    }
-    for (uint32_t off = 0; off < mx; off += SEG) {
-#pragma unroll
-      for (int q = 0; q < 16; q++) {
-        const int fl = q * 64 + lane;
-        buf[w][fl / SEG][fl % SEG] = v[q];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double an[16];
-      uint32_t cn[16];
-      bool hv[16];
-#pragma unroll
-      for (int q = 0; q < 16; q++) {
-        const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
-        const uint32_t en = off + SEG + sub;
-        hv[q] = en < rlen[w][rr];
-        an[q] = 0.0;
-        cn[q] = 0;
-        if (hv[q]) {
-          const uint64_t k = rk0[w][rr] + en;
-          an[q] = ld_stream<NTL>(a + k);
-          if (x) cn[q] = ld_stream<NTL>(col + k);
-        }
-      }
-      if (lane < RW && off < len) {
-        const uint32_t m = min((uint32_t)SEG, len - off);
-        if (m == SEG) {
-          // full segment: LDS reads issued 16 ahead of the ordered adds
-#pragma unroll
-          for (int e0 = 0; e0 < SEG; e0 += 16) {
-            double u[16];
-#pragma unroll
-            for (int e = 0; e < 16; e++) u[e] = buf[w][lane][e0 + e];
-#pragma unroll
-            for (int e = 0; e < 16; e++) t += u[e];
-            if (AMX) {
-#pragma unroll
-              for (int e = 0; e < 16; e++)
-                if (u[e] > pmx) { pmx = u[e]; ppos = rk0[w][lane] + off + e0 + e; }
-            }
-          }
-        } else {
-          for (uint32_t e = 0; e < m; e++) {
-            const double u = buf[w][lane][e];
-            t += u;
-            if (AMX && u > pmx) { pmx = u; ppos = rk0[w][lane] + off + e; }
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int q = 0; q < 16; q++) v[q] = hv[q] ? (x ? an[q] * x[cn[q]] : an[q]) : 0.0;
-    }
-    if (own && (!LIST || ro[i + 1] - ro[i] <= maxlen)) {
-      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
-      if (f) v = v * (f[i] ? 1.0 : 0.0);
-      z[i] = v;
-      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
-    }
-  }
-}
-// k_spmv_lane with the x gather one round ahead (round 3): k_spmv_lane issues the
-// next round's (value, column) loads before its ordered adds but the gather x[col]
-// only after them, so every round waits for one full gather latency.  Here a round
-// is 512 entries (8 per lane, SEG = 512 / RW per row) and two rounds are in flight
-// during the adds of the current one: the gather of round r+1 (its columns arrived
-// during round r-1) and the (value, column) loads of round r+2.  Rows, segments and
-// the left-to-right adds from +0 are k_spmv_lane's: the same sums.
-// SUM2: the same pass also writes each row's plain ordered sum of its values to z2
-// (find_support: w = R' rs and sumR = sum(R, 1) -- the column sums of R -- from one read)
-template <bool LIST, int RW, int PER = 8, bool AMX = false, bool SUM2 = false>
+// rows -- more wavefronts in flight, the first RW lanes add).
+// Long-row SpMV, the x gather one round ahead (round 3).  A wavefront owns RW rows; a
+// round is PER x 64 entries (SEG = 64 PER / RW per row), each load instruction
+// covering whole >= 128 B row segments, transposed through LDS so that lane r of the
+// first RW adds row r's segment left to right.  During the adds of round r the gather
+// x[col] of round r+1 (its columns arrived during round r-1) and the (value, column)
+// loads of round r+2 are in flight.  Every row is summed left to right from +0: the
+// reference's row sum.  LIST: the rows are list[0..n) instead of 0..n (rows longer
+// than maxlen are left to k_rows_exact).
+template <bool LIST, int RW, int PER = 16>
 __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
                                                    double *z, double alpha, const double *y,
                                                    double beta, const uint8_t *f,
-                                                   uint32_t maxlen = 0xffffffffu,
-                                                   double *amx = nullptr, uint64_t *apos = nullptr,
-                                                   double *z2 = nullptr) {
+                                                   uint32_t maxlen = 0xffffffffu) {
   constexpr int SEG = 64 * PER / RW;
   __shared__ double buf[4][RW][SEG + 1];
-  __shared__ double buf2[SUM2 ? 4 : 1][SUM2 ? RW : 1][SUM2 ? SEG + 1 : 1];
   __shared__ uint64_t rk0[4][RW];
   __shared__ uint32_t rlen[4][RW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -819,15 +694,12 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
 #pragma unroll
     for (int q = 0; q < PER; q++) g0[q] = x ? x[c0[q]] : 0.0;
     ld(SEG, a1, c1);
-    double t = 0, t2 = 0;
-    double pmx = -DBL_MAX;           // AMX: largest product, its entry (first on ties)
-    uint64_t ppos = ~0ull;
+    double t = 0;
     for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
       for (int q = 0; q < PER; q++) {
         const int fl = q * 64 + lane;
         buf[w][fl / SEG][fl % SEG] = x ? a0[q] * g0[q] : a0[q];
-        if (SUM2) buf2[w][fl / SEG][fl % SEG] = a0[q];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -850,29 +722,11 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
             double u[U];
 #pragma unroll
             for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
-            if (SUM2) {
-              double u2[U];
 #pragma unroll
-              for (int e = 0; e < U; e++) u2[e] = buf2[w][lane][e0 + e];
-#pragma unroll
-              for (int e = 0; e < U; e++) { t += u[e]; t2 += u2[e]; }
-            } else {
-#pragma unroll
-              for (int e = 0; e < U; e++) t += u[e];
-            }
-            if (AMX) {
-#pragma unroll
-              for (int e = 0; e < U; e++)
-                if (u[e] > pmx) { pmx = u[e]; ppos = rk0[w][lane] + off + e0 + e; }
-            }
+            for (int e = 0; e < U; e++) t += u[e];
           }
         } else {
-          for (uint32_t e = 0; e < m; e++) {
-            const double u = buf[w][lane][e];
-            t += u;
-            if (SUM2) t2 += buf2[w][lane][e];
-            if (AMX && u > pmx) { pmx = u; ppos = rk0[w][lane] + off + e; }
-          }
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -885,125 +739,9 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
-      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
-      if (SUM2) z2[i] = 1.0 * t2;              // amgd_colsum's beta * t
     }
   }
 }
-// Whole-matrix long-row SpMV over contiguous entry chunks.  A wavefront owns RW
-// consecutive rows, i.e. the contiguous entry range [ro[rb], ro[rb + RW]); each round
-// streams CH = 1024 entries of it with 16-byte loads (four columns, or two values,
-// per lane per instruction: the full-rate load width of MI355X_MICROARCH.md, where
-// k_spmv_lane's 4- / 8-byte row-segment loads run at ~0.5-0.7 of it), forms the
-// products a * x[col] into LDS in entry order, and lane r of the first RW adds row r's
-// part of the chunk, left to right -- the same row sums, from +0, as every other
-// SpMV kernel here.  The next chunk's (column, value) loads are in flight during the
-// adds.  AMX: the adding lanes also keep each row's largest product and its first
-// position (find_support's fused selection, amgd_spmv_amax).
-template <int RW, bool AMX = false>
-__global__ __launch_bounds__(256) void k_spmv_chunk(const uint64_t *ro, const uint32_t *col,
-                                                    const double *a, uint32_t n, const double *x,
-                                                    double *z, double alpha, const double *y,
-                                                    double beta, const uint8_t *f, double *amx,
-                                                    uint64_t *apos) {
-  constexpr int CH = 1024;
-  __shared__ double buf[4][CH];
-  __shared__ uint64_t rof[4][RW + 1];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n; rb += (uint64_t)gridDim.x * 4 * RW) {
-    const uint32_t nr = (uint32_t)min((uint64_t)RW, (uint64_t)n - rb);
-    if ((uint32_t)lane < nr) rof[w][lane] = ro[rb + lane];
-    if (lane == 0) rof[w][nr] = ro[rb + nr];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t E0 = rof[w][0], E1 = rof[w][nr];
-    const bool own = (uint32_t)lane < nr;
-    const uint64_t r0 = own ? rof[w][lane] : 0, r1 = own ? rof[w][lane + 1] : 0;
-    double t = 0;
-    double pmx = -DBL_MAX;
-    uint64_t ppos = ~0ull;
-    // one chunk's loads: lane L holds entries B + 4 (L + 64 q) + j, q < 4, j < 4
-    auto load = [&](uint64_t B, uint32_t (&cq)[16], double (&aq)[16]) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint64_t e = B + 4 * (uint64_t)(lane + 64 * q);
-        if (e + 3 < E1) {
-          const double2 a0 = *(const double2 *)(a + e), a1 = *(const double2 *)(a + e + 2);
-          aq[4 * q] = a0.x; aq[4 * q + 1] = a0.y; aq[4 * q + 2] = a1.x; aq[4 * q + 3] = a1.y;
-          if (x) {
-            const uint4 c = *(const uint4 *)(col + e);
-            cq[4 * q] = c.x; cq[4 * q + 1] = c.y; cq[4 * q + 2] = c.z; cq[4 * q + 3] = c.w;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            aq[4 * q + j] = e + j < E1 ? a[e + j] : 0.0;
-            cq[4 * q + j] = (x && e + j < E1) ? col[e + j] : 0u;
-          }
-        }
-      }
-    };
-    // the products of a loaded chunk, straight into LDS in entry order
-    auto form = [&](uint64_t B, const uint32_t (&cq)[16], const double (&aq)[16]) {
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint64_t e = B + 4 * (uint64_t)(lane + 64 * q) + j;
-          const bool ok = e >= E0 && e < E1;
-          buf[w][4 * (lane + 64 * q) + j] = ok ? (x ? aq[4 * q + j] * x[cq[4 * q + j]] : aq[4 * q + j]) : 0.0;
-        }
-    };
-    uint64_t B = E0 & ~3ull;
-    uint32_t cq[16];
-    double aq[16];
-    if (B < E1) {
-      load(B, cq, aq);
-      form(B, cq, aq);
-    }
-    for (; B < E1; B += CH) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint64_t Bn = B + CH;
-      if (Bn < E1) load(Bn, cq, aq);                 // next chunk in flight during the adds
-      if (own) {
-        const int lo = (int)(max(r0, B) - B), hi = (int)(min(r1, Bn) - B);
-        int p = lo;
-        for (; p + 8 <= hi; p += 8) {                  // LDS reads 8 ahead of the adds
-          double u[8];
-#pragma unroll
-          for (int e = 0; e < 8; e++) u[e] = buf[w][p + e];
-#pragma unroll
-          for (int e = 0; e < 8; e++) t += u[e];
-          if (AMX) {
-#pragma unroll
-            for (int e = 0; e < 8; e++)
-              if (u[e] > pmx) { pmx = u[e]; ppos = B + p + e; }
-          }
-        }
-        for (; p < hi; p++) {
-          const double u = buf[w][p];
-          t += u;
-          if (AMX && u > pmx) { pmx = u; ppos = B + p; }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (Bn < E1) form(Bn, cq, aq);
-    }
-    if (own) {
-      const uint64_t i = rb + lane;
-      double vz = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
-      if (f) vz = vz * (f[i] ? 1.0 : 0.0);
-      z[i] = vz;
-      if (AMX) { amx[i] = pmx; apos[i] = ppos; }
-    }
-  }
-}
-
 // rows per wavefront of the lane kernel for n rows (>= ~2048 wavefronts in flight)
 static int64_t g_rw_forced = -2;     // AMGD_SL_RW / amgd_spmv_set_rw (tests): 4, 16 or 64
 extern "C" void amgd_spmv_set_rw(int rw) { g_rw_forced = rw < 0 ? -2 : rw; }
@@ -1012,95 +750,26 @@ static int lane_rw(uint64_t n) {
   if (g_rw_forced == 4 || g_rw_forced == 16 || g_rw_forced == 64) return (int)g_rw_forced;
   return n >= (1u << 22) ? 64 : n >= (1u << 16) ? 16 : 4;
 }
-// AMGD_SPMV_NT=1: the matrix stream (columns, values) read with nontemporal loads
-static int spmv_nt() {
-  static int v = -1;
-  if (v < 0) { const char *e = getenv("AMGD_SPMV_NT"); v = e && *e ? atoi(e) : 0; }
-  return v;
-}
-#define LANE_LAUNCH_NT(LIST, NTL, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_)              \
-  do {                                                                                        \
-    if (rw_ == 64)                                                                            \
-      k_spmv_lane<LIST, 64, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
-                                                            z_, al, y_, be, f_, ml_);         \
-    else if (rw_ == 16)                                                                       \
-      k_spmv_lane<LIST, 16, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
-                                                            z_, al, y_, be, f_, ml_);         \
-    else                                                                                      \
-      k_spmv_lane<LIST, 4, NTL><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
-                                                           z_, al, y_, be, f_, ml_);          \
-  } while (0)
-// AMGD_SPMV_CHUNK=0 / amgd_spmv_set_chunk(0): whole-matrix products on k_spmv_lane's
-// row segments instead of k_spmv_chunk's contiguous 16-byte-load chunks (same sums)
-static int g_spmv_chunk = -1;
-extern "C" void amgd_spmv_set_chunk(int on) { g_spmv_chunk = on < 0 ? -1 : on; }  // 2: all rows
-// Chunks win where rows are moderate (256^3: rows of ~130 entries, PCG on the level-1
-// constraint operator: 3.32 -> 2.53 ms) and lose where they are long (one lane adds a
-// whole 1024-entry chunk of one row in order: rows of 700-8000 entries 1.6-2.6x slower,
-// profiles/r03/spmv_bench_chunk_vs_segments.txt): by default rows of mean < 256.
-static bool spmv_chunk_ok(const dcsr *M) {
-  // off by default: at 256^3 the chunks lost to the per-row segments even on the moderate
-  // rows (SpMV 6245 -> 6391 ms per setup, profiles/r03/ab256_r03j_chunk_lmopwave.txt)
-  if (g_spmv_chunk < 0) { const char *e = getenv("AMGD_SPMV_CHUNK"); g_spmv_chunk = e && *e ? atoi(e) : 0; }
-  const bool moderate = M->nnz < 256ull * M->rn || g_spmv_chunk == 2;
-  return g_spmv_chunk && moderate && !((uintptr_t)M->col & 15) && !((uintptr_t)M->a & 15);
-}
-#define CHUNK_LAUNCH(AMX_, rw_, g_, n_, x_, z_, al, y_, be, f_, amx_, apos_)                  \
-  do {                                                                                        \
-    if (rw_ == 64)                                                                            \
-      k_spmv_chunk<64, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_, \
-                                                      be, f_, amx_, apos_);                   \
-    else if (rw_ == 16)                                                                       \
-      k_spmv_chunk<16, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_, \
-                                                      be, f_, amx_, apos_);                   \
-    else                                                                                      \
-      k_spmv_chunk<4, AMX_><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, x_, z_, al, y_,  \
-                                                     be, f_, amx_, apos_);                    \
-  } while (0)
-// AMGD_SPMV_PIPE bits / amgd_spmv_set_pipe: lane products through k_spmv_pipe (gather one
-// round ahead; same sums) -- 1 whole-matrix, 2 listed rows; entries per lane per round 8,
-// or 4 (bit 4), 16 (bit 8), 12 (bit 16).  Default 11: both, 16 per lane (256^3 SpMV
-// 6.26 -> 5.46 s; 8 per lane 5.64 s, 4: 6.98 s, 12: 7.95 s; tools/ab_setup.py, r03m)
-static int g_spmv_pipe = -1;
-extern "C" void amgd_spmv_set_pipe(int on) { g_spmv_pipe = on < 0 ? -1 : on; }
-static int spmv_pipe() {
-  if (g_spmv_pipe < 0) { const char *e = getenv("AMGD_SPMV_PIPE"); g_spmv_pipe = e && *e ? atoi(e) : 11; }
-  return g_spmv_pipe;
-}
-#define PIPE_LAUNCH_P(LIST, PER_, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_)               \
-  do {                                                                                        \
-    if (rw_ == 64)                                                                            \
-      k_spmv_pipe<LIST, 64, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
-                                                             z_, al, y_, be, f_, ml_);        \
-    else if (rw_ == 16)                                                                       \
-      k_spmv_pipe<LIST, 16, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_, \
-                                                             z_, al, y_, be, f_, ml_);        \
-    else                                                                                      \
-      k_spmv_pipe<LIST, 4, PER_><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
-                                                            z_, al, y_, be, f_, ml_);         \
-  } while (0)
-// entries per lane per round of k_spmv_pipe (AMGD_SPMV_PIPE bits 4: 4, 8: 16, 16: 12; else 8)
-#define PIPE_LAUNCH(LIST, rw_, n_, list_, x_, z_, al, y_, be, f_, ml_)                           \
-  do {                                                                                        \
-    const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
-    if (spmv_pipe() & 4) PIPE_LAUNCH_P(LIST, 4, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
-    else if (spmv_pipe() & 8) PIPE_LAUNCH_P(LIST, 16, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
-    else if (spmv_pipe() & 16) PIPE_LAUNCH_P(LIST, 12, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_); \
-    else PIPE_LAUNCH_P(LIST, 8, rw_, gp_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
-  } while (0)
+// Long-row products: k_spmv_pipe, 16 entries per lane per round (round 3: 256^3 SpMV
+// 6.26 -> 5.46 s against the round-2 lane kernel; 8 per lane 5.64 s, 4: 6.98 s, 12:
+// 7.95 s -- tools/ab_setup.py, r03m).  The round-2 lane kernel, the contiguous-chunk
+// kernel, nontemporal loads and the fused selection / column-sum variants measured
+// slower and were removed in round 4.
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
     amgd_route_hit(AMGD_R_SPMV_LANE);                                                         \
-    const int g_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536);  \
-    if (!(LIST) && spmv_chunk_ok(M))                                                          \
-      CHUNK_LAUNCH(false, rw_, g_, n_, x_, z_, al, y_, be, f_, (double *)nullptr, (uint64_t *)nullptr); \
-    else if (spmv_pipe() & (LIST ? 2 : 1))                                                    \
-      PIPE_LAUNCH(LIST, rw_, n_, list_, x_, z_, al, y_, be, f_, ml_);                         \
-    else if (spmv_nt())                                                                       \
-      LANE_LAUNCH_NT(LIST, true, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);            \
+    amgd_route_hit(rw_ == 64 ? AMGD_R_MV_RW64 : rw_ == 16 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);   \
+    const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
+    if (rw_ == 64)                                                                            \
+      k_spmv_pipe<LIST, 64><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,     \
+                                                       z_, al, y_, be, f_, ml_);              \
+    else if (rw_ == 16)                                                                       \
+      k_spmv_pipe<LIST, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,     \
+                                                       z_, al, y_, be, f_, ml_);              \
     else                                                                                      \
-      LANE_LAUNCH_NT(LIST, false, rw_, g_, n_, list_, x_, z_, al, y_, be, f_, ml_);           \
+      k_spmv_pipe<LIST, 4><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,      \
+                                                      z_, al, y_, be, f_, ml_);               \
   } while (0)
 // ordered sums (x == nullptr) or products of the listed rows only (rows longer than
 // maxlen are skipped: k_rows_exact does them)
@@ -1290,90 +959,6 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
     k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
   }
   KCHECK();
-}
-// z = M x and, per row, the largest product M(i,k) x_k with its first entry position
-// (find_support: w = R' rs and the selection's argmax of R(i,c) rs_i per column c, in one
-// pass over R').  Only the whole-matrix lane kernel path (long rows, one GPU); returns 0
-// where that path does not apply -- the caller then multiplies and selects separately.
-static int g_fs_fused = -1;     // AMGD_FS_FUSED=1 / amgd_spmv_set_fused(1): fused selection
-extern "C" void amgd_spmv_set_fused(int on) { g_fs_fused = on < 0 ? -1 : on; }
-extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, double *amx, uint64_t *apos) {
-  if (M->rn == 0 || amgd_nshards() > 1 || M->nnz < 32ull * M->rn || (int64_t)M->rn < sl_min_whole())
-    return 0;
-  // off by default: keeping the argmax in the ordered-add loop lengthens the adding lanes'
-  // dependent chain -- at 256^3 the SpMVs took +3.1 s against 0.7 s of selection saved
-  // (profiles/r03/ab256_r03i_chunk_fused.txt)
-  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 0; }
-  if (!g_fs_fused) return 0;
-  const int rw_ = lane_rw(M->rn);
-  const int g_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
-  amgd_route_hit(AMGD_R_SPMV_LANE);
-  amgd_route_hit(AMGD_R_FS_FUSED);
-  amgd_timer_start(1);
-  if (spmv_chunk_ok(M))
-    CHUNK_LAUNCH(true, rw_, g_, M->rn, x, z, 0.0, (const double *)nullptr, 1.0, (const uint8_t *)nullptr, amx, apos);
-  else if ((spmv_pipe() & 1) && rw_ == 64)
-    k_spmv_pipe<false, 64, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  else if ((spmv_pipe() & 1) && rw_ == 16)
-    k_spmv_pipe<false, 16, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  else if (spmv_pipe() & 1)
-    k_spmv_pipe<false, 4, 16, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                              0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  else if (rw_ == 64)
-    k_spmv_lane<false, 64, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                                0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  else if (rw_ == 16)
-    k_spmv_lane<false, 16, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                                0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  else
-    k_spmv_lane<false, 4, false, true><<<g_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, nullptr, x, z,
-                                                               0.0, nullptr, 1.0, nullptr, 0xffffffffu, amx, apos);
-  amgd_timer_stop(1);
-  KCHECK();
-  const uint64_t rest = 16ull * M->rn + 8;
-  g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
-  g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
-  g_mv_launches++;
-  return 1;
-}
-// z = M x and z2 = M 1 (each row's ordered sum of its values, amgd_colsum on M = R') from
-// one pass over M: find_support's w = R' rs and sumR.  Only where the whole-matrix
-// k_spmv_pipe path applies (long rows, one GPU, AMGD_SPMV_SUM2=1); returns 0 otherwise.
-// Off by default: bit-exact (tests), but the second ordered chain costs the SpMV about
-// what the skipped column re-sums save (256^3: SpMV +0.38 s, setup -0.07 s in an
-// interleaved A/B, profiles/r03/ab256_r03s2_sum2_lmopsmall.txt).
-static int g_spmv_sum2 = -1;
-extern "C" void amgd_spmv_set_sum2(int on) { g_spmv_sum2 = on < 0 ? -1 : on; }
-extern "C" int amgd_spmv_sum2_ok(const dcsr *M) {
-  if (g_spmv_sum2 < 0) { const char *e = getenv("AMGD_SPMV_SUM2"); g_spmv_sum2 = e && *e ? atoi(e) : 0; }
-  if (g_fs_fused < 0) { const char *e = getenv("AMGD_FS_FUSED"); g_fs_fused = e && *e ? atoi(e) : 0; }
-  return g_spmv_sum2 && !g_fs_fused && M->rn && amgd_nshards() <= 1 && M->nnz >= 32ull * M->rn &&
-         (int64_t)M->rn >= sl_min_whole() && (spmv_pipe() & 1) && !spmv_chunk_ok(M);
-}
-extern "C" int amgd_spmv_sum2(const dcsr *M, const double *x, double *z, double *z2) {
-  if (!amgd_spmv_sum2_ok(M)) return 0;
-  const int rw_ = lane_rw(M->rn);
-  const int g_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
-  amgd_route_hit(AMGD_R_SPMV_LANE);
-  amgd_timer_start(1);
-  if (rw_ == 64)
-    k_spmv_pipe<false, 64, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
-        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
-  else if (rw_ == 16)
-    k_spmv_pipe<false, 16, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
-        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
-  else
-    k_spmv_pipe<false, 4, 16, false, true><<<g_, 256, 0, amgd_s()>>>(
-        M->ro, M->col, M->a, M->rn, nullptr, x, z, 0.0, nullptr, 1.0, nullptr, 0xffffffffu, nullptr, nullptr, z2);
-  amgd_timer_stop(1);
-  KCHECK();
-  const uint64_t rest = 24ull * M->rn + 8;
-  g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
-  g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
-  g_mv_launches++;
-  return 1;
 }
 // rows-filtered SpMV (k_spmv arithmetic at any row length): z_i = (M x)_i * f_i on
 // the 256-row blocks holding a row i with fs[i] - fb <= fr
@@ -2278,401 +1863,6 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
   }
 }
 
-// Wide output rows (thousands of distinct columns): a dense LDS accumulator over a
-// column window [wb, wb+W) instead of a hash table.  The row's column range is
-// covered window by window; in each window the A entries are taken in ascending k
-// (layers) and all threads cover the part of that B row inside the window (B rows
-// are sorted, so it is the next run after a per-layer cursor); one barrier per layer
-// orders layer k before layer k+1, so every output is summed in the reference's
-// order.  No probing, no CAS, and the window is emitted in column order (no sort).
-// The next layer's loads are issued before the current layer's adds.
-template <int W, int RAP = 0>
-__global__ __launch_bounds__(256) void k_sg_win(const uint32_t *rows, uint32_t nrows,
-                                                const uint64_t *aro, const uint32_t *acol,
-                                                const double *aa, const uint64_t *bro,
-                                                const uint32_t *bcol, const double *ba,
-                                                uint64_t *cnt2, const uint64_t *xro,
-                                                uint32_t *xcol, double *xa) {
-  constexpr int NT = 256, SPT = W / NT;
-  __shared__ double acc[W];
-  __shared__ uint8_t tch[W];
-  __shared__ uint64_t lbs[NT];
-  __shared__ uint32_t llen[NT], lcur[NT];
-  __shared__ double lav[NT];
-  __shared__ uint32_t wtot[NT / 64 + 1];
-  __shared__ uint32_t s_min, s_max;
-  const int t = threadIdx.x;
-  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    const uint32_t i = rows[r];
-    const uint64_t a0 = aro[i], a1 = aro[i + 1];
-    const uint64_t ob = xro[i];
-    const bool multi = a1 - a0 > (uint64_t)NT;
-    if (t == 0) { s_min = 0xffffffffu; s_max = 0; }
-    __syncthreads();
-    for (uint64_t ka = a0 + t; ka < a1; ka += NT) {     // column range of the row
-      const uint32_t k = acol[ka];
-      if (ka + 1 < a1 && acol[ka + 1] == k) continue;
-      const uint64_t b0 = bro[k], b1 = bro[k + 1];
-      if (b0 < b1) {
-        atomicMin(&s_min, bcol[b0]);
-        atomicMax(&s_max, bcol[b1 - 1]);
-      }
-    }
-    __syncthreads();
-    const uint32_t cmin = s_min, cmax = s_max;
-    uint32_t nout = 0;
-    for (uint64_t wbl = cmin; wbl <= (uint64_t)cmax && cmin <= cmax; wbl += W) {
-      const uint32_t wb = (uint32_t)wbl;
-      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + W - 1);   // inclusive
-      for (int q = t; q < W; q += NT) { acc[q] = 0.0; tch[q] = 0; }
-      for (uint64_t c0 = a0; c0 < a1; c0 += NT) {
-        const int ne = (int)min((uint64_t)NT, a1 - c0);
-        if (multi || wb == cmin) {                      // layer table of this chunk
-          if (t < ne) {
-            const uint64_t ka = c0 + t;
-            const uint32_t k = acol[ka];
-            uint32_t len = 0;
-            uint64_t b0 = 0;
-            if (!(ka + 1 < a1 && acol[ka + 1] == k)) {   // duplicate columns: the last one wins
-              b0 = bro[k];
-              len = (uint32_t)(bro[k + 1] - b0);
-            }
-            uint32_t cur = 0;
-            if (wb != cmin) {                           // lower_bound(wb) in the B row
-              uint32_t lo = 0, hi = len;
-              while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (bcol[b0 + mid] < wb) lo = mid + 1;
-                else hi = mid;
-              }
-              cur = lo;
-            }
-            lbs[t] = b0;
-            llen[t] = len;
-            lav[t] = aa[ka];
-            lcur[t] = cur;
-          }
-        }
-        __syncthreads();
-        auto nextl = [&](int e) {
-          e++;
-          while (e < ne && lcur[e] >= llen[e]) e++;
-          return e;
-        };
-        // three-stage pipeline over layers: the columns of layer e+2 and the values of
-        // layer e+1 (only where its column falls in the window) are in flight while
-        // layer e is added; out-of-window entries cost a 4-byte column read only
-        int e = nextl(-1);
-        uint32_t off = 0, col = 0xffffffffu;
-        double val = 0.0;
-        if (e < ne) {
-          off = lcur[e];
-          const uint32_t j = off + t;
-          if (j < llen[e]) {
-            col = bcol[lbs[e] + j];
-            if (col <= we) val = ba[lbs[e] + j];
-          }
-        }
-        int e2 = e < ne ? nextl(e) : ne;
-        uint32_t col2 = 0xffffffffu;
-        if (e2 < ne) {
-          const uint32_t j = lcur[e2] + t;
-          if (j < llen[e2]) col2 = bcol[lbs[e2] + j];
-        }
-        while (e < ne) {
-          const int e3 = e2 < ne ? nextl(e2) : ne;
-          double val2 = 0.0;
-          if (e2 < ne && col2 <= we) val2 = ba[lbs[e2] + lcur[e2] + t];
-          uint32_t col3 = 0xffffffffu;
-          if (e3 < ne) {
-            const uint32_t j = lcur[e3] + t;
-            if (j < llen[e3]) col3 = bcol[lbs[e3] + j];
-          }
-          const bool in = col <= we;
-          if (in) {
-            const uint32_t q = col - wb;
-            acc[q] = acc[q] + val * lav[e];
-            tch[q] = 1;
-          }
-          const uint32_t n = (uint32_t)__syncthreads_count(in);   // layer k before k+1
-          off += n;
-          if (n == (uint32_t)NT) {                     // more of this layer in the window
-            const uint32_t j = off + t;
-            col = 0xffffffffu;
-            if (j < llen[e]) {
-              col = bcol[lbs[e] + j];
-              if (col <= we) val = ba[lbs[e] + j];
-            }
-            continue;                                  // (stages e2/e3 are reissued)
-          }
-          if (t == 0) lcur[e] = off;
-          e = e2;
-          if (e < ne) off = lcur[e];
-          col = col2;
-          val = val2;
-          e2 = e3;
-          col2 = col3;
-        }
-        __syncthreads();
-      }
-      // emit the window in column order: each thread a run of SPT slots
-      uint32_t c = 0;
-      for (int q = 0; q < SPT; q++) {
-        const int sl = t * SPT + q;
-        c += (tch[sl] && acc[sl] != 0.0) ? 1u : 0u;
-      }
-      const uint32_t inc = block_incl_scan<NT>(c, wtot);
-      uint64_t o = ob + nout + (inc - c);
-      for (int q = 0; q < SPT; q++) {
-        const int sl = t * SPT + q;
-        if (tch[sl] && acc[sl] != 0.0) {
-          xcol[o] = wb + (uint32_t)sl;
-          xa[o] = acc[sl];
-          o++;
-        }
-      }
-      nout += wtot[0] + (NT / 64 > 1 ? wtot[1] : 0) + (NT / 64 > 2 ? wtot[2] : 0) +
-              (NT / 64 > 3 ? wtot[3] : 0);
-      __syncthreads();
-    }
-    if (t == 0) cnt2[i] = nout;
-    __syncthreads();
-  }
-}
-
-// Tiled windowed SpGEMM: a work-group takes T consecutive rows of the windowed-row
-// list (runs of ascending row indices: neighbouring rows, whose A rows share most of
-// their k) and walks the UNION of their A entries in ascending k.  Each B row k is
-// loaded once for the tile and added into the window accumulator of every tile row
-// holding k; one barrier per distinct k of the union orders layer k before layer k'.
-// Per output row the additions still arrive one layer at a time in ascending k,
-// starting from +0 -- the reference's sum, bit for bit -- while the B-row loads and
-// the barriers (the k_sg_win cost) fall by the tile's k overlap.
-// A rows are taken in chunks of M = NT/T entries per row (one wavefront per row for
-// T = 4); each chunk's union is ordered by (k, row) with merge-path ranks (binary
-// searches in the other rows' compacted chunk), so no sort pass.  Chunks follow
-// each other in ascending k per row, which is all the per-row order needs.
-template <int W, int T, int RAP = 0>
-__global__ __launch_bounds__(256) void k_sg_wt(const uint32_t *rows, uint32_t nrows,
-                                               const uint64_t *aro, const uint32_t *acol,
-                                               const double *aa, const uint64_t *bro,
-                                               const uint32_t *bcol, const double *ba,
-                                               uint64_t *cnt2, const uint64_t *xro,
-                                               uint32_t *xcol, double *xa) {
-  constexpr int NT = 256, SPT = W / NT, M = NT / T;
-  static_assert(M == 32 || M == 64, "one or two tile rows per wavefront");
-  __shared__ double acc[T * W];
-  __shared__ uint32_t sk[T][M];           // chunk keys of each row, compacted, ascending
-  __shared__ double sa[T][M];
-  __shared__ uint32_t sn[T];
-  __shared__ uint32_t uk[NT];             // chunk union ordered by (k, row)
-  __shared__ uint8_t ut[NT];
-  __shared__ double ua[NT];
-  __shared__ uint32_t gfirst[NT + 1];     // distinct k: first union entry
-  __shared__ uint64_t gb0[NT];
-  __shared__ uint32_t glen[NT], gcur[NT];
-  __shared__ uint32_t s_ng, s_min, s_max;
-  __shared__ uint32_t wtot[NT / 64 + 1];
-  __shared__ uint32_t s_i[T], s_nout[T];
-  __shared__ uint64_t s_a0[T], s_a1[T];
-  const int t = threadIdx.x, lane = t & 63;
-  const uint32_t ntiles = (nrows + T - 1) / T;
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int nt = (int)min((uint32_t)T, nrows - tile * T);
-    if (t < T) {
-      if (t < nt) {
-        const uint32_t i = rows[tile * T + t];
-        s_i[t] = i;
-        s_a0[t] = aro[i];
-        s_a1[t] = aro[i + 1];
-      } else {
-        s_i[t] = 0xffffffffu;
-        s_a0[t] = s_a1[t] = 0;
-      }
-      s_nout[t] = 0;
-    }
-    if (t == 0) { s_min = 0xffffffffu; s_max = 0; }
-    __syncthreads();
-    uint64_t maxlen = 0;
-    for (int r = 0; r < nt; r++) {                     // column range of the tile
-      const uint64_t a0 = s_a0[r], a1 = s_a1[r];
-      maxlen = max(maxlen, a1 - a0);
-      for (uint64_t ka = a0 + t; ka < a1; ka += NT) {
-        const uint32_t k = acol[ka];
-        if (ka + 1 < a1 && acol[ka + 1] == k) continue;
-        const uint64_t b0 = bro[k], b1 = bro[k + 1];
-        if (b0 < b1) {
-          atomicMin(&s_min, bcol[b0]);
-          atomicMax(&s_max, bcol[b1 - 1]);
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t cmin = s_min, cmax = s_max;
-    const uint32_t nch = (uint32_t)((maxlen + M - 1) / M);
-    for (uint64_t wbl = cmin; cmin <= cmax && wbl <= (uint64_t)cmax; wbl += W) {
-      const uint32_t wb = (uint32_t)wbl;
-      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + W - 1);   // inclusive
-      for (int q = t; q < nt * W; q += NT) acc[q] = 0.0;
-      for (uint32_t c = 0; c < nch; c++) {
-        if (nch > 1 || wb == cmin) {                   // union table of this chunk
-          const int r = t / M, m = t % M;
-          bool v = false;
-          uint32_t k = 0;
-          double a = 0.0;
-          if (r < nt) {
-            const uint64_t ka = s_a0[r] + (uint64_t)c * M + m, a1 = s_a1[r];
-            if (ka < a1) {
-              k = acol[ka];
-              v = !(ka + 1 < a1 && acol[ka + 1] == k);   // duplicate columns: the last one wins
-              if (v) a = aa[ka];
-            }
-          }
-          const unsigned long long bal = __ballot(v);
-          const int sh = M == 64 ? 0 : (lane / M) * M;
-          const unsigned long long rmask = M == 64 ? ~0ull : (((1ull << M) - 1ull) << sh);
-          const uint32_t pos = (uint32_t)__popcll(bal & rmask & ((1ull << lane) - 1ull));
-          if (v) { sk[r][pos] = k; sa[r][pos] = a; }
-          if (m == 0) sn[r] = (uint32_t)__popcll(bal & rmask);
-          __syncthreads();
-          if (v) {                                      // rank in the union by (k, row)
-            uint32_t rank = pos;
-            for (int r2 = 0; r2 < nt; r2++) {
-              if (r2 == r) continue;
-              uint32_t lo = 0, hi = sn[r2];
-              while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                const uint32_t km = sk[r2][mid];
-                if (r2 < r ? km <= k : km < k) lo = mid + 1;
-                else hi = mid;
-              }
-              rank += lo;
-            }
-            uk[rank] = k;
-            ut[rank] = (uint8_t)r;
-            ua[rank] = a;
-          }
-          uint32_t ntot = 0;
-          for (int r2 = 0; r2 < T; r2++) ntot += sn[r2];
-          __syncthreads();
-          const bool st = (uint32_t)t < ntot && (t == 0 || uk[t] != uk[t - 1]);
-          const uint32_t inc = block_incl_scan<NT>(st ? 1u : 0u, wtot);
-          if (st) {
-            const uint32_t g = inc - 1, kk = uk[t];
-            const uint64_t b0 = bro[kk];
-            const uint32_t len = (uint32_t)(bro[kk + 1] - b0);
-            uint32_t cur = 0;
-            if (wb != cmin) {                           // lower_bound(wb) in the B row
-              uint32_t lo = 0, hi = len;
-              while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (bcol[b0 + mid] < wb) lo = mid + 1;
-                else hi = mid;
-              }
-              cur = lo;
-            }
-            gfirst[g] = (uint32_t)t;
-            gb0[g] = b0;
-            glen[g] = len;
-            gcur[g] = cur;
-          }
-          if (t == NT - 1) {
-            s_ng = inc;
-            gfirst[inc] = ntot;
-          }
-        }
-        __syncthreads();
-        const int ne = (int)s_ng;
-        auto nextg = [&](int e) {
-          e++;
-          while (e < ne && gcur[e] >= glen[e]) e++;
-          return e;
-        };
-        // the k_sg_win pipeline over distinct k: columns of group e+2 and values of group
-        // e+1 in flight while group e is added into every member row's accumulator
-        int e = nextg(-1);
-        uint32_t off = 0, col = 0xffffffffu;
-        double val = 0.0;
-        if (e < ne) {
-          off = gcur[e];
-          const uint32_t j = off + t;
-          if (j < glen[e]) {
-            col = bcol[gb0[e] + j];
-            if (col <= we) val = ba[gb0[e] + j];
-          }
-        }
-        int e2 = e < ne ? nextg(e) : ne;
-        uint32_t col2 = 0xffffffffu;
-        if (e2 < ne) {
-          const uint32_t j = gcur[e2] + t;
-          if (j < glen[e2]) col2 = bcol[gb0[e2] + j];
-        }
-        while (e < ne) {
-          const int e3 = e2 < ne ? nextg(e2) : ne;
-          double val2 = 0.0;
-          if (e2 < ne && col2 <= we) val2 = ba[gb0[e2] + gcur[e2] + t];
-          uint32_t col3 = 0xffffffffu;
-          if (e3 < ne) {
-            const uint32_t j = gcur[e3] + t;
-            if (j < glen[e3]) col3 = bcol[gb0[e3] + j];
-          }
-          const bool in = col <= we;
-          if (in) {
-            const uint32_t q = col - wb;
-            const uint32_t u1 = gfirst[e + 1];
-            for (uint32_t u = gfirst[e]; u < u1; u++) {
-              double *p = &acc[(uint32_t)ut[u] * W + q];
-              *p = *p + val * ua[u];
-            }
-          }
-          const uint32_t n = (uint32_t)__syncthreads_count(in);   // layer k before k'
-          off += n;
-          if (n == (uint32_t)NT) {                     // more of this B row in the window
-            const uint32_t j = off + t;
-            col = 0xffffffffu;
-            if (j < glen[e]) {
-              col = bcol[gb0[e] + j];
-              if (col <= we) val = ba[gb0[e] + j];
-            }
-            continue;
-          }
-          if (t == 0) gcur[e] = off;
-          e = e2;
-          if (e < ne) off = gcur[e];
-          col = col2;
-          val = val2;
-          e2 = e3;
-          col2 = col3;
-        }
-        __syncthreads();
-      }
-      // emit the window of every tile row in column order (each thread a run of SPT slots)
-      for (int r = 0; r < nt; r++) {
-        uint32_t cc = 0;
-        for (int q = 0; q < SPT; q++) cc += acc[r * W + t * SPT + q] != 0.0 ? 1u : 0u;
-        const uint32_t inc = block_incl_scan<NT>(cc, wtot);
-        uint64_t o = xro[s_i[r]] + s_nout[r] + (inc - cc);
-        for (int q = 0; q < SPT; q++) {
-          const int sl = t * SPT + q;
-          const double v = acc[r * W + sl];
-          if (v != 0.0) {
-            xcol[o] = wb + (uint32_t)sl;
-            xa[o] = v;
-            o++;
-          }
-        }
-        uint32_t tot = 0;
-        for (int w = 0; w < NT / 64; w++) tot += wtot[w];
-        __syncthreads();
-        if (t == 0) s_nout[r] += tot;
-        __syncthreads();
-      }
-    }
-    if (t < nt) cnt2[s_i[t]] = s_nout[t];
-    __syncthreads();
-  }
-}
-
 // long rows: block per row, dense slab acc[cn] + stamp[cn] per resident block
 template <int MODE, int RAP = 0>
 __global__ __launch_bounds__(256) void k_spgemm_long(
@@ -2766,48 +1956,6 @@ extern "C" void amgd_spgemm_set_win(int w) {
   g_sg_win = w < 0 ? -1 : w;
   g_sg_win_forced = w > 0;
 }
-// the windowed kernel pays one barrier per layer per window: it wins while the output
-// rows span few windows (narrow column spaces), the hash kernels beyond
-static int g_sg_wsym = -1;      // AMGD_SG_WSYM: byte-map window of the symbolic kernel (0: hash)
-static int sg_wsym() {
-  if (g_sg_wsym < 0) {
-    const char *e = getenv("AMGD_SG_WSYM");
-    g_sg_wsym = e ? atoi(e) : 32768;
-    if (g_sg_wsym != 0 && g_sg_wsym != 8192 && g_sg_wsym != 16384 && g_sg_wsym != 32768 &&
-        g_sg_wsym != 65536)
-      g_sg_wsym = 32768;
-  }
-  return g_sg_wsym;
-}
-extern "C" void amgd_spgemm_set_wsym(int w) { g_sg_wsym = w; }
-// AMGD_SG_WT: rows per tile of the tiled windowed kernel k_sg_wt (4 or 8; 0: one row per
-// work-group, k_sg_win); windows of 1024 / 2048 columns only
-static int g_sg_wt = -1;
-static int sg_wt() {
-  if (g_sg_wt < 0) {
-    const char *e = getenv("AMGD_SG_WT");
-    g_sg_wt = e && *e ? atoi(e) : 0;
-    if (g_sg_wt != 0 && g_sg_wt != 4 && g_sg_wt != 8) g_sg_wt = 4;
-  }
-  return g_sg_wt;
-}
-extern "C" void amgd_spgemm_set_wt(int t) { g_sg_wt = t < 0 ? -1 : t; }
-// AMGD_SG_WWIN bits: 1 windowed numeric rows, 2 wide symbolic rows, 4 the 4096- / 8192-slot
-// hash-bin numeric rows through the wave-private windowed kernel k_sg_wwin; 8: its numeric
-// window 1024 columns (64: 512; else 2048); 16: symbolic byte windows of 4096 columns (32:
-// 2048; else 16384).
-// Default 27: windowed numeric rows at 1024 columns (256^3 RAP kernels 1476 -> 1355 ms) and
-// the wide symbolic rows at 4096-column byte windows (setup -0.2 s; 16384: +1.2 s, 2048:
-// +0.35 s); numeric 512 columns +0.3 s, hash-bin rows +1.5 s (tools/ab_setup.py, r03m)
-static int g_sg_wwin = -1;
-static int sg_wwin() {
-  if (g_sg_wwin < 0) {
-    const char *e = getenv("AMGD_SG_WWIN");
-    g_sg_wwin = e && *e ? atoi(e) : 27;
-  }
-  return g_sg_wwin;
-}
-extern "C" void amgd_spgemm_set_wwin(int m) { g_sg_wwin = m; }
 static uint32_t sg_win_p0() {
   static long v = -1;
   if (v < 0) { const char *e = getenv("AMGD_SG_WIN_P0"); v = e ? atol(e) : 48; }
@@ -2818,6 +1966,14 @@ static uint64_t g_sg_bytes = 0, g_sg_launches = 0;
 extern "C" uint64_t amgd_spgemm_launches(void) { return g_sg_launches; }
 static int g_sg_pattern = 0;    // amgd_spgemm_pattern: hash-bin rows emit the pattern only
 extern "C" void amgd_spgemm_set_timer(int slot) { g_sg_slot = slot; }
+extern "C" void amgd_sparse_reset_state(void) {
+  g_sg_slot = -1;
+  g_sg_pattern = 0;
+}
+extern "C" void amgd_reset_call_state(void) {
+  amgd_sparse_reset_state();
+  amgd_interp_reset_state();
+}
 extern "C" void amgd_spgemm_bytes_reset(void) { g_sg_bytes = 0; g_sg_launches = 0; }
 extern "C" uint64_t amgd_spgemm_bytes(void) { return g_sg_bytes; }
 
@@ -2904,137 +2060,6 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
     atomicAdd(&h[q], 1ull);
   }
 }
-// Symbolic pass for rows with many products: distinct columns counted with an LDS
-// byte map over a column window [wb, wb+SW) instead of a hash table (no probing, no
-// CAS; counting needs no order).  Layers (B rows, sorted) are taken one WAVEFRONT
-// at a time: the 64 lanes load 64 consecutive columns from the layer's cursor
-// (one coalesced 256 B load), mark the in-window ones (a prefix, the row being
-// sorted) and advance the cursor by their count until the layer leaves the window.
-// Windows cover the row's column range [cmin, cmax]; rows with more than MAXL layers
-// take them MAXL at a time.  No capacity limit: every row gets its exact count (no
-// dense-slab recount).
-template <int SW>
-__global__ __launch_bounds__(256) void k_sg_wsym(const uint32_t *rows, uint32_t nrows,
-                                                 const uint64_t *aro, const uint32_t *acol,
-                                                 const uint64_t *bro, const uint32_t *bcol,
-                                                 uint64_t *cnt) {
-  constexpr int NT = 256, NW = NT / 64, MAXL = 1024;
-  __shared__ uint32_t map[SW / 4];
-  __shared__ uint64_t lbs[MAXL];
-  __shared__ uint32_t lend[MAXL], lcur[MAXL];
-  __shared__ uint16_t lact[MAXL];
-  __shared__ uint32_t s_min, s_max;
-  __shared__ unsigned s_nact;
-  __shared__ unsigned long long s_tot;
-  uint8_t *mb = (uint8_t *)map;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
-    const uint32_t i = rows[r];
-    const uint64_t a0 = aro[i], a1 = aro[i + 1];
-    const uint64_t nl = a1 - a0;
-    // rows with more layers than the table: the layers are taken MAXL at a time in
-    // every window, each chunk's cursors found by bisection for the window start
-    const bool chunked = nl > (uint64_t)MAXL;
-    if (t == 0) { s_min = 0xffffffffu; s_max = 0; s_tot = 0; }
-    __syncthreads();
-    for (uint64_t e = t; e < nl; e += NT) {
-      const uint32_t k = acol[a0 + e];
-      const uint64_t b0 = bro[k], b1 = bro[k + 1];
-      if (!chunked) {
-        lbs[e] = b0;
-        lend[e] = (uint32_t)(b1 - b0);
-        lcur[e] = 0;
-      }
-      if (b0 < b1) {
-        atomicMin(&s_min, bcol[b0]);
-        atomicMax(&s_max, bcol[b1 - 1]);
-      }
-    }
-    __syncthreads();
-    const uint32_t cmin = s_min, cmax = s_max;
-    uint64_t tot = 0;
-    for (uint64_t wbl = cmin; cmin <= cmax && wbl <= (uint64_t)cmax; wbl += SW) {
-      const uint32_t wb = (uint32_t)wbl;
-      const uint32_t we = (uint32_t)min((uint64_t)cmax, wbl + SW - 1);
-      for (int q = t; q < SW / 4; q += NT) map[q] = 0;
-      __syncthreads();
-      for (uint64_t c0 = 0; c0 < nl; c0 += MAXL) {
-      const uint32_t nc = (uint32_t)min((uint64_t)MAXL, nl - c0);
-      if (chunked) {
-        for (uint32_t e = t; e < nc; e += NT) {
-          const uint32_t k = acol[a0 + c0 + e];
-          const uint64_t b0 = bro[k];
-          const uint32_t L = (uint32_t)(bro[k + 1] - b0);
-          uint32_t lo = 0, hi = L;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (bcol[b0 + mid] < wb) lo = mid + 1;
-            else hi = mid;
-          }
-          lbs[e] = b0;
-          lend[e] = L;
-          lcur[e] = lo;
-        }
-        __syncthreads();
-      }
-      // the layers with a column in this window (one peek per layer, all threads at
-      // once), then one wavefront walk per active layer: a wide row's layers mostly
-      // miss most windows, and a dependent load per missed layer per window was the
-      // kernel's cost
-      if (t == 0) s_nact = 0;
-      __syncthreads();
-      for (uint32_t e0 = 0; e0 < nc; e0 += NT) {      // uniform trip count (wave_append)
-        const uint32_t e = e0 + t;
-        bool act = false;
-        if (e < nc) {
-          const uint32_t c = lcur[e];
-          act = c < lend[e] && bcol[lbs[e] + c] <= we;
-        }
-        const unsigned p = wave_append(&s_nact, act);
-        if (act) lact[p] = (uint16_t)e;
-      }
-      __syncthreads();
-      const uint32_t na = s_nact;
-      for (uint32_t q = wv; q < na; q += NW) {
-        const uint32_t e = lact[q];
-        const uint64_t b0 = lbs[e];
-        const uint32_t L = lend[e];
-        uint32_t c = lcur[e];
-        while (c < L) {
-          // eight 64-column loads in flight per step (the layer is sorted: the in-window
-          // columns are a prefix; loads past it are wasted, not wrong)
-          uint32_t cc[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            const uint32_t j = c + 64 * u + lane;
-            cc[u] = j < L ? bcol[b0 + j] : 0xffffffffu;
-          }
-          uint32_t n = 0;
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            const bool in = cc[u] <= we;
-            if (in) mb[cc[u] - wb] = 1;
-            n += (uint32_t)__popcll(__ballot(in));
-          }
-          c += n;
-          if (n < 512) break;                // the layer left the window (or ended)
-        }
-        if (lane == 0) lcur[e] = c;
-      }
-      __syncthreads();
-      }
-      uint32_t n = 0;
-      for (int q = t; q < SW / 4; q += NT) n += __popc(map[q] & 0x01010101u);
-      atomicAdd(&s_tot, (unsigned long long)n);
-      __syncthreads();
-      tot = s_tot;
-      __syncthreads();
-    }
-    if (t == 0) cnt[i] = tot;
-    __syncthreads();
-  }
-}
-
 // Wave-private windowed SpGEMM (round 3).  k_sg_win shares one window accumulator
 // among the 256 threads of a work-group, so every layer (A entry k) costs a barrier
 // while typically only a few dozen of its B-row entries fall into the window.  Here
@@ -3310,45 +2335,21 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
-  const int wwin = kseq ? sg_wwin() : 0;
-  const int wflat = !kseq && (sg_wwin() & 128) ? sg_wwin() : 0;   // short-B-row hash bins
+  // wide symbolic rows of long-B-row products: wave-private 4096-column byte windows
+  // (k_sg_wwin MODE 0, round 3); their cursors live in `curs` (one per A entry)
   uint32_t *curs = nullptr;
-  if (wwin || wflat) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
+  if (kseq) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
   if (hc[1]) {
-    const int wsym = kseq ? sg_wsym() : 0;
-    if (wsym) amgd_route_hit(AMGD_R_SG_WSYM);
-    if ((wwin & 2) && (wwin & 32))
-      k_sg_wwin<2048, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
-          nullptr, curs);
-    else if ((wwin & 2) && (wwin & 16))
+    if (kseq) {
+      amgd_route_hit(AMGD_R_SG_WSYM);
       k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
           nullptr, curs);
-    else if (wwin & 2)
-      k_sg_wwin<16384, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
-          nullptr, curs);
-    else if (wsym == 8192)
-      k_sg_wsym<8192><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
-    else if (wsym == 16384)
-      k_sg_wsym<16384><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
-    else if (wsym == 32768)
-      k_sg_wsym<32768><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
-    else if (wsym == 65536)
-      k_sg_wsym<65536><<<(int)std::min<unsigned>(hc[1], 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, B->ro, B->col, cnt);
-    else if (kseq)
-      k_sg_kseq<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
-          nullptr);
-    else
+    } else {
       k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
           nullptr);
+    }
   }
   KCHECK();
   // numeric bins by distinct count: wave/512, wave/2048, wave/4096, block/8192 slots, dense slab
@@ -3424,16 +2425,6 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     hn[3] = wn[1];
     hn[4] = wn[3];
   }
-#define SG_WT(W_, T_, R_)                                                                         \
-  do {                                                                                          \
-    const int gt = (int)std::min<unsigned>((nrw + T_ - 1) / T_, 16384u);                       \
-    if (rap)                                                                                    \
-      k_sg_wt<W_, T_, 1><<<gt, 256, 0, s>>>(R_, nrw,    A->ro, A->col, A->a, B->ro, B->col,     \
-                                            B->a, cnt2, cnt, tcol, ta);                         \
-    else                                                                                        \
-      k_sg_wt<W_, T_, 0><<<gt, 256, 0, s>>>(R_, nrw,    A->ro, A->col, A->a, B->ro, B->col,     \
-                                            B->a, cnt2, cnt, tcol, ta);                         \
-  } while (0)
 #define SG_WW(W_, rows_, nrw)                                                                   \
   do {                                                                                          \
     const int gw = (int)std::min<unsigned>((nrw + 3) / 4, 16384u);                              \
@@ -3444,49 +2435,6 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_wwin<W_, 1, 0><<<gw, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,     \
                                              B->a, cnt2, cnt, tcol, ta, curs);                  \
   } while (0)
-#define SG_WIN(nr, rows_)                                                                       \
-  if (nr) {                                                                                     \
-    const unsigned nrw = (nr);                                                                  \
-    const int g = (int)std::min<unsigned>(nrw, 16384u);                                         \
-    const int wt = sg_wt();                                                                     \
-    if ((wwin & 1) && (wwin & 64)) SG_WW(512, rows_, nrw);                                      \
-    else if ((wwin & 1) && (wwin & 8)) SG_WW(1024, rows_, nrw);                                 \
-    else if (wwin & 1) SG_WW(2048, rows_, nrw);                                                 \
-    else if (wt == 4 && win == 2048) SG_WT(2048, 4, rows_);                                         \
-    else if (wt == 8 && win == 2048) SG_WT(2048, 8, rows_);                                         \
-    else if (wt == 4 && win == 1024) SG_WT(1024, 4, rows_);                                         \
-    else if (wt == 8 && win == 1024) SG_WT(1024, 8, rows_);                                         \
-    else if (win == 1024 && rap)                                                                \
-      k_sg_win<1024, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 1024)                                                                       \
-      k_sg_win<1024, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 2048 && rap)                                                                \
-      k_sg_win<2048, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 2048)                                                                       \
-      k_sg_win<2048, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 4096 && rap)                                                                \
-      k_sg_win<4096, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 4096)                                                                       \
-      k_sg_win<4096, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 8192 && rap)                                                                \
-      k_sg_win<8192, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (win == 8192)                                                                       \
-      k_sg_win<8192, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,   \
-                                          B->a, cnt2, cnt, tcol, ta);                           \
-    else if (rap)                                                                               \
-      k_sg_win<16384, 1><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
-                                           B->a, cnt2, cnt, tcol, ta);                          \
-    else                                                                                        \
-      k_sg_win<16384, 0><<<g, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,  \
-                                           B->a, cnt2, cnt, tcol, ta);                          \
-  }
   // threads per row of the 4096- / 8192-slot k-sequential kernels (AMGD_SG_NT2 / _NT3):
   // one row per work-group walks its layers one dependent step at a time, so more
   // wavefronts per table keep more of each layer's loads in flight (256^3: RAP
@@ -3497,17 +2445,6 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (hn[0] || hn[1] || hn[2] || hn[3]) amgd_route_hit(kseq ? AMGD_R_SG_KSEQ : AMGD_R_SG_ROW);
   if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WIN);
   if (hn[4]) amgd_route_hit(AMGD_R_SG_LONG);
-  unsigned ww_launches = 0;
-  if (kseq && (wwin & 4)) {      // the 4096- / 8192-slot hash bins through k_sg_wwin
-    for (int q = 2; q < 4; q++) {
-      const unsigned nb = hn[q];
-      if (!nb) continue;
-      ww_launches++;
-      if (wwin & 8) SG_WW(1024, lists + q * L, nb);
-      else SG_WW(2048, lists + q * L, nb);
-      hn[q] = 0;
-    }
-  }
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
@@ -3527,25 +2464,15 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
     else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
   } else {
-    if (wflat) {                 // AMGD_SG_WWIN bit 128: bins 1-3 through k_sg_wwin (1024 columns)
-      for (int q = 1; q < 4; q++) {
-        const unsigned nb = hn[q];
-        if (!nb) continue;
-        ww_launches++;
-        SG_WW(1024, lists + q * L, nb);
-        hn[q] = 0;
-      }
-    }
     SG_NUM(k_sg_row, 64, 9, 0, 65536u)
     SG_NUM(k_sg_row, 64, 11, 1, 65536u)
     SG_NUM(k_sg_row, 64, 12, 2, 65536u)
     SG_NUM(k_sg_row, 256, 13, 3, 8192u)
   }
 #undef SG_NUM
-  if (win) {
-    SG_WIN(wn[0], wlists)
-    SG_WIN(wn[2], wlists + L)
-  }
+  // windowed rows: wave-private 1024-column windows (k_sg_wwin, round 3)
+  if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
+  if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
   if (hn[4]) {
     if (rap)
       k_spgemm_long<1, 1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,
@@ -3554,8 +2481,6 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_spgemm_long<1, 0><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,
                                                B->a, B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);
   }
-#undef SG_WIN
-#undef SG_WT
 #undef SG_WW
   KCHECK();
   if (g_sg_slot >= 0) amgd_timer_stop(g_sg_slot);
@@ -3564,7 +2489,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     g_sg_bytes += 12 * (A->nnz + B->nnz + nz) + 8 * ((uint64_t)A->rn + B->rn + rn + 3);
     // launches of the RAP-instantiated numeric kernels (the rocprof regex of tools/gpurun_pmc.sh)
     for (int q = 0; q < 4; q++) g_sg_launches += hn[q] ? 1 : 0;
-    g_sg_launches += (hn[4] ? 1 : 0) + (win ? (wn[0] ? 1 : 0) + (wn[2] ? 1 : 0) : 0) + ww_launches;
+    g_sg_launches += (hn[4] ? 1 : 0) + (win ? (wn[0] ? 1 : 0) + (wn[2] ? 1 : 0) : 0);
   }
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = rn; X->cn = B->cn; X->nnz = nz;

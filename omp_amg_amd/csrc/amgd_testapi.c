@@ -175,9 +175,6 @@ API void amgd_test_qf_stats(uint64_t *out) {
 
 /* whole-matrix SpMVs that ran row-sharded (multi-GPU) since the library loaded */
 extern uint64_t amgd_spmv_shard_calls(void);
-void amgd_spgemm_set_wt(int t);
-/* rows per tile of the tiled windowed SpGEMM (4, 8; 0: one row per work-group; -1: default) */
-API void amgd_test_spgemm_wt(int t) { amgd_spgemm_set_wt(t); }
 /* cols_masked(A, mask) and transpose(rows_masked(B, mask)) for the same mask: equal */
 API int amgd_test_cols_masked(const hcsr *HA, const uint8_t *hmask, hcsr *HX) {
   if (amgd_rt_init(0) != 0) return -1;
@@ -192,19 +189,9 @@ API int amgd_test_cols_masked(const hcsr *HA, const uint8_t *hmask, hcsr *HX) {
 }
 void amgd_qfactor_set_reuse(int on);
 API void amgd_test_qf_reuse(int on) { amgd_qfactor_set_reuse(on); }
-void amgd_spmv_set_chunk(int on);
-API void amgd_test_spmv_chunk(int on) { amgd_spmv_set_chunk(on); }
 void amgd_lmop_set_small(int n);
 API void amgd_test_lmop_small(int n) { amgd_lmop_set_small(n); }
-void amgd_spmv_set_sum2(int on);
-API void amgd_test_spmv_sum2(int on) { amgd_spmv_set_sum2(on); }
-void amgd_spmv_set_pipe(int on);
-API void amgd_test_spmv_pipe(int on) { amgd_spmv_set_pipe(on); }
-void amgd_spmv_set_fused(int on);
-API void amgd_test_fs_fused(int on) { amgd_spmv_set_fused(on); }
 void amgd_lmop_set_wave(int n);
-void amgd_qfactor_set_colc(int on);
-API void amgd_test_qf_colc(int on) { amgd_qfactor_set_colc(on); }
 API void amgd_test_lmop_wave(int n) { amgd_lmop_set_wave(n); }
 void amgd_spgemm_set_pattern(int on);
 API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }
@@ -244,14 +231,10 @@ API void amgd_test_mv_long(int64_t n) { amgd_spmv_set_long(n); }
 API void amgd_test_fs_long(int64_t n) { amgd_fs_set_long(n); }
 extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
-/* window of the dense-accumulator numeric kernel for wide rows: 0 (hash kernels), 8192, 16384 */
+/* windowed (k_sg_wwin) routing of wide rows: 0 = hash kernels only; > 0 = every wide row windowed
+   (routing width 1024..16384); -1 = default (2048, rows with >= 48 products per window) */
 extern void amgd_spgemm_set_win(int w);
 API void amgd_test_spgemm_win(int w) { amgd_spgemm_set_win(w); }
-/* symbolic pass of rows with many products: 0 (LDS hash), 32768 / 65536 (byte-map windows) */
-extern void amgd_spgemm_set_wsym(int w);
-API void amgd_test_spgemm_wsym(int w) { amgd_spgemm_set_wsym(w); }
-extern void amgd_spgemm_set_wwin(int m);
-API void amgd_test_spgemm_wwin(int m) { amgd_spgemm_set_wwin(m); }
 /* SpMV: row count from which the lane-per-row kernel runs, for whole-matrix and
    listed-row products alike (0 = always, -1 = environment / default) */
 extern void amgd_spmv_set_sl_min(int64_t n);

@@ -48,6 +48,8 @@ ORA_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
 CASES = {
     "p7_48": ("oracle", {"kind": "poisson3d", "m": 48}),
     "p7_64": ("oracle", {"kind": "poisson3d", "m": 64}),
+    "p7_96": ("oracle", {"kind": "poisson3d", "m": 96}),
+    "p7_128": ("oracle", {"kind": "poisson3d", "m": 128}),
     "aniso_20": ("oracle", {"kind": "poisson3d", "m": 20, "eps": 1e-3}),
     "aniso_24": ("oracle", {"kind": "poisson3d", "m": 24, "eps": 1e-3}),
     "aniso_32": ("oracle", {"kind": "poisson3d", "m": 32, "eps": 1e-3}),

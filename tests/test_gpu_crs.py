@@ -119,3 +119,51 @@ def test_out_of_hbm_returns_error_and_recovers():
     bad = parity.compare(parity.from_npz(z), ds.export(), exact=True)
     ds.close()
     assert not bad, bad
+
+
+@pytest.mark.parametrize("frac", [0.25, 0.5, 0.75, 0.9])
+@pytest.mark.parametrize("gen", [("p7_24", lambda: problems.poisson3d(24)),
+                                 ("p27_12", lambda: problems.poisson3d(12, 27))],
+                         ids=lambda g: g[0])
+def test_out_of_hbm_mid_setup_recovers(gen, frac):
+    """the HBM cap set to a fraction of the setup's measured peak, so the failure lands
+    deep inside the setup (interpolation's products, Q factors with reuse, the pattern-only
+    constraint product, RAP) rather than at its first allocation: -2 with the reason, every
+    block released (pool in use back to its value before), and the next setup bit-exact
+    with an uncapped one (per-call state -- SpGEMM pattern mode, Q-factor reuse
+    pointers -- is reset after the unwind)"""
+    import ctypes as C
+    oa.init()
+    L = oa.lib()
+    L.amgd_test_hbm_cap.argtypes = [C.c_uint64]
+    L.amgd_test_pool_inuse.restype = C.c_uint64
+    Ai, Aj, Av = gen[1]()
+    ds = oa.DeviceSetup(Ai, Aj, Av)
+    try:
+        ds.run()
+        ref = ds.export()
+        peak = oa.stats()["peak_bytes"]          # this setup's peak (reset at its start)
+        L.amgd_hier_free(C.byref(ds.h))
+        before = L.amgd_test_pool_inuse()
+        assert peak > before
+        L.amgd_test_hbm_cap(before + int((peak - before) * frac))
+        with pytest.raises(RuntimeError, match="out of HBM"):
+            ds.run()
+        L.amgd_test_hbm_cap(0)
+        assert L.amgd_test_pool_inuse() == before
+        ds.run()
+        bad = parity.compare(ref, ds.export(), exact=True)
+        assert not bad, bad
+    finally:
+        L.amgd_test_hbm_cap(0)
+        ds.close()
+
+
+def test_crs_setup_rejects_bad_local_index():
+    """a local index >= n: NULL with the reason in amgd_error(), not a silent drop"""
+    oa.init()
+    Ai = CRS_I.copy()
+    Ai[5] = 4
+    hd = abi.crs_setup(oa.lib(), 4, [1, 2, 3, 4], Ai, CRS_J, CRS_A)
+    assert hd is None
+    assert b"local index" in oa.lib().amgd_error()

@@ -39,8 +39,11 @@ def _mk():
 EXPECT_ROUTES = {
     "p7_48": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
     "p7_64": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
+    "p7_96": ("cs_inc", "fs_inc", "spmv_lane", "mv_rw16", "mv_long", "sg_tiny", "sg_win", "sg_wsym",
+              "qf_reuse"),
+    "p7_128": ("cs_inc", "fs_inc", "spmv_lane", "mv_rw16", "mv_long", "sg_tiny", "sg_win", "sg_wsym",
+               "qf_reuse"),
     "aniso_20": ("fs_inc", "mv_long"),
-    "aniso_24": ("fs_inc",),
     "aniso_32": ("fs_inc", "spmv_lane"),
     "p27_20": ("fs_inc", "spmv_lane", "sg_win", "sg_wsym"),
     "sem_e3_N7": ("spmv_lane", "sg_wsym"),

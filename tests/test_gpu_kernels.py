@@ -142,52 +142,17 @@ def _banded(rng, rn, kn, cn, width, dens, blen, span, ints=True, dups=False, emp
     return A, B
 
 
-@pytest.mark.parametrize("wt", [0, 4, 8])
-@pytest.mark.parametrize("win", [1024, 2048])
-@pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span"])
-def test_spgemm_tiled_windows(case, win, wt):
-    """tiled windowed kernel (k_sg_wt: T = 4 / 8 rows per work-group walking the union of
-    their A rows in ascending k) vs the one-row kernel (wt 0) vs the host restatement:
-    overlapping neighbouring rows, A rows past one chunk (several unions per window),
-    duplicate A columns, exact cancellation, empty rows inside tiles, a row count that
-    leaves a partial last tile, outputs spanning many windows"""
-    rng = np.random.default_rng({"banded": 61, "long_a": 62, "dups_cancel": 63, "ragged": 64,
-                                 "wide_span": 65}[case])
-    if case == "banded":
-        A, B = _banded(rng, 301, 400, 6000, 60, 0.7, 150, 3000, ints=False)
-    elif case == "long_a":
-        A, B = _banded(rng, 70, 900, 8000, 400, 0.8, 100, 4000)
-    elif case == "dups_cancel":
-        A, B = _banded(rng, 157, 300, 5000, 50, 0.8, 160, 2500, dups=True)
-    elif case == "ragged":
-        A, B = _banded(rng, 203, 350, 7000, 90, 0.6, 120, 3500, empty_every=5)
-    else:
-        A, B = _banded(rng, 41, 500, 60000, 200, 0.7, 90, 30000)
-    assert B.a.size >= 64 * B.rn
-    R = refops.spgemm(A, B)
-    oa.spgemm_flat(False)
-    oa.spgemm_win(win)
-    oa.spgemm_wt(wt)
-    oa.route_stats(reset=True)
-    try:
-        X = oa.test_csr_op(0, A, B)
-    finally:
-        oa.spgemm_win(-1)
-        oa.spgemm_wt(-1)
-    assert oa.route_stats(reset=True)["sg_win"] > 0
-    assert refops.same(X, R)
-
-
-@pytest.mark.parametrize("wwin", [1 | 2 | 4, 1 | 2 | 4 | 8, 1 | 2 | 16, 1 | 2 | 32 | 64])
+@pytest.mark.parametrize("win", [0, 1024, 2048, 8192, -1])
 @pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
                                   "huge_a", "gapped", "dense_rows"])
-def test_spgemm_wave_windows(case, wwin):
+def test_spgemm_wave_windows(case, win):
     """wave-private windowed kernel (k_sg_wwin: one wavefront per row, its own LDS window,
-    no barrier per layer) for the symbolic counts (2) and the numeric rows of both the
-    windowed (1) and the 4096- / 8192-slot hash bins (4), windows of 2048 or 1024 (8)
-    columns: vs the host restatement, bit for bit -- rows of more than 64 layers (cursors
-    in scratch), duplicate A columns, exact cancellation, empty rows, column clusters far
-    apart (skipped windows), B-row runs past 64 entries inside one window"""
+    no barrier per layer; 4096-column byte windows for the symbolic counts, 1024-column
+    numeric windows) with every wide row routed to it (win > 0, at several routing
+    widths), none (0: LDS hash kernels) or the default routing (-1): vs the host
+    restatement, bit for bit -- rows of more than 64 layers (cursors in scratch),
+    duplicate A columns, exact cancellation, empty rows, column clusters far apart
+    (skipped windows), B-row runs past 64 entries inside one window"""
     rng = np.random.default_rng({"banded": 91, "long_a": 92, "dups_cancel": 93, "ragged": 94,
                                  "wide_span": 95, "huge_a": 96, "gapped": 97, "dense_rows": 98}[case])
     if case == "banded":
@@ -214,38 +179,17 @@ def test_spgemm_wave_windows(case, wwin):
     assert B.a.size >= 64 * B.rn
     R = refops.spgemm(A, B)
     oa.spgemm_flat(False)
-    oa.spgemm_win(2048)
-    oa.spgemm_wwin(wwin)
+    oa.spgemm_win(win)
     oa.route_stats(reset=True)
     try:
         X = oa.test_csr_op(0, A, B)
     finally:
         oa.spgemm_win(-1)
-        oa.spgemm_wwin(-1)
-    assert refops.same(X, R)
-
-
-@pytest.mark.parametrize("case", ["mid", "wide", "dups", "spread"])
-def test_spgemm_wave_windows_short_b(case):
-    """short B rows (flat products) through k_sg_wwin (AMGD_SG_WWIN bit 128: the hash bins
-    1-3 of k_sg_row): bit for bit the host restatement"""
-    rng = np.random.default_rng({"mid": 101, "wide": 102, "dups": 103, "spread": 104}[case])
-    if case == "mid":
-        A, B = refops.rand_csr(rng, 500, 400, 0.05), refops.rand_csr(rng, 400, 3000, 0.01)
-    elif case == "wide":
-        A, B = refops.rand_csr(rng, 80, 2000, 0.05), refops.rand_csr(rng, 2000, 50000, 0.0008)
-    elif case == "dups":
-        A, B = _banded(rng, 157, 300, 5000, 80, 0.8, 30, 2500, dups=True)
-    else:
-        A, B = refops.rand_csr(rng, 60, 3000, 0.05, ints=True), refops.rand_csr(rng, 3000, 900000, 0.00002, ints=True)
-    assert B.a.size < 64 * B.rn
-    R = refops.spgemm(A, B)
-    oa.spgemm_flat(False)
-    oa.spgemm_wwin(27 | 128)
-    try:
-        X = oa.test_csr_op(0, A, B)
-    finally:
-        oa.spgemm_wwin(-1)
+    routes = oa.route_stats(reset=True)
+    if win > 0:
+        assert routes["sg_win"] > 0
+    if win == 0:
+        assert routes["sg_win"] == 0
     assert refops.same(X, R)
 
 
@@ -438,16 +382,11 @@ def rw(request):
     oa.spmv_rw(-1)
 
 
-@pytest.fixture(params=[2, 0, 3], ids=["chunk", "segments", "pipe"])
+@pytest.fixture(params=[3], ids=["pipe"])
 def chunk(request):
-    """whole-matrix long-row products: contiguous 16-byte-load chunks (k_spmv_chunk, at
-    every row length), per-row segments (k_spmv_lane) or per-row segments with the gather
-    one round ahead (k_spmv_pipe, whole-matrix and listed rows)"""
-    oa.spmv_chunk(0 if request.param == 3 else request.param)
-    oa.spmv_pipe(11 if request.param == 3 else 0)
+    """whole-matrix long-row products: per-row segments with the gather one round ahead
+    (k_spmv_pipe, whole-matrix and listed rows) -- the one long-row kernel since round 4"""
     yield request.param
-    oa.spmv_chunk(-1)
-    oa.spmv_pipe(-1)
 
 
 def _adversarial_rows(rng, rn=700):
@@ -863,19 +802,19 @@ def test_qfactor_split_bitexact(structure, mode):
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))
 
 
-@pytest.mark.parametrize("colc", [1, 0], ids=["colc", "rows"])
 @pytest.mark.parametrize("structure,split", [("tiers", 0), ("blocks", 1)])
-def test_qfactor_colc_bitexact(structure, split, colc):
-    """the blocked tiers (256 / 512 / 1024 points) with the s2 pass over a column-packed
-    copy of U (and over U itself), bit for bit the oracle"""
+def test_qfactor_blocked_tiers_bitexact(structure, split):
+    """the blocked tiers (256 / 512 / 1024 points), bit for bit the oracle"""
     W, A = _qfactor_case(structure)
-    oa.qf_colc(colc)
     oa.qf_split(split)
+    oa.route_stats(reset=True)
     try:
         X = oa.test_csr_op(5, W, A)
     finally:
-        oa.qf_colc(-1)
         oa.qf_split(-1)
+    if structure == "tiers":
+        r = oa.route_stats(reset=True)
+        assert r["qf_t512"] > 0 and r["qf_t1024"] > 0, r
     ref = _oracle_qfactor(W, A)
     assert X.nnz == len(ref)
     assert np.array_equal(X.a.view(np.uint64), ref.view(np.uint64))

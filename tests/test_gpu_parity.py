@@ -268,53 +268,24 @@ def test_gpu_qfactor_reuse_matches_refactor(gen):
 
 
 @pytest.mark.parametrize("gen", [("p7_32", lambda: problems.poisson3d(32)),
+                                 ("aniso_16", lambda: problems.poisson3d(16, eps=1e-3)),
                                  ("p27_16", lambda: problems.poisson3d(16, 27)),
                                  ("sem_e4_N4", lambda: problems.sem_laplacian(4, 4, 4, 4, seed=5, jitter=0.3))],
                          ids=lambda g: g[0])
-@pytest.mark.parametrize("pipe", [0, 11], ids=["lane", "pipe"])
-def test_gpu_fs_fused_select_matches_separate(gen, pipe):
-    """find_support's selection from the argmax kept by the fused w = R' rs product vs
-    the separate selection pass (and the lane path forced at every size; k_spmv_lane or
-    k_spmv_pipe): identical hierarchies, and the fused path is taken"""
-    Ai, Aj, Av = gen[1]()
-    oa.spmv_sl_min(0)
-    oa.spmv_pipe(pipe)
-    try:
-        oa.fs_fused(1)
-        oa.route_stats(reset=True)
-        h_f = abi.run_setup(oa.lib(), Ai, Aj, Av)
-        assert oa.route_stats(reset=True)["fs_fused"] > 0
-        oa.fs_fused(0)
-        h_s = abi.run_setup(oa.lib(), Ai, Aj, Av)
-    finally:
-        oa.fs_fused(-1)
-        oa.spmv_sl_min(-1)
-        oa.spmv_pipe(-1)
-    bad = parity.compare(h_s, h_f, exact=True)
-    assert not bad, bad
-
-
-@pytest.mark.parametrize("gen", [("p7_32", lambda: problems.poisson3d(32)),
-                                 ("aniso_16", lambda: problems.poisson3d(16, eps=1e-3)),
-                                 ("sem_e4_N4", lambda: problems.sem_laplacian(4, 4, 4, 4, seed=5, jitter=0.3))],
-                         ids=lambda g: g[0])
 @pytest.mark.parametrize("inc", ["1", "0", "2"], ids=["inc_default", "inc_off", "inc_all"])
-def test_gpu_fs_sum2_matches_separate(gen, inc, monkeypatch):
-    """find_support's column sums re-summed inside the full sweeps' w = R' rs pass
-    (k_spmv_pipe SUM2, the selection's own column re-sum skipped when the next sweep is
-    certainly full) vs re-summed after every selection: identical hierarchies, with the
-    lane path forced at every size and incremental sweeps at their default / off / at
-    every size"""
+def test_gpu_lane_spmv_forced_matches_default(gen, inc, monkeypatch):
+    """the long-row pipelined SpMV (k_spmv_pipe) forced at every size, with find_support's
+    incremental sweeps at their default / off / at every size, vs the default routing:
+    identical hierarchies"""
     Ai, Aj, Av = gen[1]()
     monkeypatch.setenv("AMGD_FS_INC", inc)
+    h_d = abi.run_setup(oa.lib(), Ai, Aj, Av)
     oa.spmv_sl_min(0)
     try:
-        oa.spmv_sum2(1)
+        oa.route_stats(reset=True)
         h_f = abi.run_setup(oa.lib(), Ai, Aj, Av)
-        oa.spmv_sum2(0)
-        h_s = abi.run_setup(oa.lib(), Ai, Aj, Av)
+        assert oa.route_stats(reset=True)["spmv_lane"] > 0
     finally:
-        oa.spmv_sum2(-1)
         oa.spmv_sl_min(-1)
-    bad = parity.compare(h_s, h_f, exact=True)
+    bad = parity.compare(h_d, h_f, exact=True)
     assert not bad, bad

@@ -21,9 +21,8 @@ import numpy as np  # noqa: E402
 import omp_amg_amd as oa  # noqa: E402
 from omp_amg_amd import parity, problems  # noqa: E402
 
-HOOKS = {"wt": oa.spgemm_wt, "win": oa.spgemm_win, "wsym": oa.spgemm_wsym, "rw": oa.spmv_rw,
-         "qfr": oa.qf_reuse, "pat": oa.sg_pattern, "fused": oa.fs_fused,
-         "chunk": oa.spmv_chunk, "lw": oa.lmop_wave, "colc": oa.qf_colc, "ww": oa.spgemm_wwin, "pipe": oa.spmv_pipe, "lsm": oa.lmop_small, "sum2": oa.spmv_sum2}
+HOOKS = {"win": oa.spgemm_win, "rw": oa.spmv_rw, "qfr": oa.qf_reuse, "pat": oa.sg_pattern,
+         "lw": oa.lmop_wave, "lsm": oa.lmop_small}
 
 
 def digest(h):

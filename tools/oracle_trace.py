@@ -5,7 +5,7 @@ problem, with a wall-clock stamp per line.
 
 The oracle prints, per interpolation iteration, " <nnz(W_skel)> nzs, <n> cols > gamma,
 worst = <sqrt(max r)>" (ORACLE_VERBOSE, oracle/amg_oracle.c, the reference's own
-printout at amg_setup.c:717); the GPU library prints the same line under
+printout at amg_setup.c:803); the GPU library prints the same line under
 AMGD_VERBOSE=1 (amgd_setup.c interpolation()).  tools/trace_diff.py compares the two.
 
 usage: python tools/oracle_trace.py <stencil> <m> <out.txt> [--eps E] [--timeout S] [--lib SO]

@@ -16,8 +16,6 @@ L.amgd_test_spmv_bench.restype = C.c_double
 shapes = [(187960, 508253, 2070), (696213, 1847299, 715), (10661, 37121, 8442),
           (47782, 140178, 4751), (5842783, 5842783, 130), (1692, 8969, 6501)]
 kernels = [("wave", 1 << 40, -1), ("rw4", 0, 4), ("rw16", 0, 16), ("rw64", 0, 64)]
-if "--chunk" in sys.argv:       # k_spmv_lane (segments) vs k_spmv_chunk (16-byte chunks), each RW
-    kernels = [(f"{k}{r}", 0, r) for r in (4, 16, 64) for k in ("seg", "chk")]
 for rn, cn, mean in shapes:
     for gapname in ("contig", "spread"):
         gap = 1 if gapname == "contig" else max(1, (cn // 2) // mean)
@@ -26,8 +24,6 @@ for rn, cn, mean in shapes:
             for kname, slm, rw in kernels:
                 oa.spmv_sl_min(slm)
                 oa.spmv_rw(rw)
-                if kname.startswith(("seg", "chk")):
-                    oa.spmv_chunk(1 if kname.startswith("chk") else 0)
                 nnz = C.c_uint64()
                 ms = L.amgd_test_spmv_bench(rn, cn, mean // 2, mean * 3 // 2, gap, with_x, 5, C.byref(nnz))
                 gbs = nnz.value * (12 + 8 * with_x) / (ms * 1e6)
@@ -36,4 +32,3 @@ for rn, cn, mean in shapes:
                   + " | ".join(cells), flush=True)
 oa.spmv_sl_min(-1)
 oa.spmv_rw(-1)
-oa.spmv_chunk(-1)
