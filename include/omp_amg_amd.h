@@ -75,6 +75,18 @@ int amgd_comm_init_sim(int nshards);   /* one process computes all shards in tur
 void amgd_comm_free(void);             /* back to one GPU */
 int amgd_comm_size(void);
 int amgd_comm_rank(void);
+/* Partitioned mode (the north_star layout): with a multi-process
+   communicator (RCCL or host), amgd_setup_device takes each rank's OWN entries (global
+   indices; every rank's entries together are the matrix, duplicates summed in rank order),
+   routes them to the owners of their rows (contiguous equal row blocks of level 0, every
+   coarser level inheriting the owners), and builds a hierarchy of which each rank holds
+   only its row blocks: rows of A, Af, W and AfP of every level and of every intermediate;
+   products fetch the halo rows they reference, transposes exchange row pieces, vectors
+   stay whole.  amgd_hier_export gathers the whole hierarchy to every rank (bit-identical
+   to the one-GPU hierarchy); crs_setup with np > 1 passes the local entries through.
+   amgd_comm_set_partitioned(1) after amgd_comm_init_*; amgd_comm_free resets it. */
+void amgd_comm_set_partitioned(int on);
+int amgd_comm_partitioned(void);
 /* scale of the per-op minimum work below which an op runs unsharded (1 = default, 0 = always shard) */
 void amgd_comm_set_min_work(double scale);
 void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms);

@@ -66,6 +66,7 @@ void amgd_timer_start(int slot);
 void amgd_timer_stop(int slot);
 double amgd_timer_ms(int slot);          /* accumulated, syncs */
 void amgd_timer_reset(void);
+void amgd_spgemm_set_timer(int slot);     /* SpGEMM numeric kernels timed on slot (-1: off) */
 
 dcsr *dcsr_new(uint32_t rn, uint32_t cn, uint64_t nnz);
 void dcsr_free(dcsr **A);
@@ -98,6 +99,15 @@ void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h);
 void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off);
 void amgd_allgather_u64(uint64_t *vals_h);       /* vals_h[s] of the own shards -> all */
 void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_t *out_h);
+
+/* partitioned mode (amgd_psetup.c): ranks own row blocks; amgd_nshards() is 1 there */
+int amgd_comm_partitioned(void);
+void amgd_comm_suspend_partition(int on);
+int amgd_pcomm_rank(void);
+int amgd_pcomm_size(void);
+void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m);   /* vals_h[N*m]: own m -> all */
+/* rank sends send[soff[p]..soff[p+1]) to p, receives p's into recv[roff[p]..roff[p+1]) (bytes) */
+void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff);
 
 /* ---------------- reductions (return host values, sync) ---------------- */
 void amgd_set_exact(int on);     /* 1: reference-order (sequential) dots -- default; 0: tree */
@@ -224,8 +234,8 @@ void amgd_qfactor_reuse_stats(uint64_t *reused, uint64_t *factored);
 void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qoff, const dcsr *Bt,
                  const double *u, const double *lambda, double *out);
 /* S := interp_lmop contributions (S pattern = W_skel*W_skel'); kpos from amgd_lmop_kpos */
-void amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt, const double *Q,
-               const uint64_t *qoff, const double *u);
+int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt, const double *Q,
+              const uint64_t *qoff, const double *u);
 uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm);
 void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses, pruned supports */
 void amgd_lmop_stats_reset(void);
@@ -237,6 +247,11 @@ void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] s
 uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                         const double *w, double *sumR, double thr,
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
+/* the same over rows c0.. of R' (w, sumR at c0; sel_j global); perm NULL: R untouched;
+   resum 0: rs / sumR not re-summed (partitioned mode) */
+uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
+                           const double *w, double *sumR, double thr, uint32_t *sel_i,
+                           uint32_t *sel_j, uint32_t *nremoved, uint32_t c0, int resum);
 /* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
    returns the count, > cap when the list overflowed */
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,

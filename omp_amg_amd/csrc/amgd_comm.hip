@@ -40,6 +40,10 @@
 
 enum { COMM_NONE = 0, COMM_RCCL = 1, COMM_HOST = 2, COMM_SIM = 3 };
 static int g_kind = COMM_NONE, g_rank = 0, g_size = 1;
+// partitioned mode (amgd_psetup.c): the ranks own row blocks of every matrix; the
+// replicated-hierarchy sharding of the kernels below is switched off (amgd_nshards() = 1)
+// and the partitioned ops exchange rows / vectors through amgd_pcomm_* directly
+static int g_part = 0, g_part_susp = 0;
 static amgd_allgatherv_fn g_cb = nullptr;
 static void *g_user = nullptr;
 static double g_min_scale = 1.0;      // work thresholds x this (0: shard everything)
@@ -143,11 +147,14 @@ extern "C" API void amgd_comm_free(void) {
   g_kind = COMM_NONE;
   g_rank = 0;
   g_size = 1;
+  g_part = 0;
   g_cb = nullptr;
   g_user = nullptr;
 }
 
 extern "C" API int amgd_comm_size(void) { return g_size; }
+extern "C" API void amgd_comm_set_partitioned(int on) { g_part = on ? 1 : 0; }
+extern "C" API int amgd_comm_partitioned(void) { return g_part && !g_part_susp && g_kind != COMM_SIM; }
 extern "C" API int amgd_comm_rank(void) { return g_rank; }
 extern "C" API void amgd_comm_set_min_work(double scale) { g_min_scale = scale < 0 ? 1.0 : scale; }
 extern "C" API void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms) {
@@ -158,7 +165,10 @@ extern "C" API void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms
 extern "C" API void amgd_comm_stats_reset(void) { g_calls = g_bytes = 0; g_ms = 0; }
 
 // ---- internal API (amgd.h) ----
-int amgd_nshards(void) { return g_kind == COMM_NONE ? 1 : g_size; }
+int amgd_nshards(void) { return g_kind == COMM_NONE || g_part ? 1 : g_size; }
+// a partitioned setup running one operation on gathered (whole) data on every rank:
+// the kernels see neither partitioning nor sharding meanwhile
+void amgd_comm_suspend_partition(int on) { g_part_susp = on ? 1 : 0; }
 int amgd_comm_procs(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? g_size : 1; }
 void amgd_my_shards(int *first, int *last) {
   if (g_kind == COMM_SIM) { *first = 0; *last = g_size; }
@@ -263,4 +273,106 @@ void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_
   amgd_d2h(out_h, dv, 8 * (size_t)n);
   amgd_free(di);
   amgd_free(dv);
+}
+
+// ---------------------------------------------------------------------------
+// Partitioned-mode collectives (amgd_part.hip / amgd_psetup.c): every process is one
+// rank (sim is not a partitioned transport).  Ranks own contiguous row blocks, so these
+// move rows and vector segments, never whole matrices.
+// ---------------------------------------------------------------------------
+int amgd_pcomm_rank(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? g_rank : 0; }
+int amgd_pcomm_size(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? g_size : 1; }
+
+// vals_h[N * rank .. N * rank + m) of this rank -> every rank (m u64 per rank)
+void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m) {
+  const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  if (N == 1) return;
+  uint64_t *d = (uint64_t *)amgd_alloc(8ull * N * m + 8);
+  amgd_h2d(d + (size_t)me * m, vals_h + (size_t)me * m, 8ull * m);
+  std::vector<uint64_t> off(N + 1);
+  for (int s = 0; s <= N; s++) off[s] = 8ull * s * m;
+  void *b = d;
+  amgd_allgatherv(1, &b, off.data());
+  amgd_d2h(vals_h, d, 8ull * N * m);
+  amgd_free(d);
+}
+
+// Personalised exchange: this rank sends bytes [soff[p], soff[p+1]) of `send` to rank p
+// and receives rank p's bytes for it into [roff[p], roff[p+1]) of `recv` (the counts of
+// both sides must agree: callers exchange counts first).  RCCL: one group of send/recv
+// pairs with every peer (each xGMI link carries its own pair).  Host transport: staged
+// through the allgatherv callback (every rank sees every send buffer; tests only).
+void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+  const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  const uint64_t own = soff[me + 1] - soff[me];
+  if (own) HIPCK(hipMemcpyAsync((char *)recv + roff[me], (const char *)send + soff[me], own,
+                                hipMemcpyDeviceToDevice, amgd_s()));
+  if (N == 1) return;
+  double t0 = amgd_wtime();
+  g_calls++;
+  if (g_kind == COMM_RCCL) {
+    hipStream_t s = amgd_s();
+    NCCK(R.GroupStart());
+    for (int p = 0; p < N; p++) {
+      if (p == me) continue;
+      const uint64_t sl = soff[p + 1] - soff[p], rl = roff[p + 1] - roff[p];
+      if (sl) NCCK(R.Send((const char *)send + soff[p], sl, ncclChar, p, g_nc, s));
+      if (rl) NCCK(R.Recv((char *)recv + roff[p], rl, ncclChar, p, g_nc, s));
+      g_bytes += rl;
+    }
+    NCCK(R.GroupEnd());
+    amgd_sync();
+  } else {
+    // every rank's whole send buffer to every rank, then each takes its pieces
+    std::vector<uint64_t> tot(N, 0);
+    tot[me] = soff[N];
+    {
+      std::vector<uint64_t> v(N, 0);
+      v[me] = soff[N];
+      uint64_t *d = (uint64_t *)amgd_alloc(8ull * N + 8);
+      amgd_h2d(d + me, &v[me], 8);
+      std::vector<uint64_t> o(N + 1);
+      for (int q = 0; q <= N; q++) o[q] = 8ull * q;
+      void *b = d;
+      amgd_allgatherv(1, &b, o.data());
+      amgd_d2h(tot.data(), d, 8ull * N);
+      amgd_free(d);
+    }
+    std::vector<uint64_t> base(N + 1, 0), so((size_t)N * (N + 1));
+    for (int q = 0; q < N; q++) base[q + 1] = base[q] + tot[q];
+    // every rank's offsets table, so each can find its piece in every buffer
+    uint64_t *dt = (uint64_t *)amgd_alloc(8ull * N * (N + 1) + 8);
+    amgd_h2d(dt + (size_t)me * (N + 1), soff, 8ull * (N + 1));
+    {
+      std::vector<uint64_t> o(N + 1);
+      for (int q = 0; q <= N; q++) o[q] = 8ull * q * (N + 1);
+      void *b = dt;
+      amgd_allgatherv(1, &b, o.data());
+    }
+    amgd_d2h(so.data(), dt, 8ull * N * (N + 1));
+    amgd_free(dt);
+    char *stage = (char *)amgd_alloc(base[N] + 16);
+    if (tot[me]) HIPCK(hipMemcpyAsync(stage + base[me], send, tot[me], hipMemcpyDeviceToDevice, amgd_s()));
+    {
+      std::vector<uint64_t> o(base.begin(), base.end());
+      void *b = stage;
+      amgd_allgatherv(1, &b, o.data());
+    }
+    for (int p = 0; p < N; p++) {
+      if (p == me) continue;
+      const uint64_t *sp = so.data() + (size_t)p * (N + 1);
+      const uint64_t len = sp[me + 1] - sp[me];
+      if (len != roff[p + 1] - roff[p]) {
+        fprintf(stderr, "omp_amg_amd: alltoallv: rank %d expects %lu bytes from %d, which sends %lu\n", me,
+                (unsigned long)(roff[p + 1] - roff[p]), p, (unsigned long)len);
+        abort();
+      }
+      if (len) HIPCK(hipMemcpyAsync((char *)recv + roff[p], stage + base[p] + sp[me], len,
+                                    hipMemcpyDeviceToDevice, amgd_s()));
+      g_bytes += len;
+    }
+    amgd_sync();
+    amgd_free(stage);
+  }
+  g_ms += (amgd_wtime() - t0) * 1e3;
 }

@@ -2219,7 +2219,7 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     if (sub == 0) {              // slot r of the list: no contended counter
       si[r] = best != ~0ull ? trow[best] : 0u;
       sj[r] = c;
-      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
+      if (best != ~0ull) { ta[best] = 0.0; if (perm) a[perm[best]] = 0.0; *removed = 1u; }
     }
   }
 }
@@ -2255,7 +2255,7 @@ __global__ __launch_bounds__(1024) void k_fs_select_long(const uint64_t *tro, co
         if (smx[q] > mx || (smx[q] == mx && sbest[q] < best)) { mx = smx[q]; best = sbest[q]; }
       si[r] = best != ~0ull ? trow[best] : 0u;
       sj[r] = c;
-      if (best != ~0ull) { ta[best] = 0.0; a[perm[best]] = 0.0; *removed = 1u; }
+      if (best != ~0ull) { ta[best] = 0.0; if (perm) a[perm[best]] = 0.0; *removed = 1u; }
     }
     __syncthreads();
   }
@@ -2394,6 +2394,16 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
                                    double *rs, const double *w, double *sumR,
                                    double thr, uint32_t *sel_i, uint32_t *sel_j,
                                    uint32_t *nremoved) {
+  return amgd_fs_select_ex(Rl, Rt, perm, rs, w, sumR, thr, sel_i, sel_j, nremoved, 0, 1);
+}
+// c0: Rt holds rows c0.. of R' (partitioned mode: sel_j gets the global column, w / sumR are
+// the caller's pointers at c0); perm NULL: R's own copy is not touched; resum 0: rs / sumR
+// are left to the caller
+__global__ void k_add_u32(uint32_t *a, uint64_t n, uint32_t v) { GRID_STRIDE(i, n) a[i] += v; }
+extern "C" uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
+                                      double *rs, const double *w, double *sumR,
+                                      double thr, uint32_t *sel_i, uint32_t *sel_j,
+                                      uint32_t *nremoved, uint32_t c0, int resum) {
   hipStream_t s = amgd_s();
   const uint32_t nc = Rt->rn;
   uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
@@ -2428,7 +2438,8 @@ extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_
   unsigned h[4];
   amgd_d2h(h, cnt, 12);
   h[0] = h[2];                    // selections = bad columns (one per column)
-  if (h[1]) {
+  if (c0 && h[0]) k_add_u32<<<grid_for(h[0]), 256, 0, s>>>(sel_j, h[0], c0);
+  if (h[1] && resum) {
     const dcsr *M[2] = {Rl, Rt};
     const uint32_t *L[2] = {sel_i, sel_j};
     double *O[2] = {rs, sumR};

@@ -1,0 +1,848 @@
+/*
+ * amgd_psetup.c -- host driver (C) of the PARTITIONED multi-GPU setup
+ * (amgd_part.h for the data layout).
+ *
+ * The same level loop as amgd_setup.c (reference amg_setup.c:60-400) with every matrix
+ * held as row blocks: rank p owns rows [split[p], split[p+1]) of each level's A, Af, W and
+ * AfP and of every intermediate (R, R', W_skel, the constraint operator S, Q factors of
+ * its coarse points ...).  Vectors are kept whole on every rank, so the reference-order
+ * dots, maxima and every host decision (coarsening norm bound, Lanczos, PCG, the
+ * find_support loop) are computed identically everywhere without a collective.  The
+ * exchanges are the ones the rows need:
+ *   - a product's output rows complete the whole vector (allgatherv of row segments);
+ *   - X = A*B fetches the rows of B the local rows of A reference (halo, alltoallv);
+ *   - transposes send each rank the pieces of its rows (alltoallv), concatenated in
+ *     rank = ascending-row order, which is the stable transpose of amg_setup.c:2000;
+ *   - the Q factors fetch the Af rows of their supports, interp_lmop the supports and
+ *     Q factors of the coarse points its rows meet;
+ *   - find_support's selections are allgathered and each rank removes its own entries.
+ * Every row is computed by the one-GPU kernels from the same row data, so the hierarchy
+ * is bit-identical to the one-GPU one (tests/test_gpu_partition.py).
+ *
+ * Not partitioned (each rank computes the whole, identically): the per-sweep vector
+ * arithmetic and reductions.  Paths taken in full on every rank instead: interp_lmop's
+ * general walk (sp_add lands past the end of a row into the next rows,
+ * amg_setup.c:1665-1677 -- gathered operator), the incremental coarsening / find_support
+ * sweeps (full sweeps here: the same values, amgd_coarsen.hip), the transposed product
+ * forms of the one-GPU driver (direct products here: the same sums).
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "amgd.h"
+#include "amgd_hostmath.h"
+#include "amgd_part.h"
+#include "amgd_psetup.h"
+
+static double *dalloc(uint64_t n) { return (double *)amgd_alloc(n * 8 + 8); }
+static double *dones(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 1.0); return p; }
+static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0); return p; }
+
+static int g_me, g_N;
+static uint64_t g_ub;
+static int g_verbose = -1;
+static int verbose(void) {
+  if (g_verbose < 0) { const char *e = getenv("AMGD_VERBOSE"); g_verbose = e && *e && *e != '0'; }
+  return g_verbose && g_me == 0;
+}
+static uint64_t g_lmop_full;        /* interp_lmop calls done on gathered data */
+
+/* sum / OR / max of one u64 per rank, identical on every rank */
+static uint64_t all_sum(uint64_t v) {
+  uint64_t *a = (uint64_t *)calloc((size_t)g_N, 8);
+  a[g_me] = v;
+  amgd_pcomm_allgather_u64(a, 1);
+  uint64_t s = 0;
+  for (int p = 0; p < g_N; p++) s += a[p];
+  free(a);
+  return s;
+}
+static uint64_t all_max(uint64_t v) {
+  uint64_t *a = (uint64_t *)calloc((size_t)g_N, 8);
+  a[g_me] = v;
+  amgd_pcomm_allgather_u64(a, 1);
+  uint64_t s = 0;
+  for (int p = 0; p < g_N; p++) s = a[p] > s ? a[p] : s;
+  free(a);
+  return s;
+}
+static uint64_t gnnz(const pmat *A) { return all_sum(A->m->nnz); }
+
+/* ------------------------------------------------------------------------ */
+/* coarsen (amg_setup.c:2737): full sweeps, whole vectors                     */
+/* ------------------------------------------------------------------------ */
+static pmat *p_strength(const pmat *A) {
+  const uint32_t n = A->rp->n;
+  double *D = dalloc(n);
+  pm_diag(A, D);
+  amgd_vunary(D, n, AMGD_V_SQRT);
+  amgd_vunary(D, n, AMGD_V_INV);
+  pmat *S = pm_copy(A);
+  pm_diag_op2(S, D, D, AMGD_SCALE2_ABS);
+  pm_diag(S, D);
+  pm_diag_op(S, D, AMGD_DMINUS);
+  amgd_free(D);
+  return S;
+}
+static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
+  const uint32_t n = A->rp->n, r0 = A->rp->split[g_me];
+  pmat *S = p_strength(A);
+  pmat *St = pm_transpose(S);
+  uint8_t *vf = (uint8_t *)amgd_alloc(n + 1), *ma = (uint8_t *)amgd_alloc(n + 1), *mb = (uint8_t *)amgd_alloc(n + 1);
+  double *vfd = dones(n), *g = dalloc(n), *w1 = dalloc(n), *w2a = dalloc(n), *w2 = dalloc(n);
+  double *w = dalloc(n), *x1 = dalloc(n), *x2 = dalloc(n), *m1 = dalloc(n), *m2 = dalloc(n), *amax = dalloc(n);
+  uint32_t *anyvc = (uint32_t *)amgd_alloc(4), *stamp = (uint32_t *)amgd_alloc(4ull * n + 4);
+  uint32_t *front = (uint32_t *)amgd_alloc(4ull * n + 4), *cnt = (uint32_t *)amgd_alloc(64);
+  amgd_memset(vc, 0, n);
+  amgd_memset(vf, 1, n);
+  amgd_memset(anyvc, 0, 4);
+  amgd_memset(stamp, 0, 4ull * n);
+  int it = 0;
+  for (;;) {
+    it++;
+    pm_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);           /* g   = vf.*(S*vf)  */
+    pm_spmv(S, g, w1, 0.0, NULL, 1.0, vf);            /* w1  = vf.*(S*g)   */
+    pm_spmv(S, w1, w2a, 0.0, NULL, 1.0, vf);          /* w2a = vf.*(S*w1)  */
+    pm_spmv(S, w2a, w2, 0.0, NULL, 1.0, vf);          /* w2  = vf.*(S*w2a) */
+    amgd_cs_w_mask1(n, w1, w2, w, ctol * ctol, g, ma, x1, NULL, 4);
+    uint64_t mi = 0;
+    double wm = 0;
+    double w1m = amgd_max_first2(w1, w, n, &mi, &wm);
+    double b = (w1m < wm) ? sqrt(w1m) : sqrt(wm);
+    if (b <= ctol) {
+      uint32_t any = 0;
+      amgd_d2h(&any, anyvc, 4);
+      if (!any) { uint8_t one = 1; amgd_h2d(vc + mi, &one, 1); }
+      if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
+      break;
+    }
+    /* Amax rows: local, then whole (the gather reads Amax of any row of S) */
+    amgd_mat_amax(S->m, vf, 0.1, amax + r0);
+    pm_allgather_vec(amax, 8, S->rp);
+    amgd_mat_max_gather(St->m, vf + r0, x1, amax, m1 + r0);
+    pm_allgather_vec(m1, 8, St->rp);
+    amgd_cs_mask2(n, g, m1, ma, mb, x2, NULL, 5);
+    amgd_mat_max_gather(St->m, vf + r0, x2, amax, m2 + r0);
+    pm_allgather_vec(m2, 8, St->rp);
+    amgd_memset(cnt, 0, 64);
+    amgd_cs_mask3(n, m2, mb, vc, vf, vfd, anyvc, front, cnt, stamp, 8u * it + 8, NULL, 6);
+  }
+  pm_free(&S); pm_free(&St);
+  amgd_free(vf); amgd_free(ma); amgd_free(mb); amgd_free(vfd); amgd_free(g); amgd_free(w1);
+  amgd_free(w2a); amgd_free(w2); amgd_free(w); amgd_free(x1); amgd_free(x2); amgd_free(m1);
+  amgd_free(m2); amgd_free(amax); amgd_free(anyvc); amgd_free(stamp); amgd_free(front); amgd_free(cnt);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Lanczos (amg_setup.c:2435), PCG (amg_setup.c:2242)                         */
+/* ------------------------------------------------------------------------ */
+/* the value of a 1 x 1 matrix (on the rank owning row 0) */
+static double p_a00(const pmat *A) {
+  double v = 0;
+  if (A->m->rn && A->m->nnz) amgd_d2h(&v, A->m->a, 8);
+  uint64_t *a = (uint64_t *)calloc((size_t)g_N, 8);
+  memcpy(&a[g_me], &v, 8);
+  amgd_pcomm_allgather_u64(a, 1);
+  int owner = 0;
+  for (int p = 0; p < g_N; p++) if (A->rp->split[p + 1] > A->rp->split[p]) { owner = p; break; }
+  memcpy(&v, &a[owner], 8);
+  free(a);
+  return v;
+}
+#define KMAX 299
+static uint32_t p_lanczos(const pmat *A, double *out) {
+  const uint32_t rn = A->rp->n;
+  double *rh = (double *)malloc((size_t)rn * 8 + 8);
+  for (uint32_t i = 0; i < rn; i++) rh[i] = (double)rand() / (double)RAND_MAX;
+  double *r = dalloc(rn);
+  amgd_h2d(r, rh, (size_t)rn * 8);
+  free(rh);
+  double l[KMAX + 2], y[KMAX + 2], d[KMAX + 2], v[KMAX + 2];
+  double beta = amgd_norm2(r, rn), beta2 = beta * beta, change;
+  beta = sqrt(beta2);
+  uint32_t k = 0;
+  {
+    double fr = pm_fro_minus_eye(A), fro = sqrt(fr), fro2 = fro * fro;
+    fro = sqrt(fro2);
+    if (fro < 1e-11) { l[0] = 1; l[1] = 1; y[0] = 0; y[1] = 0; k = 2; change = 0.0; }
+    else change = 1.0;
+  }
+  if (rn == 1) {
+    const double a00 = p_a00(A);
+    l[0] = a00; l[1] = a00; y[0] = 0; y[1] = 0; k = 2; change = 0.0;
+  }
+  double *qk = dzeros(rn), *qkm1 = dalloc(rn), *Aqk = dalloc(rn);
+  while (k < KMAX && (change > 1e-5 || y[0] > 1e-3 || y[k - 1] > 1e-3)) {
+    k++;
+    amgd_lanczos_step(r, 1. / beta, qk, qkm1, rn);
+    pm_spmv(A, qk, Aqk, 0, NULL, 1, NULL);
+    double alpha = amgd_dot(qk, Aqk, rn);
+    amgd_lanczos_resid(r, Aqk, qk, alpha, qkm1, beta, rn);
+    if (k == 1) { l[0] = alpha; y[0] = 1; }
+    else {
+      double l0 = l[0], lkm2 = l[k - 2];
+      d[0] = 0;
+      for (uint32_t i = 1; i < k; i++) d[i] = l[i - 1];
+      d[k] = 0;
+      v[0] = alpha;
+      for (uint32_t i = 1; i < k; i++) v[i] = beta * y[i - 1];
+      tdeig(l, y, d, v, (int)k - 1);
+      change = fabs(l0 - l[0]) + fabs(lkm2 - l[k - 1]);
+    }
+    beta = amgd_norm2(r, rn);
+    beta2 = beta * beta;
+    beta = sqrt(beta2);
+    if (beta == 0) break;
+  }
+  uint32_t n = 0;
+  for (uint32_t i = 0; i < k; i++) if (y[i] < 0.01) out[n++] = l[i];
+  amgd_free(r); amgd_free(qk); amgd_free(qkm1); amgd_free(Aqk);
+  return n;
+}
+
+static double g_pcg_rho, g_pcg_stop;
+static uint32_t p_pcg(double *x, const pmat *A, double *r, const double *M, double tol, const double *b) {
+  const uint32_t rn = A->rp->n;
+  amgd_vfill(x, rn, 0.0);
+  if (rn == 0) return 0;
+  double *p = dzeros(rn), *z = dalloc(rn), *w = dalloc(rn);
+  amgd_vmul_dot_prep(z, M, r, rn);
+  double rho = amgd_dot(r, z, rn);
+  double rho_0 = amgd_dot3(M, b, rn);
+  double rho_stop = tol * tol * rho_0, rho_old = 1, alpha, beta;
+  uint32_t n = rn <= 100 ? rn : 100, k = 0;
+  while (rho > rho_stop && k < n) {
+    k++;
+    beta = rho / rho_old;
+    amgd_pcg_p(p, z, beta, rn);
+    pm_spmv(A, p, w, 0, NULL, 1, NULL);
+    alpha = amgd_dot(p, w, rn);
+    alpha = rho / alpha;
+    amgd_pcg_xrz(x, r, z, p, w, M, alpha, rn);
+    rho_old = rho;
+    rho = amgd_dot(r, z, rn);
+  }
+  g_pcg_rho = rho;
+  g_pcg_stop = rho_stop;
+  amgd_free(p); amgd_free(z); amgd_free(w);
+  return k;
+}
+
+/* ------------------------------------------------------------------------ */
+/* interpolation pieces                                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  pmat *Wt;            /* W_skel^T: rows = coarse points of this rank */
+  double *Q;           /* packed Q factors of those coarse points */
+  uint64_t *qoff, qtot;
+  pmat *S, *W0, *W0t;
+} pfactor;
+static void pfactor_free(pfactor *f) {
+  pm_free(&f->Wt);
+  if (f->Q) amgd_free(f->Q);
+  if (f->qoff) amgd_free(f->qoff);
+  pm_free(&f->S); pm_free(&f->W0); pm_free(&f->W0t);
+}
+
+/* interp_lmop (amg_setup.c:1589) on the own rows of S: the supports and Q factors of the
+   coarse points those rows meet are fetched (halo); where the general walk is needed the
+   operator is formed on gathered data and each rank keeps its rows */
+static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u) {
+  dcsr *WtE = pm_halo_rows(f->Wt, Wskel->m);
+  /* the Q factors as a matrix whose row c holds Q_c (offsets qoff): halo rows of it */
+  dcsr qm;
+  qm.rn = f->Wt->m->rn;
+  qm.cn = 1;
+  qm.nnz = f->qtot;
+  qm.ro = f->qoff;
+  qm.col = (uint32_t *)amgd_alloc(4 * f->qtot + 8);
+  amgd_memset(qm.col, 0, 4 * f->qtot + 8);
+  qm.a = f->Q;
+  pmat qp = {&qm, f->Wt->rp, f->Wt->cp};
+  dcsr *QE = pm_halo_rows(&qp, Wskel->m);
+  uint32_t *kpos = pm_kpos(Wskel, WtE);
+  const int st = amgd_lmop(S->m, Wskel->m, kpos, WtE, QE->a, QE->ro, u);
+  amgd_free(kpos);
+  dcsr_free(&WtE);
+  dcsr_free(&QE);
+  if (all_max((uint64_t)st) != 0) {
+    g_lmop_full++;
+    dcsr *Sf = pm_gather_full(S), *Wsf = pm_gather_full(Wskel), *Qf = pm_gather_full(&qp);
+    uint64_t *perm = NULL;
+    dcsr *Wtf = amgd_transpose(Wsf, &perm);
+    uint32_t *kp = amgd_lmop_kpos(Wtf, perm);
+    amgd_free(perm);
+    amgd_comm_suspend_partition(1);
+    amgd_lmop(Sf, Wsf, kp, Wtf, Qf->a, Qf->ro, u);
+    amgd_comm_suspend_partition(0);
+    const uint32_t r0 = S->rp->split[g_me];
+    uint64_t off = 0;
+    amgd_d2h(&off, Sf->ro + r0, 8);
+    if (S->m->nnz) amgd_d2d(S->m->a, Sf->a + off, 8 * S->m->nnz);
+    amgd_free(kp);
+    dcsr_free(&Sf); dcsr_free(&Wsf); dcsr_free(&Wtf); dcsr_free(&Qf);
+  }
+  amgd_free(qm.col);
+}
+
+static void p_solve_constraint(double *lam, const pmat *W_skel, pfactor *fac, const pmat *W0,
+                               const double *alpha, const double *u, const double *v, double tol) {
+  const uint32_t nf = W_skel->rp->n, nc = W_skel->cp->n;
+  double *au2 = dalloc(nc);
+  amgd_vop(au2, u, u, nc, AMGD_V_MUL);
+  amgd_vop(au2, au2, alpha, nc, AMGD_V_MUL);
+  if (!fac->S) {
+    pmat *Wn = pm_drop_zeros(W_skel), *Wnt = pm_drop_zeros(fac->Wt);
+    fac->S = pm_spgemm(Wn, Wnt, 1);
+    pm_free(&Wn); pm_free(&Wnt);
+    p_lmop(fac->S, W_skel, fac, au2);
+  }
+  pmat *S = fac->S;
+  double *resid = dalloc(nf), *d = dalloc(nf);
+  pm_spmv(W0, u, resid, 1.0, v, -1.0, NULL);
+  pm_diag(S, d);
+  uint8_t *dl = (uint8_t *)amgd_alloc(nf + 1);
+  amgd_u8_nonzero(d, dl, nf);
+  uint64_t ncond = amgd_u8_count(dl, nf);
+  double *q = dalloc(ncond), *xx = dalloc(ncond);
+  if (ncond != nf) {
+    amgd_vzero_where(lam, dl, nf);
+    apart *Pc = apart_induced(S->rp, dl);
+    pmat *S2 = pm_sub_mat(S, dl, dl, Pc, Pc);
+    double *rc = dalloc(nf), *dc = dalloc(nf), *lc = dalloc(nf);
+    amgd_vcompact(rc, resid, dl, nf);
+    amgd_vcompact(dc, d, dl, nf);
+    amgd_vcompact(lc, lam, dl, nf);
+    pm_spmv(S2, lc, q, 1., rc, -1., NULL);
+    amgd_vunary(dc, ncond, AMGD_V_INV);
+    const uint32_t its = p_pcg(xx, S2, q, dc, tol, rc);
+    if (verbose())
+      printf("   constraint: %lu of %u rows, pcg %u its, rho %.9e stop %.9e\n", (unsigned long)ncond, nf, its,
+             g_pcg_rho, g_pcg_stop), fflush(stdout);
+    amgd_vexpand_add(lam, xx, dl, nf);
+    amgd_free(rc); amgd_free(dc); amgd_free(lc);
+    pm_free(&S2);
+    apart_free(&Pc);
+  } else {
+    pm_spmv(S, lam, q, 1., resid, -1., NULL);
+    amgd_vunary(d, nf, AMGD_V_INV);
+    const uint32_t its = p_pcg(xx, S, q, d, tol, resid);
+    if (verbose())
+      printf("   constraint: %u of %u rows, pcg %u its, rho %.9e stop %.9e\n", nf, nf, its, g_pcg_rho, g_pcg_stop),
+          fflush(stdout);
+    amgd_vop(lam, lam, xx, nf, AMGD_V_ADD);
+  }
+  amgd_free(au2); amgd_free(resid); amgd_free(d); amgd_free(dl); amgd_free(q); amgd_free(xx);
+}
+
+/* solve_weights (amg_setup.c:1437) */
+static pmat *p_qapply(const pfactor *f, const pmat *Amt, const double *au, const double *lam) {
+  pmat *Wt = pm_new(dcsr_empty_like_pattern(f->Wt->m), f->Wt->rp, f->Wt->cp);
+  const uint32_t c0 = f->Wt->rp->split[g_me];
+  amgd_qapply(f->Wt->m, f->Q, f->qoff, Amt->m, au + c0, lam, Wt->m->a);
+  return Wt;
+}
+static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, pfactor *fac, const pmat *Amt,
+                             const double *alpha, const double *u, const double *v, double tol) {
+  const uint32_t nf = W_skel->rp->n, nc = W_skel->cp->n;
+  double *au = dalloc(nc), *zeros = dzeros(nf);
+  amgd_vop(au, alpha, u, nc, AMGD_V_MUL);
+  if (!fac->W0) {
+    fac->W0t = p_qapply(fac, Amt, au, zeros);
+    fac->W0 = pm_transpose(fac->W0t);
+  }
+  *W0 = fac->W0;
+  p_solve_constraint(lam, W_skel, fac, *W0, alpha, u, v, tol);
+  pmat *Wt = p_qapply(fac, Amt, au, lam);
+  pmat *W = pm_transpose(Wt);
+  pm_free(&Wt);
+  amgd_free(au); amgd_free(zeros);
+  return W;
+}
+
+/* find_support (amg_setup.c:1260): full sweeps; selections per coarse point on the rank
+   owning it, gathered, and each rank removes the selected entries of its own rows of R */
+typedef struct { const double *rs, *w, *tmp, *w2; } pfs_first;
+static uint32_t p_fs_select(pmat *Rl, pmat *Rt, double *rs, const double *w, double *sumR, double thr,
+                            uint32_t *si, uint32_t *sj, uint32_t *nremoved) {
+  const uint32_t c0 = Rt->rp->split[g_me], nl = Rt->m->rn;
+  uint32_t *li = (uint32_t *)amgd_alloc(4ull * nl + 8), *lj = (uint32_t *)amgd_alloc(4ull * nl + 8);
+  uint32_t rem = 0;
+  const uint32_t h = amgd_fs_select_ex(Rl->m, Rt->m, NULL, rs, w + c0, sumR + c0, thr, li, lj, &rem, c0, 0);
+  uint64_t *cnt = (uint64_t *)calloc(2ull * g_N, 8);
+  cnt[2 * g_me] = h;
+  cnt[2 * g_me + 1] = rem;
+  amgd_pcomm_allgather_u64(cnt, 2);
+  uint64_t *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
+  uint64_t remall = 0;
+  for (int p = 0; p < g_N; p++) { pre[p + 1] = pre[p] + cnt[2 * p]; remall += cnt[2 * p + 1]; }
+  const uint64_t tot = pre[g_N];
+  if (h) { amgd_d2d(si + pre[g_me], li, 4ull * h); amgd_d2d(sj + pre[g_me], lj, 4ull * h); }
+  uint64_t *off = (uint64_t *)malloc(2 * ((size_t)g_N + 1) * 8);
+  for (int p = 0; p <= g_N; p++) { off[p] = 4 * pre[p]; off[g_N + 1 + p] = 4 * pre[p]; }
+  void *bufs[2] = {si, sj};
+  amgd_allgatherv(2, bufs, off);
+  free(off);
+  pm_zero_entries(Rl, si, sj, tot);
+  if (remall) {
+    pm_list_rowsum(Rl, si, (uint32_t)tot, rs);
+    pm_list_rowsum(Rt, sj, (uint32_t)tot, sumR);
+  }
+  free(cnt); free(pre);
+  amgd_free(li); amgd_free(lj);
+  *nremoved = (uint32_t)(remall ? 1 : 0);
+  return (uint32_t)tot;
+}
+static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_first *f1) {
+  const uint32_t nf = R->rp->n, nc = R->cp->n;
+  pmat *Rl = pm_copy(R);
+  double *onec = dones(nc), *rs = dalloc(nf), *w = dalloc(nc), *w2 = dalloc(nc), *tmp = dalloc(nf);
+  double *vv = dalloc(nc), *sumR = dalloc(nc);
+  const uint64_t cap = gnnz(R) + nc + 16;
+  uint64_t ns = 0;
+  uint32_t *si = (uint32_t *)amgd_alloc(cap * 4), *sj = (uint32_t *)amgd_alloc(cap * 4);
+  double theta = 0.5;
+  int it = 0;
+  if (f1) amgd_d2d(rs, f1->rs, (size_t)nf * 8);
+  else pm_spmv(Rl, onec, rs, 0., NULL, 1., NULL);
+  pm_colsum(Rt, sumR);
+  for (;;) {
+    it++;
+    if (it == 1 && f1) {
+      amgd_d2d(w, f1->w, (size_t)nc * 8);
+      amgd_d2d(tmp, f1->tmp, (size_t)nf * 8);
+      amgd_d2d(w2, f1->w2, (size_t)nc * 8);
+    } else {
+      pm_spmvt(Rt, rs, w);
+      pm_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
+      pm_spmvt(Rt, tmp, w2);
+    }
+    amgd_vdiv_guard(vv, w2, w, nc);
+    double mv = amgd_max_first(vv, nc, NULL), mw = mv;
+    if (mv < goal || mw < goal) break;
+    while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
+    if (theta == 0) { g_ub++; break; }
+    if (nf <= 1) { g_ub++; break; }
+    uint32_t nrem = 0;
+    const uint32_t nsel = p_fs_select(Rl, Rt, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    ns += nsel;
+    if (nrem == 0) { g_ub++; break; }
+    if (ns + nc > cap) { g_ub++; break; }
+  }
+  pmat *Sk = pm_coo_ones(si, sj, ns, R->rp, R->cp);
+  if (verbose()) printf("    find_support: %d sweeps, %lu entries\n", it, (unsigned long)ns);
+  pm_free(&Rl); pm_free(&Rt);
+  amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
+  amgd_free(sumR); amgd_free(si); amgd_free(sj);
+  return Sk;
+}
+
+typedef struct {
+  const pmat *Af, *W0, *Ar;
+  const double *Dfsqrti, *Dcs;
+} pr0_ctx;
+static pmat *p_r0_rows(const pr0_ctx *c, const uint8_t *bad) {
+  pmat *Afb = pm_rows_masked(c->Af, bad);
+  pmat *AfW0 = pm_spgemm(Afb, c->W0, 0);
+  pm_free(&Afb);
+  pmat *Arb = pm_rows_masked(c->Ar, bad);
+  pmat *Arhat0 = pm_mpm(1., AfW0, 1., Arb);
+  pm_free(&AfW0); pm_free(&Arb);
+  pm_diag_op2(Arhat0, c->Dfsqrti, c->Dcs, AMGD_SCALE_ABS);   /* |Dfsqrti*X|*Dcs in place */
+  return Arhat0;
+}
+/* expand_support (amg_setup.c:907) */
+static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const pr0_ctx *r0c, double gamma,
+                              const pfs_first *f1) {
+  const uint32_t nf = W_skel->rp->n, r0 = W_skel->rp->split[g_me];
+  pmat *M = p_find_support(R, Rt, gamma, f1);
+  pmat *ns = pm_mpm(1., M, 1., W_skel);
+  pm_free(&M);
+  uint32_t nb_local = 0;
+  uint8_t *badl = amgd_bad_rows(ns->m, &nb_local);
+  const uint64_t nbad = all_sum(nb_local);
+  if (nbad == 0) {
+    amgd_skel_binarize(ns->m, 0);
+    amgd_free(badl);
+    return ns;
+  }
+  uint8_t *bad = (uint8_t *)amgd_alloc(nf + 8);
+  amgd_memset(bad, 0, nf);
+  if (ns->m->rn) amgd_d2d(bad + r0, badl, ns->m->rn);
+  amgd_free(badl);
+  pm_allgather_vec(bad, 1, W_skel->rp);
+  if (verbose()) printf("    expand_support: %lu bad rows of %u\n", (unsigned long)nbad, nf);
+  pmat *R0 = p_r0_rows(r0c, bad);
+  pmat *R0W = pm_mxmpoint(R0, W_skel);
+  pmat *Xf = pm_mpm(1., R0, -1., R0W);
+  pm_free(&R0W); pm_free(&R0);
+  uint32_t *pi = NULL, *pj = NULL;
+  uint64_t np = amgd_expand_pick(Xf->m, bad + r0, &pi, &pj);
+  double *ones = dones(np);
+  pmat *N = pm_new(amgd_coo2csr(np, pi, pj, ones, W_skel->m->rn, W_skel->m->cn, 1), W_skel->rp, W_skel->cp);
+  pmat *out = pm_mpm(1., ns, 1., N);
+  amgd_skel_binarize(out->m, 1);
+  pm_free(&N); pm_free(&ns); pm_free(&Xf);
+  amgd_free(ones); amgd_free(pi); amgd_free(pj); amgd_free(bad);
+  return out;
+}
+
+static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, double gamma2, double tol) {
+  const uint32_t rnf = Af->rp->n, cnc = Ac->rp->n;
+  double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
+  pm_diag(Af, Df);
+  amgd_d2d(Dfinv, Df, (size_t)rnf * 8);
+  amgd_vunary(Dfinv, rnf, AMGD_V_INV);
+  double *uc = dones(cnc), *tmp = dalloc(rnf), *v = dalloc(rnf), *b = dones(rnf);
+  pm_spmv(Ar, uc, tmp, 0, NULL, -1, NULL);              /* tmp = -Ar*uc */
+  p_pcg(v, Af, tmp, Df, 1e-16, b);
+  double *Dc = dalloc(cnc), *Dcinv = dalloc(cnc);
+  pm_diag(Ac, Dc);
+  amgd_d2d(Dcinv, Dc, (size_t)cnc * 8);
+  amgd_vunary(Dcinv, cnc, AMGD_V_INV);
+  pmat *ArD = pm_copy(Ar);
+  amgd_vals_sqr(ArD->m);
+  pm_diag_op2(ArD, Dfinv, Dcinv, AMGD_SCALE2);
+  pmat *W_skel = pm_new(amgd_min_skel(ArD->m), Ar->rp, Ar->cp);   /* row-local: one entry per row */
+  pm_free(&ArD);
+  double *lam = dzeros(rnf), *alpha = dalloc(cnc);
+  amgd_d2d(alpha, Dc, (size_t)cnc * 8);
+  double *Dfsqrti = Dfinv;
+  amgd_vunary(Dfsqrti, rnf, AMGD_V_SQRT);
+  pmat *Amt = pm_transpose(Ar);                          /* -Ar' */
+  amgd_vals_scale(Amt->m, -1.0);
+  double *Dcs = dalloc(cnc), *w1 = dalloc(cnc), *w2 = dalloc(cnc), *onesc = dones(cnc), *r = dalloc(cnc);
+  double *rs1 = dalloc(rnf);
+  pmat *W = NULL;
+  uint64_t prev_nnz = (uint64_t)-1;
+  pmat *prevWt = NULL;
+  double *prevQ = NULL;
+  uint64_t *prevQoff = NULL;
+  for (;;) {
+    pfactor fac;
+    memset(&fac, 0, sizeof fac);
+    fac.Wt = pm_transpose(W_skel);
+    dcsr *AfE = pm_halo_rows(Af, fac.Wt->m);             /* the Af rows of the supports */
+    fac.Q = amgd_qfactor_reuse(fac.Wt->m, AfE, &fac.qoff, &fac.qtot, prevWt ? prevWt->m : NULL, prevQ, prevQoff);
+    dcsr_free(&AfE);
+    if (prevWt) { pm_free(&prevWt); amgd_free(prevQ); amgd_free(prevQoff); prevQ = NULL; prevQoff = NULL; }
+    const pmat *W0;
+    pmat *Wtmp = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
+    pmat *AfW = pm_spgemm(Af, Wtmp, 0);
+    pmat *Arhat = pm_mpm(1., AfW, 1., Ar);
+    pm_free(&AfW);
+    pmat *Arr = pm_mpm(1.0, Arhat, 1.0, Ar);
+    pmat *ArW = pm_mxmpoint(Wtmp, Arr);
+    pm_free(&Arr);
+    pmat *ArWt = pm_transpose(ArW);
+    pm_colsum(ArWt, Dcs);
+    pm_free(&ArW); pm_free(&ArWt);
+    amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+    amgd_vunary(Dcs, cnc, AMGD_V_INV);
+    amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+    pmat *R = Arhat;                                     /* |Dfsqrti*Arhat|*Dcsqrti, in place */
+    pm_diag_op2(R, Dfsqrti, Dcs, AMGD_SCALE_ABS);
+    pmat *Rt = pm_transpose(R);
+    pm_spmv(R, onesc, rs1, 0., NULL, 1., NULL);
+    pm_spmvt(Rt, rs1, w1);
+    pm_spmv(R, w1, tmp, 0., NULL, 1., NULL);
+    pm_spmvt(Rt, tmp, w2);
+    amgd_vdiv_guard(r, w2, w1, cnc);
+    double maxr = 0;
+    uint64_t n = amgd_count_gt(r, cnc, gamma2, &maxr);
+    double w1m = amgd_max_first(w1, cnc, NULL);
+    const uint64_t wsk = gnnz(W_skel);
+    if (verbose())
+      printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)wsk, (unsigned long)n, sqrt(gamma2),
+             sqrt(maxr)), fflush(stdout);
+    int stalled = prev_nnz == wsk;
+    if (stalled) g_ub++;
+    prev_nnz = wsk;
+    if (n == 0 || w1m <= gamma2 || stalled) {
+      pm_free(&Rt);
+      W = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
+      double *wuc = dalloc(rnf);
+      pm_spmv(W, uc, wuc, 0., NULL, 1., NULL);
+      dcsr g = pm_gview(W);                              /* the diagonal match reads row ids */
+      amgd_scale_diag_match(&g, v, wuc);
+      pm_gview_free(&g);
+      amgd_free(wuc);
+      pm_free(&Wtmp);
+      pm_free(&R);
+      pfactor_free(&fac);
+      break;
+    }
+    amgd_alpha_update(alpha, Dc, w2, cnc);
+    pr0_ctx r0c = {Af, W0, Ar, Dfsqrti, Dcs};
+    const pfs_first f1 = {rs1, w1, tmp, w2};
+    pmat *nsk = p_expand_support(W_skel, R, Rt, &r0c, gamma2, &f1);
+    pm_free(&W_skel);
+    W_skel = nsk;
+    pm_free(&Wtmp);
+    pm_free(&R);
+    prevWt = fac.Wt; prevQ = fac.Q; prevQoff = fac.qoff;
+    fac.Wt = NULL; fac.Q = NULL; fac.qoff = NULL;
+    pfactor_free(&fac);
+  }
+  pm_free(&W_skel); pm_free(&Amt);
+  amgd_free(Df); amgd_free(Dfinv); amgd_free(uc); amgd_free(tmp); amgd_free(v); amgd_free(b);
+  amgd_free(Dc); amgd_free(Dcinv); amgd_free(lam); amgd_free(alpha); amgd_free(Dcs);
+  amgd_free(w1); amgd_free(w2); amgd_free(onesc); amgd_free(r); amgd_free(rs1);
+  return W;
+}
+
+/* ------------------------------------------------------------------------ */
+/* hierarchy                                                                 */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  pmat *A, *Af, *W, *AfP;
+  uint8_t *vc;                 /* whole */
+  double *D;                   /* whole (F points) */
+  unsigned long *idc, *idf;    /* whole */
+  double m, rho;
+  apart *Pn, *Pf;              /* rows of A (owned by this level), F points */
+} plevel;
+struct amgd_phier {
+  uint32_t nlevels, cap, n0;
+  plevel *lv;
+  unsigned long *id;
+  int nullspace;
+  double tolc, gamma;
+};
+
+static void add_time(double *acc, double *t0) {
+  amgd_sync();
+  double t = amgd_wtime();
+  *acc += (t - *t0) * 1e3;
+  *t0 = t;
+}
+
+__attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const uint32_t *dAi,
+                                                           const uint32_t *dAj, const double *dAv,
+                                                           amgd_phier **out, amgd_stats *st) {
+  g_me = amgd_pcomm_rank();
+  g_N = amgd_pcomm_size();
+  g_ub = 0;
+  g_lmop_full = 0;
+  amgd_sync();
+  double t_start = amgd_wtime(), t0 = t_start;
+  /* level 0: the global size, the even split, the entries to the owners of their rows,
+     build_csr's empty-row / -column removal with the whole mask (amg_setup.c:3612) */
+  uint32_t mx[2] = {0, 0};
+  amgd_max_ij(nz, dAi, dAj, mx);
+  const uint32_t n_in = (uint32_t)all_max(mx[0] > mx[1] ? mx[0] : mx[1]);
+  apart *P0 = apart_even(n_in, g_N);
+  uint32_t *I = NULL, *J = NULL;
+  double *V = NULL;
+  const uint64_t m = pm_route_coo(nz, dAi, dAj, dAv, P0, &I, &J, &V);
+  const uint32_t r0 = P0->split[g_me], nl = P0->split[g_me + 1] - r0;
+  amgd_vadd_u32(I, m, (uint32_t)(0u - r0));
+  dcsr *T = amgd_coo2csr(m, I, J, V, nl, n_in, 1);
+  amgd_free(I); amgd_free(J); amgd_free(V);
+  uint8_t *zr = (uint8_t *)amgd_alloc((size_t)n_in + 8);
+  amgd_nonempty_rows(T, zr + r0);
+  pm_allgather_vec(zr, 1, P0);
+  amgd_phier *h = (amgd_phier *)calloc(1, sizeof(amgd_phier));
+  *out = h;
+  h->cap = 64;
+  h->lv = (plevel *)calloc(h->cap, sizeof(plevel));
+  apart *Pn = apart_induced(P0, zr);
+  pmat *Tp = pm_new(T, P0, P0);
+  pmat *A = pm_sub_mat(Tp, zr, zr, Pn, Pn);
+  pm_free(&Tp);
+  amgd_free(zr);
+  apart_free(&P0);
+  add_time(&st->t_build_ms, &t0);
+  const double tol = 0.5, ctol = 0.7, itol = 1e-4;
+  const double gamma2 = 1. - sqrt(1. - tol), gamma = sqrt(gamma2);
+  h->tolc = ctol;
+  h->gamma = gamma;
+  h->n0 = Pn->n;
+  h->id = (unsigned long *)amgd_alloc((size_t)Pn->n * 8 + 8);
+  amgd_ids_iota(h->id, Pn->n);
+  st->rows0 = Pn->n;
+  st->nnz0 = gnnz(A);
+  uint32_t level = 0;
+  for (;;) {
+    if (level + 1 >= h->cap) {
+      h->cap *= 2;
+      h->lv = (plevel *)realloc(h->lv, h->cap * sizeof(plevel));
+      memset(h->lv + h->cap / 2, 0, (h->cap / 2) * sizeof(plevel));
+    }
+    plevel *L = &h->lv[level];
+    const uint32_t n = Pn->n;
+    L->A = A;
+    L->Pn = Pn;
+    if (verbose()) printf("Level %u, dim(A) = %u, nnz(A)/dim(A) = %f\n", level + 1, n,
+                          n ? (double)gnnz(A) / n : 0.0), fflush(stdout);
+    if (n <= 1) {
+      const double a0 = n ? p_a00(A) : 0.0;
+      h->nullspace = a0 < 1e-9 ? 1 : 0;
+      break;
+    }
+    uint8_t *vc = (uint8_t *)amgd_alloc(n + 1), *vf = (uint8_t *)amgd_alloc(n + 1);
+    p_coarsen(A, vc, ctol);
+    amgd_u8_not(vc, vf, n);
+    L->vc = vc;
+    add_time(&st->t_coarsen_ms, &t0);
+    apart *Pf = apart_induced(Pn, vf), *Pc = apart_induced(Pn, vc);
+    L->Pf = Pf;
+    pmat *Af = pm_sub_mat(A, vf, vf, Pf, Pf);
+    const uint32_t rnf = Pf->n;
+    double *s = dalloc(rnf), *D = dalloc(rnf);
+    pm_rowsum_sq_inv(Af, s);
+    pm_diag(Af, D);
+    amgd_vop(D, D, s, rnf, AMGD_V_MUL);
+    amgd_free(s);
+    if (rnf >= 2) {
+      double *Dh = dalloc(rnf);
+      amgd_d2d(Dh, D, (size_t)rnf * 8);
+      amgd_vunary(Dh, rnf, AMGD_V_SQRT);
+      pmat *DAD = pm_copy(Af);
+      pm_diag_op2(DAD, Dh, Dh, AMGD_SCALE2);
+      double lambda[KMAX + 2];
+      uint32_t k = p_lanczos(DAD, lambda);
+      double a = lambda[0], bb = lambda[k - 1];
+      amgd_vscale(D, rnf, 2. / (a + bb));
+      L->rho = (bb - a) / (bb + a);
+      double c;
+      chebsim(&L->m, &c, L->rho, gamma2);
+      amgd_free(Dh);
+      pm_free(&DAD);
+    } else {
+      L->rho = 0;
+      L->m = 1;
+    }
+    L->D = D;
+    L->Af = Af;
+    add_time(&st->t_smoother_ms, &t0);
+    pmat *Afc = pm_sub_mat(A, vf, vc, Pf, Pc), *Ac = pm_sub_mat(A, vc, vc, Pc, Pc);
+    const uint32_t rnc = Pc->n;
+    L->idc = (unsigned long *)amgd_alloc((size_t)rnc * 8 + 8);
+    L->idf = (unsigned long *)amgd_alloc((size_t)rnf * 8 + 8);
+    amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, n, L->idc, L->idf);
+    pmat *W = p_interpolation(Af, Ac, Afc, gamma2, itol);
+    L->W = W;
+    add_time(&st->t_interp_ms, &t0);
+    /* Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) (amg_setup.c:339-372) */
+    pmat *Acf = pm_transpose(Afc);
+    amgd_spgemm_set_timer(0);
+    pmat *Wt = pm_transpose(W);
+    pmat *AfW = pm_spgemm(Af, W, 0);
+    pmat *AfP = pm_mpm(1., AfW, 1., Afc);
+    pm_free(&AfW);
+    L->AfP = AfP;
+    pmat *WtAfP = pm_spgemm(Wt, AfP, 0);
+    pmat *AcfW = pm_spgemm(Acf, W, 0);
+    amgd_spgemm_set_timer(-1);
+    pmat *Atmp = pm_mpm(1., WtAfP, 1., AcfW);
+    A = pm_mpm(1., Atmp, 1, Ac);
+    st->rap_out_nnz += gnnz(A);
+    pm_free(&Wt); pm_free(&WtAfP); pm_free(&Acf); pm_free(&AcfW); pm_free(&Atmp);
+    pm_free(&Afc); pm_free(&Ac);
+    amgd_free(vf);
+    add_time(&st->t_rap_ms, &t0);
+    Pn = Pc;
+    level++;
+  }
+  h->nlevels = level + 1;
+  amgd_sync();
+  st->t_total_ms = (amgd_wtime() - t_start) * 1e3;
+  st->ub_events = (uint32_t)g_ub;
+  st->nlevels = h->nlevels;
+  if (verbose() && g_lmop_full)
+    printf("partitioned setup: %lu interp_lmop calls on gathered data\n", (unsigned long)g_lmop_full);
+  return 0;
+}
+
+/* the hierarchy gathered (every rank gets all of it) into the ABI struct */
+static struct csr_mat *pcsr_to_host(const pmat *A) {
+  dcsr *F = pm_gather_full(A);
+  struct csr_mat *M = (struct csr_mat *)malloc(sizeof *M);
+  M->rn = F->rn;
+  M->cn = F->cn;
+  M->row_off = (amg_uint *)malloc(((size_t)F->rn + 1) * sizeof(amg_uint));
+  M->col = (amg_uint *)malloc((F->nnz ? F->nnz : 1) * sizeof(amg_uint));
+  M->a = (double *)malloc((F->nnz ? F->nnz : 1) * sizeof(double));
+  amgd_to_host_cols(F, M->row_off, M->col, M->a);
+  dcsr_free(&F);
+  return M;
+}
+__attribute__((visibility("hidden"))) int amgd_phier_export(const amgd_phier *h, struct amg_setup_data *data) {
+  uint32_t nl = h->nlevels, cap = nl + 1;
+  data->tolc = h->tolc;
+  data->gamma = h->gamma;
+  data->n = (double *)malloc(cap * 8); data->nnz = (double *)malloc(cap * 8);
+  data->nnzf = (double *)malloc(cap * 8); data->nnzfp = (double *)malloc(cap * 8);
+  data->m = (double *)malloc(cap * 8); data->rho = (double *)malloc(cap * 8);
+  data->A = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->Af = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->W = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->AfP = (struct csr_mat **)malloc(cap * sizeof(void *));
+  data->idc = (amg_uint **)malloc(cap * sizeof(void *));
+  data->idf = (amg_uint **)malloc(cap * sizeof(void *));
+  data->C = (double **)malloc(cap * sizeof(void *));
+  data->F = (double **)malloc(cap * sizeof(void *));
+  data->D = (double **)malloc(cap * sizeof(void *));
+  data->id = (amg_uint *)malloc((size_t)h->n0 * sizeof(amg_uint) + 8);
+  amgd_d2h(data->id, h->id, (size_t)h->n0 * 8);
+  for (uint32_t l = 0; l < nl; l++) {
+    const plevel *L = &h->lv[l];
+    data->n[l] = L->Pn->n;
+    data->A[l] = pcsr_to_host(L->A);
+    data->nnz[l] = (double)data->A[l]->row_off[data->A[l]->rn];
+    if (l + 1 == nl) break;
+    uint32_t rn = L->Pn->n, rnf = L->Pf->n, rnc = rn - rnf;
+    uint8_t *vc = (uint8_t *)malloc(rn + 1);
+    amgd_d2h(vc, L->vc, rn);
+    data->C[l] = (double *)malloc((size_t)rn * 8 + 8);
+    data->F[l] = (double *)malloc((size_t)rn * 8 + 8);
+    for (uint32_t i = 0; i < rn; i++) { data->C[l][i] = vc[i] ? 1. : 0.; data->F[l][i] = vc[i] ? 0. : 1.; }
+    free(vc);
+    data->D[l] = (double *)malloc((size_t)rnf * 8 + 8);
+    amgd_d2h(data->D[l], L->D, (size_t)rnf * 8);
+    data->m[l] = L->m;
+    data->rho[l] = L->rho;
+    data->Af[l] = pcsr_to_host(L->Af);
+    data->W[l] = pcsr_to_host(L->W);
+    data->AfP[l] = pcsr_to_host(L->AfP);
+    data->nnzf[l] = (double)data->Af[l]->row_off[data->Af[l]->rn];
+    data->nnzfp[l] = (double)data->AfP[l]->row_off[data->AfP[l]->rn];
+    data->idc[l] = (amg_uint *)malloc((size_t)rnc * 8 + 8);
+    data->idf[l] = (amg_uint *)malloc((size_t)rnf * 8 + 8);
+    amgd_d2h(data->idc[l], L->idc, (size_t)rnc * 8);
+    amgd_d2h(data->idf[l], L->idf, (size_t)rnf * 8);
+  }
+  data->nlevels = nl;
+  data->nullspace = (amg_uint)h->nullspace;
+  return 0;
+}
+__attribute__((visibility("hidden"))) void amgd_phier_free(amgd_phier **hp) {
+  amgd_phier *h = *hp;
+  if (!h) return;
+  for (uint32_t l = 0; l < h->nlevels || (l < h->cap && h->lv[l].A); l++) {
+    plevel *L = &h->lv[l];
+    pm_free(&L->A); pm_free(&L->Af); pm_free(&L->W); pm_free(&L->AfP);
+    if (L->vc) amgd_free(L->vc);
+    if (L->D) amgd_free(L->D);
+    if (L->idc) amgd_free(L->idc);
+    if (L->idf) amgd_free(L->idf);
+    apart_free(&L->Pn);
+    apart_free(&L->Pf);
+  }
+  if (h->id) amgd_free(h->id);
+  free(h->lv);
+  free(h);
+  *hp = NULL;
+}
+/* the rows this rank holds (its partition of level 0) and the levels */
+__attribute__((visibility("hidden"))) void amgd_phier_info(const amgd_phier *h, uint32_t *nlevels,
+                                                           uint32_t *r0, uint32_t *r1) {
+  *nlevels = h->nlevels;
+  *r0 = h->lv[0].Pn->split[g_me];
+  *r1 = h->lv[0].Pn->split[g_me + 1];
+}

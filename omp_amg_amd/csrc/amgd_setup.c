@@ -28,6 +28,7 @@
 #include "amg_setup.h"
 #include "crs.h"
 #include "omp_amg_amd.h"
+#include "amgd_psetup.h"
 
 #define API __attribute__((visibility("default")))
 
@@ -230,74 +231,7 @@ static void coarsen(const dcsr *A, uint8_t *vc, double ctol) {
 /* ------------------------------------------------------------------------ */
 /* Lanczos + tdeig (amg_setup.c:2435-2726); tdeig runs on the host           */
 /* ------------------------------------------------------------------------ */
-#define EPS (128 * DBL_EPSILON)
-static double sum_3(double a, double b, double c) {
-  if ((a >= 0 && b >= 0) || (a <= 0 && b <= 0)) return (a + b) + c;
-  if ((a >= 0 && c >= 0) || (a <= 0 && c <= 0)) return (a + c) + b;
-  return a + (b + c);
-}
-static double rat_root(double a, double b, double c, double sign) {
-  double bh = (fabs(b) + sqrt(b * b + 4 * a * c)) / 2;
-  return sign * (b * sign <= 0 ? bh / a : c / bh);
-}
-/* secular-equation root in [d[ri], d[ri+1]] (amg_setup.c:2638) */
-static double sec_root(double *y, const double *d, const double *v, int ri, int n) {
-  double dl = d[ri], dr = d[ri + 1], L = dr - dl, x0l = L / 2, x0r = -L / 2;
-  double tol = L;
-  if (fabs(dl) > tol) tol = fabs(dl);
-  if (fabs(dr) > tol) tol = fabs(dr);
-  tol *= EPS;
-  for (;;) {
-    double al = 0, ar = 0, cl = 0, cr = 0, bln = 0, blp = 0, brn = 0, brp = 0, fn = 0, fp = 0;
-    double lambda0, lambda;
-    if (fabs(x0l) == 0 || x0l < 0) { *y = 0; return dl; }
-    if (fabs(x0r) == 0 || x0r > 0) { *y = 0; return dr; }
-    lambda0 = fabs(x0l) < fabs(x0r) ? dl + x0l : dr + x0r;
-    for (int i = 1; i <= ri; ++i) {
-      double den = (d[i] - dl) - x0l, fac = v[i] / den, num = sum_3(d[i], -dr, -2 * x0r);
-      fn += v[i] * fac; fac *= fac; ar += fac;
-      if (num > 0) brp += fac * num; else brn += fac * num;
-      bln += fac * (d[i] - dl);
-      cl += fac * x0l * x0l;
-    }
-    for (int i = ri + 1; i <= n; ++i) {
-      double den = (d[i] - dr) - x0r, fac = v[i] / den, num = sum_3(d[i], -dl, -2 * x0l);
-      fp += v[i] * fac; fac *= fac; al += fac;
-      if (num > 0) blp += fac * num; else bln += fac * num;
-      brp += fac * (d[i] - dr);
-      cr += fac * x0r * x0r;
-    }
-    if (lambda0 > 0) fp += lambda0; else fn += lambda0;
-    if (v[0] < 0) fp -= v[0], blp -= v[0], brp -= v[0];
-    else fn -= v[0], bln -= v[0], brn -= v[0];
-    if (fp + fn > 0) {
-      x0l = rat_root(1 + al, sum_3(dl, blp, bln), cl, 1);
-      lambda = dl + x0l; x0r = x0l - L;
-    } else {
-      x0r = rat_root(1 + ar, sum_3(dr, brp, brn), cr, -1);
-      lambda = dr + x0r; x0l = x0r + L;
-    }
-    if (fabs(lambda - lambda0) < tol) {
-      double ty = 0, fac;
-      for (int i = 1; i <= ri; ++i) fac = v[i] / ((d[i] - dl) - x0l), ty += fac * fac;
-      for (int i = ri + 1; i <= n; ++i) fac = v[i] / ((d[i] - dr) - x0r), ty += fac * fac;
-      *y = 1 / sqrt(1 + ty);
-      return lambda;
-    }
-  }
-}
-static void tdeig(double *lambda, double *y, double *d, const double *v, int n) {
-  double v1 = 0, mn = v[0], mx = v[0];
-  for (int i = 1; i <= n; ++i) {
-    double vi = fabs(v[i]), a = d[i] - vi, b = d[i] + vi;
-    v1 += vi;
-    if (a < mn) mn = a;
-    if (b > mx) mx = b;
-  }
-  d[0] = v[0] - v1 < mn ? v[0] - v1 : mn;
-  d[n + 1] = v[0] + v1 > mx ? v[0] + v1 : mx;
-  for (int i = 0; i <= n; ++i) lambda[i] = sec_root(&y[i], d, v, i, n);
-}
+#include "amgd_hostmath.h"
 
 #define KMAX 299
 static uint32_t lanczos(const dcsr *A, double *out) {
@@ -351,18 +285,6 @@ static uint32_t lanczos(const dcsr *A, double *out) {
   for (uint32_t i = 0; i < k; i++) if (y[i] < 0.01) out[n++] = l[i];
   amgd_free(r); amgd_free(qk); amgd_free(qkm1); amgd_free(Aqk);
   return n;
-}
-
-static void chebsim(double *m, double *c, double rho, double tol) {   /* amg_setup.c:2412 */
-  double alpha = 0.25 * rho * rho, cp = 1, gamma = 1, d, cn;
-  *m = 1; *c = rho;
-  while (*c > tol) {
-    *m += 1;
-    d = alpha * (1 + gamma);
-    gamma = d / (1 - d);
-    cn = (1 + gamma) * rho * (*c) - gamma * cp;
-    cp = *c; *c = cn;
-  }
 }
 
 static double g_pcg_rho, g_pcg_stop;     /* last pcg's final rho and stop level (trace) */
@@ -880,6 +802,7 @@ typedef struct {
 } level_t;
 
 struct amgd_hier {
+  amgd_phier *ph;         /* partitioned mode: the row blocks of this rank (amgd_psetup.c) */
   uint32_t nlevels, cap, n0;
   level_t *lv;
   unsigned long *id;      /* device, level-0 ids 1..n */
@@ -921,6 +844,31 @@ typedef struct {
   amgd_hier *h;          /* the hierarchy under construction (host part freed on failure) */
 } setup_args;
 static int setup_body(void *arg);
+/* partitioned mode: dAi / dAj / dAv are this rank's entries */
+static int psetup_try(void *arg) {
+  setup_args *sa = (setup_args *)arg;
+  memset(&g_st, 0, sizeof g_st);
+  amgd_reset_call_state();
+  amgd_pool_peak_reset();
+  amgd_timer_reset();
+  amgd_spmv_bytes_reset();
+  amgd_spgemm_bytes_reset();
+  amgd_hier *h = (amgd_hier *)calloc(1, sizeof(amgd_hier));
+  sa->h = h;
+  const int rc = amgd_psetup_body(sa->nz, sa->dAi, sa->dAj, sa->dAv, &h->ph, &g_st);
+  h->nlevels = g_st.nlevels;
+  g_st.rap_kernel_ms = amgd_timer_ms(0);
+  g_st.spmv_kernel_ms = amgd_timer_ms(1);
+  g_st.spmv_bytes = amgd_spmv_bytes();
+  g_st.spmv_bytes_strict = amgd_spmv_bytes_strict();
+  g_st.spmv_launches = amgd_spmv_launches();
+  g_st.rap_launches = amgd_spgemm_launches();
+  g_st.rap_bytes = amgd_spgemm_bytes();
+  amgd_spmv_bytes_reset();
+  amgd_spgemm_bytes_reset();
+  g_st.peak_bytes = amgd_pool_peak_bytes();
+  return rc;
+}
 
 /* Out of HBM anywhere in the setup: amgd_try unwinds it, releases every device block
    the setup had allocated, and this returns -2 with the text in amgd_error() (the
@@ -934,9 +882,9 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
     return -1;
   }
   setup_args a = {nz, dAi, dAj, dAv, NULL};
-  int rc = amgd_try(setup_body, &a);
+  int rc = amgd_try(amgd_comm_partitioned() ? psetup_try : setup_body, &a);
   if (rc != 0) {
-    if (a.h) { free(a.h->lv); free(a.h); }
+    if (a.h) { free(a.h->lv); free(a.h); }   /* device blocks: released by the unwind */
     return rc;
   }
   *out = a.h;
@@ -1097,6 +1045,11 @@ static struct csr_mat *csr_to_host(const dcsr *A) {
 API int amgd_hier_export(const amgd_hier *h, struct amg_setup_data *data) {
   amgd_sync();
   double t0 = amgd_wtime();
+  if (h->ph) {
+    const int rc = amgd_phier_export(h->ph, data);
+    g_st.t_copy_ms = (amgd_wtime() - t0) * 1e3;
+    return rc;
+  }
   uint32_t nl = h->nlevels, cap = nl + 1;
   data->tolc = h->tolc;
   data->gamma = h->gamma;
@@ -1150,6 +1103,12 @@ API int amgd_hier_export(const amgd_hier *h, struct amg_setup_data *data) {
 API void amgd_hier_free(amgd_hier **hp) {
   amgd_hier *h = *hp;
   if (!h) return;
+  if (h->ph) {
+    amgd_phier_free(&h->ph);
+    free(h);
+    *hp = NULL;
+    return;
+  }
   for (uint32_t l = 0; l < h->nlevels; l++) {
     level_t *L = &h->lv[l];
     dcsr_free(&L->A); dcsr_free(&L->Af); dcsr_free(&L->W); dcsr_free(&L->AfP);
@@ -1347,8 +1306,11 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
     return NULL;
   }
   struct crs_data *d = (struct crs_data *)calloc(1, sizeof *d);
-  /* entries of every rank: counts (above), then one allgatherv of (i, j, v) */
-  for (int r = 0; r < np; r++) pre[r + 1] = pre[r] + cnt[r];
+  /* entries of every rank: counts (above), then one allgatherv of (i, j, v) -- or, in
+     partitioned mode, each rank hands its own entries to the partitioned setup, which
+     routes them to the owners of their rows (the same rank order for duplicates) */
+  const int part = np > 1 && amgd_comm_partitioned();
+  for (int r = 0; r < np; r++) pre[r + 1] = pre[r] + (part && r != me ? 0 : cnt[r]);
   const uint64_t M = pre[np];
   uint32_t *di = (uint32_t *)amgd_alloc(M * 4 + 4), *dj = (uint32_t *)amgd_alloc(M * 4 + 4);
   double *dv = dalloc(M);
@@ -1356,7 +1318,7 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
   for (amg_uint k = 0; k < m; k++) { hi[k] = (uint32_t)I[k]; hj[k] = (uint32_t)J[k]; }
   amgd_h2d(di + pre[me], hi, m * 4); amgd_h2d(dj + pre[me], hj, m * 4); amgd_h2d(dv + pre[me], V, m * 8);
   free(hi); free(hj); free(I); free(J); free(V);
-  if (np > 1) {
+  if (np > 1 && !part) {
     uint64_t *off = (uint64_t *)malloc(3 * ((size_t)np + 1) * 8);
     void *bufs[3] = {di, dj, dv};
     for (int r = 0; r <= np; r++) {

@@ -1,0 +1,73 @@
+"""One rank of the partitioned-setup tests (tests/test_gpu_partition.py).
+
+Launched N times on the same GPU with RANK / WORLD_SIZE / MASTER_PORT set: gloo group,
+host-staged transport (RCCL refuses two ranks on one device), partitioned mode.  Each
+rank passes only ITS slice of the COO entries (a contiguous 1/N of them, or -- with
+PART_CRS -- its block of rows as a crs_setup local matrix); the library routes them to
+the row owners, builds the row-partitioned hierarchy, and the exported (gathered)
+hierarchy is compared bit for bit with the reference fixture or the stored digest.
+Prints one JSON line (per-rank peak HBM bytes included); exit code 0 = pass."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import omp_amg_amd as oa  # noqa: E402
+from omp_amg_amd import abi, parity, shard  # noqa: E402
+
+
+def main():
+    rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    oa.init(0)
+    case = os.environ["PART_CASE"]
+    out = {"rank": rank, "case": case, "size": size}
+    ref = digest = None
+    if case.startswith("gold:"):
+        z = np.load(os.path.join(HERE, "golden", case[5:] + ".npz"))
+        ref = parity.from_npz(z)
+        Ai, Aj, Av = z["in_Ai"], z["in_Aj"], z["in_Av"]
+    else:
+        import make_digests as md
+        digest = json.load(open(md.OUT))["cases"][case[7:]]
+        Ai, Aj, Av = md.generate(digest["gen"])
+    shard.init_host(rank, size)
+    oa.lib().amgd_comm_set_partitioned(1)
+    shard.stats(reset=True)
+    Ai64, Aj64, Av = np.asarray(Ai, np.int64), np.asarray(Aj, np.int64), np.asarray(Av)
+    if os.environ.get("PART_CRS"):
+        n = int(max(Ai64.max(), Aj64.max())) + 1
+        lo, hi = rank * n // size, (rank + 1) * n // size
+        sel = (Ai64 >= lo) & (Ai64 < hi)
+        ids = np.arange(1, n + 1, dtype=np.uint64)
+        hd = abi.crs_setup(oa.lib(), n, ids, Ai64[sel], Aj64[sel], Av[sel], rank=rank, np_=size)
+        assert hd is not None, "crs_setup returned NULL"
+        h = abi.crs_export(oa.lib(), hd)
+        oa.lib().crs_free(hd)
+    else:
+        nz = len(Av)
+        k0, k1 = rank * nz // size, (rank + 1) * nz // size
+        h = abi.run_setup(oa.lib(), Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+    st = shard.stats()
+    out["peak_bytes"] = int(oa.stats()["peak_bytes"])
+    shard.free()
+    if ref is not None:
+        bad = parity.compare(ref, h, exact=True)
+    else:
+        import make_digests as md
+        got = md.hierarchy_digest(h)
+        exp = digest["arrays"]
+        bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    out.update(calls=st["calls"], bytes=st["bytes"], bad=bad[:5], levels=h.nlevels)
+    print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+    sys.exit(0 if not bad and st["calls"] > 0 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -250,11 +250,11 @@ def _rows_masked(B, m):
     return np.array(ro), np.array(cols, dtype=np.int64), np.array(vals)
 
 
-@pytest.mark.parametrize("wsym", [0, 32768, 65536])
 @pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
-def test_spgemm_symbolic_windows(case, wsym):
-    """symbolic pass of rows with many products: LDS hash (0) or byte-map column windows
-    (several windows per row; A rows past the layer table fall back to the slab recount)"""
+def test_spgemm_symbolic_windows(case):
+    """symbolic pass of rows with many products: the wave-private 4096-column byte windows
+    (k_sg_wwin MODE 0: several windows per row, A rows past 64 layers with cursors in
+    scratch, column clusters far apart)"""
     rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54,
                                  "gapped": 55}[case])
     if case == "wide":
@@ -276,11 +276,9 @@ def test_spgemm_symbolic_windows(case, wsym):
         B = refops.rand_csr(rng, 1400, 3000, 0.03)
     assert B.a.size >= 64 * B.rn
     R = refops.spgemm(A, B)
-    oa.spgemm_wsym(wsym)
-    try:
-        X = oa.test_csr_op(0, A, B)
-    finally:
-        oa.spgemm_wsym(-1)
+    oa.route_stats(reset=True)
+    X = oa.test_csr_op(0, A, B)
+    assert oa.route_stats(reset=True)["sg_wsym"] > 0
     assert refops.same(X, R)
 
 

@@ -1,0 +1,74 @@
+"""The row-partitioned multi-GPU setup (north_star: rows sharded over the
+GPUs, halo rows exchanged before each product).  N processes share the test box's one GPU
+over the host transport (tests/part_worker.py); each passes only its slice of the
+entries, holds only its row blocks of every matrix, and the gathered hierarchy must equal
+the reference's fixture or the oracle digest bit for bit -- the one-GPU parity contract."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(size, case, crs="", timeout=110):
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(size),
+               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8")
+    ps = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "part_worker.py")],
+                           env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True) for r in range(size)]
+    outs = []
+    for p in ps:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in ps:
+                q.kill()
+            raise
+        outs.append((p.returncode, o, e[-3000:]))
+    res = []
+    for rc, o, e in outs:
+        assert rc == 0, (o[-2000:], e)
+        d = json.loads(o.strip().splitlines()[-1])
+        assert not d["bad"] and d["calls"] > 0, d
+        res.append(d)
+    return res
+
+
+@pytest.mark.parametrize("size,case", [(2, "gold:p7_12"), (3, "gold:p27_8"), (2, "gold:sem_e3_N2"),
+                                       (2, "gold:amgdmp"), (4, "gold:aniso_12"), (3, "gold:p7_16x6x5"),
+                                       (2, "gold:sem_e2_N5")],
+                         ids=lambda v: str(v).replace("gold:", ""))
+def test_partitioned_matches_reference_fixture(size, case):
+    """each rank passes 1/size of the entries; the partitioned hierarchy (row blocks of
+    every level, halo products, distributed transposes) is the reference's fixture"""
+    _run(size, case)
+
+
+@pytest.mark.parametrize("size,case", [(3, "digest:p7_48"), (2, "digest:p27_20"), (3, "digest:sem_e4_N7"),
+                                       (2, "digest:aniso_20")],
+                         ids=lambda v: str(v).replace("digest:", ""))
+def test_partitioned_matches_digest(size, case):
+    """larger grids: the gathered partitioned hierarchy hashes to the stored oracle /
+    reference digest (every array of every level)"""
+    _run(size, case, timeout=240)
+
+
+def test_partitioned_crs_setup():
+    """crs_setup(comm = {rank, 3}) in partitioned mode: each rank's local rows go straight
+    to the partitioned setup (no gather of the matrix); the reference fixture bit for bit"""
+    _run(3, "gold:p7_12", crs="1")
