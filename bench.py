@@ -8,11 +8,13 @@ workload: BASELINE.json configs[1] -- 3D 7-point Poisson 256^3 CSR (16.7M rows,
           Galerkin RAP for every level) from a device-resident COO matrix to a
           hierarchy resident in HBM.  Inputs are uploaded before the timed region.
 value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup of
-          the same matrix row-sharded over the N GPUs (--mode shard, default): the
-          heavy row-independent kernels are split by work and completed by RCCL
-          allgatherv over xGMI, value = rows / max-over-ranks seconds, scaling
-          "strong"; --mode replicas runs N independent setups (value = N x rows /
-          max time, scaling "weak").
+          the matrix row-PARTITIONED over the N GPUs (--mode part, default): each rank
+          generates its own rows and holds only its row blocks of every matrix of the
+          hierarchy; products fetch halo rows, transposes exchange row pieces, vectors
+          are completed by allgatherv (RCCL send/recv over xGMI); value = rows /
+          max-over-ranks seconds, scaling "strong".  --mode shard: the round-2
+          replicated hierarchy with sharded kernels; --mode replicas: N independent
+          setups (value = N x rows / max time, scaling "weak").
 roofline: the dominant kernel by time, the long-row SpMV (k_spmv_pipe<false,RW,16>,
           whole-matrix products: find_support's sweeps, PCG, Lanczos), event-timed
           live on the library stream; algorithmic bytes = 12 B per entry + 8 B per
@@ -51,8 +53,10 @@ def parse():
     p.add_argument("--budget-s", type=float, default=450.0,
                    help="wall-time budget of the whole run (s): warmup and timed steps stop early "
                         "when one more step would pass it; `steps`/`warmup` report what ran")
-    p.add_argument("--mode", choices=["shard", "replicas"], default="shard",
-                   help="N>1: one row-sharded setup (strong scaling) or N independent replicas")
+    p.add_argument("--mode", choices=["part", "shard", "replicas"], default="part",
+                   help="N>1: one row-partitioned setup (each rank holds its row blocks of every "
+                        "matrix, halo exchange; strong scaling), the round-2 replicated-hierarchy "
+                        "sharding, or N independent replicas")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                    help="shard mode data path: RCCL over xGMI, or host-staged gloo (rehearsal "
                         "of N ranks on fewer GPUs; ranks share devices round-robin)")
@@ -204,13 +208,20 @@ def main():
     from omp_amg_amd import problems, shard
 
     oa.lib().amgd_init(device)
-    sharded = world > 1 and args.mode == "shard"
+    sharded = world > 1 and args.mode in ("shard", "part")
+    part = world > 1 and args.mode == "part"
     if sharded and args.transport == "host":
         shard.init_host(rank, world)
     elif sharded:
         shard.init_rccl(rank, world)
-    Ai, Aj, Av = problems.poisson3d(args.m, args.stencil)
     rows = args.m ** 3
+    if part:
+        # every rank generates and uploads only its own rows
+        oa.lib().amgd_comm_set_partitioned(1)
+        Ai, Aj, Av = problems.poisson3d(args.m, args.stencil,
+                                        rows_range=(rank * rows // world, (rank + 1) * rows // world))
+    else:
+        Ai, Aj, Av = problems.poisson3d(args.m, args.stencil)
     ds = oa.DeviceSetup(Ai, Aj, Av)
     del Ai, Aj, Av
 
@@ -313,7 +324,10 @@ def main():
             "config": {"workload": f"3D {args.stencil}-point Poisson {args.m}^3 CSR, full AMG setup "
                                    f"(BASELINE configs[1])",
                        "rows": rows, "nnz": int(st["nnz0"]), "levels": int(st["nlevels"]),
-                       "parallelism": (f"rows sharded x{world} (replicated hierarchy, RCCL allgatherv over xGMI)"
+                       "parallelism": (f"rows partitioned x{world} (row blocks of every matrix per rank, "
+                                       f"halo rows before each product, {args.transport.upper()} over xGMI)"
+                                       if part else
+                                       f"rows sharded x{world} (replicated hierarchy, RCCL allgatherv over xGMI)"
                                        if sharded and args.transport == "rccl" else
                                        f"rows sharded x{world} (host-staged gloo rehearsal)" if sharded
                                        else f"replicas x{world}"),
@@ -357,6 +371,8 @@ def main():
                          "algorithmic_bytes_per_setup": rap_bytes / steps,
                          "kernel_ms_per_setup": rap_ms / steps},
         }
+        if part:
+            out["peak_hbm_bytes_rank0"] = int(st["peak_bytes"])
         if comm is not None:
             out["comm_rank0_per_step"] = {"allgatherv_calls": comm["calls"] / steps,
                                           "bytes": comm["bytes"] / steps, "ms": comm["ms"] / steps}

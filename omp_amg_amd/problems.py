@@ -33,19 +33,23 @@ def _stencil_offsets(stencil: int, dim: int):
 
 
 def poisson3d(m: int, stencil: int = 7, eps: float = 1.0, mx: int | None = None,
-              my: int | None = None, dtype_idx=np.uint32):
+              my: int | None = None, dtype_idx=np.uint32, rows_range: tuple | None = None):
     """Dirichlet-eliminated finite-difference Laplacian on an mx*my*m grid.
 
     7-point: diagonal 2(1+1+eps)-ish weights with the z-coupling scaled by eps
     (eps < 1 gives the anisotropic case).  27-point: the trilinear-FE-like stencil
     26 on the diagonal and -1 off it.  Rows are ordered x fastest.
+    rows_range=(r0, r1): only the entries of rows r0..r1-1 -- exactly that slice of the
+    full (row-major sorted) COO, so the slices of all ranks concatenate to the matrix
+    (the partitioned bench: each rank generates its own rows).
     """
     mx = m if mx is None else mx
     my = m if my is None else my
     mz = m
     n = mx * my * mz
     offs = _stencil_offsets(stencil, 3)
-    idx = np.arange(n, dtype=np.int64)
+    r0, r1 = rows_range if rows_range is not None else (0, n)
+    idx = np.arange(r0, r1, dtype=np.int64)
     x = idx % mx
     y = (idx // mx) % my
     z = idx // (mx * my)
