@@ -257,6 +257,7 @@ def main():
     barrier()
     rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, mv_strict, st = 0.0, 0, 0, 0.0, 0, 0, None
     mv_n, rap_n = 0, 0
+    rw_ms, rw_b, rw_n = [0.0] * 3, [0] * 3, [0] * 3
     steps = 0
     if sharded:
         shard.stats(reset=True)
@@ -276,6 +277,10 @@ def main():
         mv_strict += st["spmv_bytes_strict"]
         mv_n += st["spmv_launches"]
         rap_n += st["rap_launches"]
+        for q in range(3):
+            rw_ms[q] += st["spmv_rw_ms"][q]
+            rw_b[q] += st["spmv_rw_bytes_strict"][q]
+            rw_n[q] += st["spmv_rw_launches"][q]
         if rank == 0:
             print(f"[bench] step {steps}: {t_step:.2f} s", file=sys.stderr, flush=True)
     barrier()
@@ -351,6 +356,12 @@ def main():
                          "algorithmic_bytes_def": "12 B per entry (u32 col + f64 a) + 8 B per column (x once) "
                                                   "+ 16 B per row (row offsets, z)",
                          "kernel_ms_per_setup": mv_ms / steps,
+                         "by_shape": {f"RW{rw}": {"ms_per_setup": rw_ms[q] / steps,
+                                                  "launches_per_setup": rw_n[q] / steps,
+                                                  "algorithmic_bytes_per_setup": rw_b[q] / steps,
+                                                  "achieved_gbs": (rw_b[q] / (rw_ms[q] * 1e-3) / 1e9
+                                                                   if rw_ms[q] > 0 else None)}
+                                      for q, rw in enumerate((4, 16, 64))},
                          "pmc_rate_gbs": mv_pmc,
                          "pmc_frac": mv_pmc / HBM_PEAK_GBS if mv_pmc else None,
                          "pmc_over_algorithmic": t_mv * steps / mv_strict if (t_mv and mv_strict) else None,

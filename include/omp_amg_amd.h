@@ -35,6 +35,9 @@ typedef struct {
   uint64_t spmv_bytes;           /* their bytes with x gathered once per entry */
   uint64_t spmv_bytes_strict;    /* their algorithmic HBM bytes: x read once per product */
   uint64_t spmv_launches, rap_launches;   /* kernel launches behind spmv_/rap_kernel_ms */
+  /* the long-row SpMV per shape: RW = 4 / 16 / 64 rows per wavefront (k_spmv_pipe<.., RW>) */
+  double spmv_rw_ms[3];
+  uint64_t spmv_rw_bytes_strict[3], spmv_rw_launches[3];
 } amgd_stats;
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */

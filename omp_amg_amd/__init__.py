@@ -37,7 +37,9 @@ class AmgdStats(C.Structure):
                 ("nlevels", C.c_uint32), ("ub_events", C.c_uint32),
                 ("peak_bytes", C.c_size_t), ("spmv_kernel_ms", C.c_double),
                 ("spmv_bytes", C.c_uint64), ("spmv_bytes_strict", C.c_uint64),
-                ("spmv_launches", C.c_uint64), ("rap_launches", C.c_uint64)]
+                ("spmv_launches", C.c_uint64), ("rap_launches", C.c_uint64),
+                ("spmv_rw_ms", C.c_double * 3), ("spmv_rw_bytes_strict", C.c_uint64 * 3),
+                ("spmv_rw_launches", C.c_uint64 * 3)]
 
 
 class HCsr(C.Structure):
@@ -142,7 +144,11 @@ def amg_setup(Ai, Aj, Av, *, seed: int = 1) -> abi.Hierarchy:
 def stats() -> dict:
     st = AmgdStats()
     lib().amgd_get_stats(C.byref(st))
-    return {f: getattr(st, f) for f, _ in AmgdStats._fields_}
+    out = {}
+    for f, _ in AmgdStats._fields_:
+        v = getattr(st, f)
+        out[f] = list(v) if hasattr(v, "__len__") else v
+    return out
 
 
 class DeviceSetup:

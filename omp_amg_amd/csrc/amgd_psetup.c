@@ -402,9 +402,12 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
   pmat *Rl = pm_copy(R);
   double *onec = dones(nc), *rs = dalloc(nf), *w = dalloc(nc), *w2 = dalloc(nc), *tmp = dalloc(nf);
   double *vv = dalloc(nc), *sumR = dalloc(nc);
-  const uint64_t cap = gnnz(R) + nc + 16;
+  const uint64_t cap = gnnz(R) + nc + 16;      /* the one-GPU driver's guard (UB) */
   uint64_t ns = 0;
-  uint32_t *si = (uint32_t *)amgd_alloc(cap * 4), *sj = (uint32_t *)amgd_alloc(cap * 4);
+  /* the selection lists are whole on every rank: grown as they fill instead of sized
+     nnz(R) up front (that would replicate an nnz-sized buffer on every rank) */
+  uint64_t room = 4ull * nc + 64;
+  uint32_t *si = (uint32_t *)amgd_alloc(room * 4), *sj = (uint32_t *)amgd_alloc(room * 4);
   double theta = 0.5;
   int it = 0;
   if (f1) amgd_d2d(rs, f1->rs, (size_t)nf * 8);
@@ -428,6 +431,13 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
     if (theta == 0) { g_ub++; break; }
     if (nf <= 1) { g_ub++; break; }
     uint32_t nrem = 0;
+    if (ns + nc + 16 > room) {                  /* a sweep selects at most nc entries */
+      const uint64_t r2 = 2 * room + nc + 16;
+      uint32_t *a = (uint32_t *)amgd_alloc(r2 * 4), *b = (uint32_t *)amgd_alloc(r2 * 4);
+      if (ns) { amgd_d2d(a, si, ns * 4); amgd_d2d(b, sj, ns * 4); }
+      amgd_free(si); amgd_free(sj);
+      si = a; sj = b; room = r2;
+    }
     const uint32_t nsel = p_fs_select(Rl, Rt, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     ns += nsel;
     if (nrem == 0) { g_ub++; break; }

@@ -833,6 +833,11 @@ extern uint64_t amgd_spmv_bytes_strict(void);
 extern uint64_t amgd_spmv_launches(void);
 extern uint64_t amgd_spgemm_launches(void);
 extern void amgd_spmv_bytes_reset(void);
+extern void amgd_spmv_rw_counts(uint64_t *bytes, uint64_t *launches);
+static void rw_stats(void) {
+  amgd_spmv_rw_counts(g_st.spmv_rw_bytes_strict, g_st.spmv_rw_launches);
+  for (int i = 0; i < 3; i++) g_st.spmv_rw_ms[i] = amgd_timer_ms(2 + i);
+}
 extern void amgd_spgemm_set_timer(int slot);
 extern void amgd_spgemm_bytes_reset(void);
 extern uint64_t amgd_spgemm_bytes(void);
@@ -864,6 +869,7 @@ static int psetup_try(void *arg) {
   g_st.spmv_launches = amgd_spmv_launches();
   g_st.rap_launches = amgd_spgemm_launches();
   g_st.rap_bytes = amgd_spgemm_bytes();
+  rw_stats();
   amgd_spmv_bytes_reset();
   amgd_spgemm_bytes_reset();
   g_st.peak_bytes = amgd_pool_peak_bytes();
@@ -1022,6 +1028,7 @@ static int setup_body(void *arg) {
   g_st.spmv_bytes_strict = amgd_spmv_bytes_strict();
   g_st.spmv_launches = amgd_spmv_launches();
   g_st.rap_launches = amgd_spgemm_launches();
+  rw_stats();
   amgd_spmv_bytes_reset();
   g_st.rap_bytes = amgd_spgemm_bytes();
   amgd_spgemm_bytes_reset();

@@ -845,10 +845,17 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
 // g_mv_bytes_strict: the same with x read once (8 B per column), the minimum any
 // kernel must move -- the roofline's algorithmic bytes
 static uint64_t g_mv_bytes = 0, g_mv_bytes_strict = 0, g_mv_launches = 0;
+static uint64_t g_rw_bytes[3], g_rw_launches[3];      // per shape RW 4 / 16 / 64 (timer slots 2..4)
+extern "C" void amgd_spmv_rw_counts(uint64_t *bytes, uint64_t *launches) {
+  for (int i = 0; i < 3; i++) { bytes[i] = g_rw_bytes[i]; launches[i] = g_rw_launches[i]; }
+}
 extern "C" uint64_t amgd_spmv_bytes(void) { return g_mv_bytes; }
 extern "C" uint64_t amgd_spmv_bytes_strict(void) { return g_mv_bytes_strict; }
 extern "C" uint64_t amgd_spmv_launches(void) { return g_mv_launches; }
-extern "C" void amgd_spmv_bytes_reset(void) { g_mv_bytes = g_mv_bytes_strict = g_mv_launches = 0; }
+extern "C" void amgd_spmv_bytes_reset(void) {
+  g_mv_bytes = g_mv_bytes_strict = g_mv_launches = 0;
+  for (int i = 0; i < 3; i++) g_rw_bytes[i] = g_rw_launches[i] = 0;
+}
 // AMGD_MVLOG=1: one line per whole-matrix SpMV (rows, nnz, kernel, time, effective GB/s)
 extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                           double beta, const uint8_t *f) {
@@ -944,13 +951,18 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   if (M->nnz >= 32ull * M->rn && spmv_sharded(M, x, z, alpha, y, beta, f)) return;
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
+    const int rwi = lane_rw(M->rn) == 64 ? 2 : lane_rw(M->rn) == 16 ? 1 : 0;
     amgd_timer_start(1);                       // roofline: whole-matrix long-row products
+    amgd_timer_start(2 + rwi);                 // ... and per shape (RW 4 / 16 / 64)
     LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
+    amgd_timer_stop(2 + rwi);
     amgd_timer_stop(1);
     const uint64_t rest = 16ull * M->rn + 8 + (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
     g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
     g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
     g_mv_launches++;
+    g_rw_bytes[rwi] += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
+    g_rw_launches[rwi]++;
   } else if (M->nnz >= 32ull * M->rn) {
     int g = (int)std::min<uint64_t>((M->rn + 3) / 4, 65536);
     k_spmv_wave<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);

@@ -53,6 +53,7 @@ CASES = {
     "aniso_20": ("oracle", {"kind": "poisson3d", "m": 20, "eps": 1e-3}),
     "aniso_24": ("oracle", {"kind": "poisson3d", "m": 24, "eps": 1e-3}),
     "aniso_32": ("oracle", {"kind": "poisson3d", "m": 32, "eps": 1e-3}),
+    "aniso_40": ("oracle", {"kind": "poisson3d", "m": 40, "eps": 1e-3}),
     "aniso_48": ("oracle", {"kind": "poisson3d", "m": 48, "eps": 1e-3}),
     "p27_20": ("oracle", {"kind": "poisson3d", "m": 20, "stencil": 27}),
     "p27_24": ("oracle", {"kind": "poisson3d", "m": 24, "stencil": 27}),
