@@ -72,3 +72,31 @@ def test_partitioned_crs_setup():
     """crs_setup(comm = {rank, 3}) in partitioned mode: each rank's local rows go straight
     to the partitioned setup (no gather of the matrix); the reference fixture bit for bit"""
     _run(3, "gold:p7_12", crs="1")
+
+
+@pytest.mark.parametrize("case", ["p7_48", "p27_20", "sem_e4_N7"])
+def test_partitioned_one_rank_rccl(case):
+    """the partitioned driver with a one-rank RCCL communicator (every partitioned
+    operation on a single block: views, halo builder, transpose assembly, selections) in
+    this process: the stored digest"""
+    import ctypes as C
+    import omp_amg_amd as oa
+    from omp_amg_amd import abi, shard
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_digests as md
+    d = json.load(open(md.OUT))["cases"][case]
+    Ai, Aj, Av = md.generate(d["gen"])
+    oa.init()
+    L = oa.lib()
+    uid = C.create_string_buffer(128)
+    assert L.amgd_comm_rccl_uid(uid) == 0
+    assert L.amgd_comm_init_rccl(0, 1, uid.raw) == 0
+    try:
+        L.amgd_comm_set_partitioned(1)
+        assert L.amgd_comm_partitioned() == 1
+        h = abi.run_setup(L, Ai, Aj, Av)
+    finally:
+        shard.free()
+    got = md.hierarchy_digest(h)
+    bad = sorted(k for k in set(got) | set(d["arrays"]) if got.get(k) != d["arrays"].get(k))
+    assert not bad, bad[:8]
