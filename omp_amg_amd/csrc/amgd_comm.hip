@@ -245,7 +245,12 @@ void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h) {
 }
 
 // per-shard u64 values gathered to every rank (in-place on a device buffer)
+void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m);
 void amgd_allgather_u64(uint64_t *vals_h) {
+  if (g_part) {                                  // partitioned mode: one value per process
+    amgd_pcomm_allgather_u64(vals_h, 1);
+    return;
+  }
   const int N = amgd_nshards();
   int f, l;
   amgd_my_shards(&f, &l);
