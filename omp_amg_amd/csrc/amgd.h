@@ -51,7 +51,8 @@ void amgd_rt_shutdown(void);             /* free everything; pointers become inv
 void amgd_pool_release(void);            /* return every cached block to the driver */
 size_t amgd_pool_bytes_in_use(void);
 size_t amgd_pool_peak_bytes(void);
-void amgd_pool_peak_reset(void);          /* peak := bytes in use now (start of a setup) */
+void amgd_pool_peak_reset(void);
+size_t amgd_pool_ipeak_take(void);        /* peak since the last call, then reset */          /* peak := bytes in use now (start of a setup) */
 void amgd_pool_stats(uint64_t *nmalloc, double *gbytes, double *ms, uint64_t *nrelease);
 void amgd_h2d(void *d, const void *h, size_t n);
 void amgd_d2h(void *h, const void *d, size_t n);
@@ -200,6 +201,11 @@ typedef struct {
 } amgd_csrows;
 int amgd_cs_grow(const dcsr *S, const dcsr *St, uint32_t *front, uint32_t *cnt_d,
                  uint32_t *stamp, uint32_t base8, uint32_t limit, uint32_t *cum);
+/* partitioned mode: one BFS hop of amgd_cs_grow, and the claim of another rank's hop rows */
+void amgd_cs_hop1(const dcsr *S, const dcsr *St, uint32_t *front, uint32_t *cnt_d, int r, uint32_t *stamp,
+                  uint32_t base8, uint32_t limit);
+void amgd_cs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t base8, int r,
+                       uint32_t *front, uint32_t hi0, uint32_t *cntr);
 void amgd_spmv_filt(const dcsr *M, const double *x, double *z, const uint8_t *f,
                     const uint32_t *fs, uint32_t fb, uint32_t fr);
 void amgd_mat_amax_filt(const dcsr *S, const uint8_t *f, double tol, double *amax,
@@ -256,6 +262,9 @@ uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
    returns the count, > cap when the list overflowed */
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,
                         uint32_t tag, uint32_t *out, uint32_t cap);
+/* partitioned mode: ids of another rank's expansion claimed into out (have: entries so far) */
+uint32_t amgd_fs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                           uint32_t have, uint32_t cap);
 uint8_t *amgd_bad_rows(const dcsr *ns, uint32_t *nbad);
 uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_t **pi, uint32_t **pj);
 void amgd_skel_binarize(dcsr *A, int mode);

@@ -275,3 +275,33 @@ extern "C" void amgd_cs_mask3(uint32_t n, const double *m2, const uint8_t *mb, u
                               const amgd_csrows *rows, uint32_t R) {
   CS_LAUNCH(k_cs_mask3, rows, n, R, m2, mb, vc, vf, vfd, anyvc, d0, d0cnt, stamp, next_base8);
 }
+
+// ---------------------------------------------------------------------------
+// Partitioned mode (amgd_psetup.c): the BFS runs on global-row views of S and S^T in
+// which only the rank's own rows hold entries, so each rank expands its own frontier
+// rows; after every hop the ranks' new rows are exchanged and claimed here, so every
+// rank ends each hop with the same set of rows (stamped with the same hop).
+// ---------------------------------------------------------------------------
+extern "C" void amgd_cs_hop1(const dcsr *S, const dcsr *St, uint32_t *front, uint32_t *cnt_d, int r,
+                             uint32_t *stamp, uint32_t base8, uint32_t limit) {
+  const int g = grid_for((uint64_t)S->rn, 256, 4096);
+  k_cs_hop<<<g, 256, 0, amgd_s()>>>(S->ro, S->col, St->ro, St->col, front, cnt_d, r, stamp, base8, limit);
+  KCHECK();
+}
+__global__ void k_cs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t key, uint32_t base8,
+                               uint32_t *front, uint32_t hi0, uint32_t *cntr) {
+  GRID_STRIDE(t, n) {
+    const uint32_t i = ids[t];
+    const uint32_t old = stamp[i];
+    if (old >= base8 || atomicCAS(&stamp[i], old, key) != old) continue;
+    front[hi0 + atomicAdd(cntr, 1u)] = i;
+  }
+}
+// rows ids[0..n) of another rank's hop r: claimed and appended to hop r's segment of
+// front (hi0 = the segment's start, cntr = its count)
+extern "C" void amgd_cs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t base8, int r,
+                                  uint32_t *front, uint32_t hi0, uint32_t *cntr) {
+  if (n) k_cs_claim_ext<<<grid_for(n), 256, 0, amgd_s()>>>(ids, n, stamp, base8 + (uint32_t)r, base8, front, hi0,
+                                                          cntr);
+  KCHECK();
+}

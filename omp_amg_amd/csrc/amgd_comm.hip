@@ -328,24 +328,10 @@ void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, co
     NCCK(R.GroupEnd());
     amgd_sync();
   } else {
-    // every rank's whole send buffer to every rank, then each takes its pieces
-    std::vector<uint64_t> tot(N, 0);
-    tot[me] = soff[N];
-    {
-      std::vector<uint64_t> v(N, 0);
-      v[me] = soff[N];
-      uint64_t *d = (uint64_t *)amgd_alloc(8ull * N + 8);
-      amgd_h2d(d + me, &v[me], 8);
-      std::vector<uint64_t> o(N + 1);
-      for (int q = 0; q <= N; q++) o[q] = 8ull * q;
-      void *b = d;
-      amgd_allgatherv(1, &b, o.data());
-      amgd_d2h(tot.data(), d, 8ull * N);
-      amgd_free(d);
-    }
-    std::vector<uint64_t> base(N + 1, 0), so((size_t)N * (N + 1));
-    for (int q = 0; q < N; q++) base[q + 1] = base[q] + tot[q];
-    // every rank's offsets table, so each can find its piece in every buffer
+    // host transport (tests, several ranks on one GPU): N-1 rounds; in round k every rank
+    // contributes its piece for rank (r + k) mod N to one allgatherv and takes the piece
+    // of rank (r - k) mod N -- staging per round ~1/N of the data, not all of it
+    std::vector<uint64_t> so((size_t)N * (N + 1));
     uint64_t *dt = (uint64_t *)amgd_alloc(8ull * N * (N + 1) + 8);
     amgd_h2d(dt + (size_t)me * (N + 1), soff, 8ull * (N + 1));
     {
@@ -356,28 +342,36 @@ void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, co
     }
     amgd_d2h(so.data(), dt, 8ull * N * (N + 1));
     amgd_free(dt);
-    char *stage = (char *)amgd_alloc(base[N] + 16);
-    if (tot[me]) HIPCK(hipMemcpyAsync(stage + base[me], send, tot[me], hipMemcpyDeviceToDevice, amgd_s()));
-    {
-      std::vector<uint64_t> o(base.begin(), base.end());
-      void *b = stage;
-      amgd_allgatherv(1, &b, o.data());
-    }
-    for (int p = 0; p < N; p++) {
-      if (p == me) continue;
-      const uint64_t *sp = so.data() + (size_t)p * (N + 1);
-      const uint64_t len = sp[me + 1] - sp[me];
-      if (len != roff[p + 1] - roff[p]) {
+    for (int k = 1; k < N; k++) {
+      std::vector<uint64_t> base(N + 1, 0);
+      for (int r = 0; r < N; r++) {
+        const int d = (r + k) % N;
+        const uint64_t *sr = so.data() + (size_t)r * (N + 1);
+        base[r + 1] = base[r] + (sr[d + 1] - sr[d]);
+      }
+      if (base[N] == 0) continue;
+      char *stage = (char *)amgd_alloc(base[N] + 16);
+      const int dst = (me + k) % N, src = (me - k + N) % N;
+      const uint64_t mine = soff[dst + 1] - soff[dst];
+      if (mine) HIPCK(hipMemcpyAsync(stage + base[me], (const char *)send + soff[dst], mine,
+                                     hipMemcpyDeviceToDevice, amgd_s()));
+      {
+        std::vector<uint64_t> o(base.begin(), base.end());
+        void *b = stage;
+        amgd_allgatherv(1, &b, o.data());
+      }
+      const uint64_t len = base[src + 1] - base[src];
+      if (len != roff[src + 1] - roff[src]) {
         fprintf(stderr, "omp_amg_amd: alltoallv: rank %d expects %lu bytes from %d, which sends %lu\n", me,
-                (unsigned long)(roff[p + 1] - roff[p]), p, (unsigned long)len);
+                (unsigned long)(roff[src + 1] - roff[src]), src, (unsigned long)len);
         abort();
       }
-      if (len) HIPCK(hipMemcpyAsync((char *)recv + roff[p], stage + base[p] + sp[me], len,
-                                    hipMemcpyDeviceToDevice, amgd_s()));
+      if (len) HIPCK(hipMemcpyAsync((char *)recv + roff[src], stage + base[src], len, hipMemcpyDeviceToDevice,
+                                    amgd_s()));
       g_bytes += len;
+      amgd_sync();
+      amgd_free(stage);
     }
-    amgd_sync();
-    amgd_free(stage);
   }
   g_ms += (amgd_wtime() - t0) * 1e3;
 }

@@ -2675,3 +2675,27 @@ __global__ void k_scale_diag_match(const uint64_t *ro, const uint32_t *col, doub
 extern "C" void amgd_scale_diag_match(dcsr *W, const double *v, const double *wuc) {
   if (W->rn) k_scale_diag_match<<<grid_for(W->rn), 256, 0, amgd_s()>>>(W->ro, W->col, W->a, W->rn, v, wuc);
 }
+
+// partitioned mode: another rank's expansion rows claimed with the same tag (the union of
+// the ranks' lists; count in *cnt, entries past cap not stored -- as k_fs_expand)
+__global__ void k_fs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                               unsigned *cnt, uint32_t cap) {
+  GRID_STRIDE(t, n) {
+    const uint32_t c = ids[t];
+    if (stamp[c] != tag && atomicExch(&stamp[c], tag) != tag) {
+      const unsigned p = atomicAdd(cnt, 1u);
+      if (p < cap) out[p] = c;
+    }
+  }
+}
+extern "C" uint32_t amgd_fs_claim_ext(const uint32_t *ids, uint64_t n, uint32_t *stamp, uint32_t tag, uint32_t *out,
+                                      uint32_t have, uint32_t cap) {
+  unsigned *cnt = (unsigned *)amgd_alloc(8);
+  amgd_h2d(cnt, &have, 4);
+  if (n) k_fs_claim_ext<<<grid_for(n), 256, 0, amgd_s()>>>(ids, n, stamp, tag, out, cnt, cap);
+  KCHECK();
+  unsigned h = 0;
+  amgd_d2h(&h, cnt, 4);
+  amgd_free(cnt);
+  return h;
+}

@@ -88,6 +88,55 @@ static pmat *p_strength(const pmat *A) {
   amgd_free(D);
   return S;
 }
+/* amgd_cs_grow across the ranks: every hop expands the own rows of the frontier (global
+   views: the other rows are empty here), then the ranks' new rows are exchanged and
+   claimed, so all ranks hold the same hop sets; 0 when a hop passes `limit` (the same
+   decision everywhere: it reads the union's counts) */
+static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t *cnt_d, uint32_t *stamp,
+                     uint32_t base8, uint32_t limit, uint32_t *cum) {
+  uint32_t c[8];
+  uint64_t *cn = (uint64_t *)calloc((size_t)g_N, 8), *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
+  uint64_t *off = (uint64_t *)malloc(((size_t)g_N + 1) * 8);
+  int ok = 1;
+  for (int r = 1; r <= 6 && ok; r++) {
+    amgd_d2h(c, cnt_d, 32);
+    uint32_t hi = 0;
+    for (int q = 0; q < r; q++) hi += c[q];
+    if (hi > limit) { ok = 0; break; }
+    amgd_cs_hop1(gS, gSt, front, cnt_d, r, stamp, base8, limit);
+    amgd_d2h(c, cnt_d, 32);
+    memset(cn, 0, 8ull * g_N);
+    cn[g_me] = c[r];
+    amgd_pcomm_allgather_u64(cn, 1);
+    for (int p = 0; p < g_N; p++) pre[p + 1] = pre[p] + cn[p];
+    if (pre[g_N] == c[r]) continue;                       /* nothing from the others */
+    uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
+    if (c[r]) amgd_d2d(ids + pre[g_me], front + hi, 4ull * c[r]);
+    for (int p = 0; p <= g_N; p++) off[p] = 4 * pre[p];
+    void *b = ids;
+    amgd_allgatherv(1, &b, off);
+    for (int p = 0; p < g_N; p++)
+      if (p != g_me && cn[p]) amgd_cs_claim_ext(ids + pre[p], cn[p], stamp, base8, r, front, hi, cnt_d + r);
+    amgd_free(ids);
+  }
+  free(cn); free(pre); free(off);
+  if (!ok) return 0;
+  amgd_d2h(c, cnt_d, 32);
+  uint32_t t = 0, cu[7];
+  for (int r = 0; r <= 6; r++) {
+    t += c[r];
+    cu[r] = t;
+    if (t > limit) return 0;
+  }
+  for (int r = 0; r <= 6; r++) cum[r] = cu[r];
+  return 1;
+}
+
+/* Incremental sweeps as on one GPU (amgd_coarsen.hip: after the first sweep only the rows
+   within 6 hops of the last sweep's new C points change), always in list mode: every
+   stage runs its list kernel on the global views (the other ranks' rows come out empty)
+   and the owners' values of the listed rows are exchanged (pm_list_sync) -- the same
+   values a full sweep gives, for a fraction of the rows.  AMGD_CS_INC=0: full sweeps. */
 static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
   const uint32_t n = A->rp->n, r0 = A->rp->split[g_me];
   pmat *S = p_strength(A);
@@ -96,19 +145,47 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
   double *vfd = dones(n), *g = dalloc(n), *w1 = dalloc(n), *w2a = dalloc(n), *w2 = dalloc(n);
   double *w = dalloc(n), *x1 = dalloc(n), *x2 = dalloc(n), *m1 = dalloc(n), *m2 = dalloc(n), *amax = dalloc(n);
   uint32_t *anyvc = (uint32_t *)amgd_alloc(4), *stamp = (uint32_t *)amgd_alloc(4ull * n + 4);
-  uint32_t *front = (uint32_t *)amgd_alloc(4ull * n + 4), *cnt = (uint32_t *)amgd_alloc(64);
+  uint32_t *front[2], *cnt[2];
+  for (int q = 0; q < 2; q++) {
+    front[q] = (uint32_t *)amgd_alloc(4ull * n + 4);
+    cnt[q] = (uint32_t *)amgd_alloc(64);
+  }
+  const char *e1 = getenv("AMGD_CS_INC"), *e2 = getenv("AMGD_CS_MIN_ROWS");
+  const uint64_t min_rows = e2 && *e2 ? strtoull(e2, NULL, 10) : 65536;
+  const int inc = !(e1 && *e1 && atoi(e1) == 0) && n >= min_rows && gnnz(S) + gnnz(St) <= 64ull * n;
+  const uint32_t limit = n / 4;
+  dcsr gS, gSt;
+  if (inc) { gS = pm_gview(S); gSt = pm_gview(St); }
   amgd_memset(vc, 0, n);
   amgd_memset(vf, 1, n);
   amgd_memset(anyvc, 0, 4);
   amgd_memset(stamp, 0, 4ull * n);
-  int it = 0;
+  amgd_memset(cnt[0], 0, 64);
+  int it = 0, cur = 0;
   for (;;) {
     it++;
-    pm_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);           /* g   = vf.*(S*vf)  */
-    pm_spmv(S, g, w1, 0.0, NULL, 1.0, vf);            /* w1  = vf.*(S*g)   */
-    pm_spmv(S, w1, w2a, 0.0, NULL, 1.0, vf);          /* w2a = vf.*(S*w1)  */
-    pm_spmv(S, w2a, w2, 0.0, NULL, 1.0, vf);          /* w2  = vf.*(S*w2a) */
-    amgd_cs_w_mask1(n, w1, w2, w, ctol * ctol, g, ma, x1, NULL, 4);
+    amgd_csrows rows_, *rows = NULL;
+    if (inc && it > 1 && p_cs_grow(&gS, &gSt, front[cur], cnt[cur], stamp, 8u * it, limit, rows_.cum)) {
+      rows_.list = front[cur];
+      rows_.fs = stamp;
+      rows_.fb = 8u * it;
+      rows = &rows_;
+      amgd_route_hit(AMGD_R_CS_INC);
+    }
+    const uint32_t *L = rows ? rows->list : NULL;
+#define PSYNC(v, R) pm_list_sync((v), L, rows->cum[(R)], S->rp)
+    if (rows) {
+      amgd_cs_spmv(&gS, vfd, g, vf, rows, 1);  PSYNC(g, 1);
+      amgd_cs_spmv(&gS, g, w1, vf, rows, 2);   PSYNC(w1, 2);
+      amgd_cs_spmv(&gS, w1, w2a, vf, rows, 3); PSYNC(w2a, 3);
+      amgd_cs_spmv(&gS, w2a, w2, vf, rows, 4); PSYNC(w2, 4);
+    } else {
+      pm_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);           /* g   = vf.*(S*vf)  */
+      pm_spmv(S, g, w1, 0.0, NULL, 1.0, vf);            /* w1  = vf.*(S*g)   */
+      pm_spmv(S, w1, w2a, 0.0, NULL, 1.0, vf);          /* w2a = vf.*(S*w1)  */
+      pm_spmv(S, w2a, w2, 0.0, NULL, 1.0, vf);          /* w2  = vf.*(S*w2a) */
+    }
+    amgd_cs_w_mask1(n, w1, w2, w, ctol * ctol, g, ma, x1, rows, 4);
     uint64_t mi = 0;
     double wm = 0;
     double w1m = amgd_max_first2(w1, w, n, &mi, &wm);
@@ -120,21 +197,33 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
       if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
       break;
     }
-    /* Amax rows: local, then whole (the gather reads Amax of any row of S) */
-    amgd_mat_amax(S->m, vf, 0.1, amax + r0);
-    pm_allgather_vec(amax, 8, S->rp);
-    amgd_mat_max_gather(St->m, vf + r0, x1, amax, m1 + r0);
-    pm_allgather_vec(m1, 8, St->rp);
-    amgd_cs_mask2(n, g, m1, ma, mb, x2, NULL, 5);
-    amgd_mat_max_gather(St->m, vf + r0, x2, amax, m2 + r0);
-    pm_allgather_vec(m2, 8, St->rp);
-    amgd_memset(cnt, 0, 64);
-    amgd_cs_mask3(n, m2, mb, vc, vf, vfd, anyvc, front, cnt, stamp, 8u * it + 8, NULL, 6);
+    if (rows) {
+      amgd_cs_amax(&gS, vf, 0.1, amax, rows, 1);              PSYNC(amax, 1);
+      amgd_cs_gather(&gSt, vf, x1, amax, m1, rows, 5);        PSYNC(m1, 5);
+      amgd_cs_mask2(n, g, m1, ma, mb, x2, rows, 5);
+      amgd_cs_gather(&gSt, vf, x2, amax, m2, rows, 6);        PSYNC(m2, 6);
+    } else {
+      /* Amax rows: local, then whole (the gather reads Amax of any row of S) */
+      amgd_mat_amax(S->m, vf, 0.1, amax + r0);
+      pm_allgather_vec(amax, 8, S->rp);
+      amgd_mat_max_gather(St->m, vf + r0, x1, amax, m1 + r0);
+      pm_allgather_vec(m1, 8, St->rp);
+      amgd_cs_mask2(n, g, m1, ma, mb, x2, NULL, 5);
+      amgd_mat_max_gather(St->m, vf + r0, x2, amax, m2 + r0);
+      pm_allgather_vec(m2, 8, St->rp);
+    }
+#undef PSYNC
+    const int nx = cur ^ 1;
+    amgd_memset(cnt[nx], 0, 64);
+    amgd_cs_mask3(n, m2, mb, vc, vf, vfd, anyvc, front[nx], cnt[nx], stamp, 8u * it + 8, rows, 6);
+    cur = nx;
   }
+  if (inc) { pm_gview_free(&gS); pm_gview_free(&gSt); }
   pm_free(&S); pm_free(&St);
   amgd_free(vf); amgd_free(ma); amgd_free(mb); amgd_free(vfd); amgd_free(g); amgd_free(w1);
   amgd_free(w2a); amgd_free(w2); amgd_free(w); amgd_free(x1); amgd_free(x2); amgd_free(m1);
-  amgd_free(m2); amgd_free(amax); amgd_free(anyvc); amgd_free(stamp); amgd_free(front); amgd_free(cnt);
+  amgd_free(m2); amgd_free(amax); amgd_free(anyvc); amgd_free(stamp);
+  for (int q = 0; q < 2; q++) { amgd_free(front[q]); amgd_free(cnt[q]); }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -397,6 +486,34 @@ static uint32_t p_fs_select(pmat *Rl, pmat *Rt, double *rs, const double *w, dou
   *nremoved = (uint32_t)(remall ? 1 : 0);
   return (uint32_t)tot;
 }
+/* amgd_fs_expand across the ranks: the own listed rows' neighbours (global view), then
+   the union of the ranks' lists; > cap when any rank's list or the union overflowed */
+static uint32_t p_fs_expand(const dcsr *gM, const uint32_t *list, uint32_t n, uint32_t *stamp, uint32_t tag,
+                            uint32_t *out, uint32_t cap) {
+  const uint32_t h = amgd_fs_expand(gM, list, n, stamp, tag, out, cap);
+  uint64_t *cn = (uint64_t *)calloc((size_t)g_N, 8), *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
+  cn[g_me] = h;
+  amgd_pcomm_allgather_u64(cn, 1);
+  uint32_t res = h;
+  int over = 0;
+  for (int p = 0; p < g_N; p++) { pre[p + 1] = pre[p] + cn[p]; if (cn[p] > cap) over = 1; }
+  if (over) res = cap + 1;
+  else if (pre[g_N] > h) {
+    uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
+    if (h) amgd_d2d(ids + pre[g_me], out, 4ull * h);
+    uint64_t *off = (uint64_t *)malloc(((size_t)g_N + 1) * 8);
+    for (int p = 0; p <= g_N; p++) off[p] = 4 * pre[p];
+    void *b = ids;
+    amgd_allgatherv(1, &b, off);
+    free(off);
+    for (int p = 0; p < g_N; p++)
+      if (p != g_me && cn[p]) res = amgd_fs_claim_ext(ids + pre[p], cn[p], stamp, tag, out, res, cap);
+    amgd_free(ids);
+  }
+  free(cn); free(pre);
+  return res;
+}
+
 static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_first *f1) {
   const uint32_t nf = R->rp->n, nc = R->cp->n;
   pmat *Rl = pm_copy(R);
@@ -413,13 +530,56 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
   if (f1) amgd_d2d(rs, f1->rs, (size_t)nf * 8);
   else pm_spmv(Rl, onec, rs, 0., NULL, 1., NULL);
   pm_colsum(Rt, sumR);
+  /* incremental sweeps as on one GPU (amgd_setup.c find_support): the listed products run
+     on global views of R and R' (own rows only) and the owners' values are exchanged */
+  const char *e_inc = getenv("AMGD_FS_INC");
+  const int fs_mode = e_inc && *e_inc ? atoi(e_inc) : 1;
+  const int fs_inc = fs_mode == 2 || (fs_mode == 1 && nf >= 4096);
+  const uint32_t cap_c = nc / 4 + 1, cap_r = nf / 4 + 1;
+  uint32_t *st_r = NULL, *st_c = NULL, *L1 = NULL, *L2 = NULL, *L3 = NULL, tag = 0;
+  dcsr gRl, gRt;
+  if (fs_inc) {
+    st_r = (uint32_t *)amgd_alloc((size_t)nf * 4 + 4);
+    st_c = (uint32_t *)amgd_alloc((size_t)nc * 4 + 4);
+    amgd_memset(st_r, 0, (size_t)nf * 4);
+    amgd_memset(st_c, 0, (size_t)nc * 4);
+    L1 = (uint32_t *)amgd_alloc((size_t)cap_c * 4 + 4);
+    L2 = (uint32_t *)amgd_alloc((size_t)cap_r * 4 + 4);
+    L3 = (uint32_t *)amgd_alloc((size_t)cap_c * 4 + 4);
+    gRl = pm_gview(Rl);
+    gRt = pm_gview(Rt);
+  }
+  uint64_t prev_off = 0;
+  uint32_t prev_nsel = 0;
   for (;;) {
     it++;
-    if (it == 1 && f1) {
+    int done = 0;
+    if (fs_inc && it > 1 && prev_nsel <= cap_c) {
+      const uint32_t n1 = p_fs_expand(&gRl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c);
+      if (n1 <= cap_c) {
+        const uint32_t n2 = p_fs_expand(&gRt, L1, n1, st_r, ++tag, L2, cap_r);
+        if (n2 <= cap_r) {
+          const uint32_t n3 = p_fs_expand(&gRl, L2, n2, st_c, ++tag, L3, cap_c);
+          if (n3 <= cap_c) {
+            amgd_spmv_rows(&gRt, L1, n1, rs, w);           /* w  on C1 */
+            pm_list_sync(w, L1, n1, Rt->rp);
+            amgd_spmv_rows(&gRl, L2, n2, w, tmp);          /* tmp on D2 */
+            pm_list_sync(tmp, L2, n2, Rl->rp);
+            amgd_spmv_rows(&gRt, L3, n3, tmp, w2);         /* w2 on C3 */
+            pm_list_sync(w2, L3, n3, Rt->rp);
+            done = 1;
+            amgd_route_hit(AMGD_R_FS_INC);
+          }
+        }
+      }
+    }
+    if (!done && it == 1 && f1) {
       amgd_d2d(w, f1->w, (size_t)nc * 8);
       amgd_d2d(tmp, f1->tmp, (size_t)nf * 8);
       amgd_d2d(w2, f1->w2, (size_t)nc * 8);
-    } else {
+      done = 1;
+    }
+    if (!done) {
       pm_spmvt(Rt, rs, w);
       pm_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       pm_spmvt(Rt, tmp, w2);
@@ -439,12 +599,18 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
       si = a; sj = b; room = r2;
     }
     const uint32_t nsel = p_fs_select(Rl, Rt, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    prev_off = ns;
+    prev_nsel = nsel;
     ns += nsel;
     if (nrem == 0) { g_ub++; break; }
     if (ns + nc > cap) { g_ub++; break; }
   }
   pmat *Sk = pm_coo_ones(si, sj, ns, R->rp, R->cp);
   if (verbose()) printf("    find_support: %d sweeps, %lu entries\n", it, (unsigned long)ns);
+  if (fs_inc) {
+    pm_gview_free(&gRl); pm_gview_free(&gRt);
+    amgd_free(st_r); amgd_free(st_c); amgd_free(L1); amgd_free(L2); amgd_free(L3);
+  }
   pm_free(&Rl); pm_free(&Rt);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);
@@ -630,6 +796,23 @@ static void add_time(double *acc, double *t0) {
   *acc += (t - *t0) * 1e3;
   *t0 = t;
 }
+/* AMGD_PHASES=1: per level the pool peak (GB) inside coarsen / smoother / interpolation /
+   RAP on every rank (stderr) -- where a rank's HBM peak sits */
+static int g_pph = -1;
+static double g_pk[64][4];
+static void pk_mark(uint32_t level, int ph) {
+  if (g_pph < 0) { const char *e = getenv("AMGD_PHASES"); g_pph = e && *e && *e != '0'; }
+  if (!g_pph || level >= 64) return;
+  const double pk = amgd_pool_ipeak_take() / 1e9;
+  if (pk > g_pk[level][ph]) g_pk[level][ph] = pk;
+}
+static void pk_report(uint32_t nl) {
+  if (g_pph <= 0) return;
+  fprintf(stderr, "rank %d pool peak GB per level: coarsen smoother interp rap\n", g_me);
+  for (uint32_t l = 0; l < nl && l < 64; l++)
+    fprintf(stderr, "rank %d L%u %8.3f %8.3f %8.3f %8.3f\n", g_me, l, g_pk[l][0], g_pk[l][1], g_pk[l][2], g_pk[l][3]);
+  memset(g_pk, 0, sizeof g_pk);
+}
 
 __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const uint32_t *dAi,
                                                            const uint32_t *dAj, const double *dAv,
@@ -638,6 +821,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
   g_N = amgd_pcomm_size();
   g_ub = 0;
   g_lmop_full = 0;
+  (void)amgd_pool_ipeak_take();
   amgd_sync();
   double t_start = amgd_wtime(), t0 = t_start;
   /* level 0: the global size, the even split, the entries to the owners of their rows,
@@ -699,6 +883,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     amgd_u8_not(vc, vf, n);
     L->vc = vc;
     add_time(&st->t_coarsen_ms, &t0);
+    pk_mark(level, 0);
     apart *Pf = apart_induced(Pn, vf), *Pc = apart_induced(Pn, vc);
     L->Pf = Pf;
     pmat *Af = pm_sub_mat(A, vf, vf, Pf, Pf);
@@ -730,6 +915,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     L->D = D;
     L->Af = Af;
     add_time(&st->t_smoother_ms, &t0);
+    pk_mark(level, 1);
     pmat *Afc = pm_sub_mat(A, vf, vc, Pf, Pc), *Ac = pm_sub_mat(A, vc, vc, Pc, Pc);
     const uint32_t rnc = Pc->n;
     L->idc = (unsigned long *)amgd_alloc((size_t)rnc * 8 + 8);
@@ -738,6 +924,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     pmat *W = p_interpolation(Af, Ac, Afc, gamma2, itol);
     L->W = W;
     add_time(&st->t_interp_ms, &t0);
+    pk_mark(level, 2);
     /* Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) (amg_setup.c:339-372) */
     pmat *Acf = pm_transpose(Afc);
     amgd_spgemm_set_timer(0);
@@ -756,12 +943,14 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     pm_free(&Afc); pm_free(&Ac);
     amgd_free(vf);
     add_time(&st->t_rap_ms, &t0);
+    pk_mark(level, 3);
     Pn = Pc;
     level++;
   }
   h->nlevels = level + 1;
   amgd_sync();
   st->t_total_ms = (amgd_wtime() - t_start) * 1e3;
+  pk_report(h->nlevels);
   st->ub_events = (uint32_t)g_ub;
   st->nlevels = h->nlevels;
   if (verbose() && g_lmop_full)

@@ -91,7 +91,7 @@ static std::multimap<size_t, size_t> g_free_sz;      // size -> offset
 struct UsedBlock { size_t sz; uint64_t serial; };
 static std::unordered_map<void *, UsedBlock> g_used; // live block -> size, allocation serial
 static std::unordered_map<void *, size_t> g_direct;  // live hipMalloc fallbacks -> size
-static size_t g_inuse = 0, g_peak = 0;
+static size_t g_inuse = 0, g_peak = 0, g_ipeak = 0;
 static uint64_t g_serial = 0;                         // allocations made so far
 static size_t g_cap = (size_t)-1;                    // AMGD_HBM_CAP_GB / amgd_set_hbm_cap
 static int g_cap_read = 0, g_try_depth = 0;
@@ -216,6 +216,7 @@ extern "C" void *amgd_alloc(size_t bytes) {
   g_used[p] = UsedBlock{sz, g_serial++};
   g_inuse += sz;
   if (g_inuse > g_peak) g_peak = g_inuse;
+  if (g_inuse > g_ipeak) g_ipeak = g_inuse;
   return p;
 }
 
@@ -249,6 +250,12 @@ extern "C" void amgd_pool_release(void) {
 extern "C" size_t amgd_pool_bytes_in_use(void) { return g_inuse; }
 extern "C" size_t amgd_pool_peak_bytes(void) { return g_peak; }
 extern "C" void amgd_pool_peak_reset(void) { g_peak = g_inuse; }
+// the peak since the last call (phase tables: which phase holds the setup's peak)
+extern "C" size_t amgd_pool_ipeak_take(void) {
+  const size_t p = g_ipeak;
+  g_ipeak = g_inuse;
+  return p;
+}
 
 extern "C" void amgd_h2d(void *d, const void *h, size_t n) {
   if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, amgd_s()));

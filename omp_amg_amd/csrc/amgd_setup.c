@@ -74,6 +74,7 @@ static const char *ph_name[PH_N] = {"coarsen", "smoother", "interp0", "qfactor",
                                     "fs_max", "fs_sel", "expand", "exp_R0", "final", "rap"};
 #define PH_MAXL 64
 static double g_ph[PH_MAXL][PH_N], g_ph_t;
+static double g_phpk[PH_MAXL][PH_N];      /* GB: pool peak inside the phase */
 static int g_phases = -1;
 static int phases_on(void) {
   if (g_phases < 0) { const char *e = getenv("AMGD_PHASES"); g_phases = e && *e && *e != '0'; }
@@ -83,7 +84,11 @@ static void ph(int id) {
   if (!phases_on()) return;
   amgd_sync();
   double t = amgd_wtime();
-  if (id >= 0 && g_lvl < PH_MAXL) g_ph[g_lvl][id] += (t - g_ph_t) * 1e3;
+  const double pk = amgd_pool_ipeak_take() / 1e9;
+  if (id >= 0 && g_lvl < PH_MAXL) {
+    g_ph[g_lvl][id] += (t - g_ph_t) * 1e3;
+    if (pk > g_phpk[g_lvl][id]) g_phpk[g_lvl][id] = pk;
+  }
   g_ph_t = t;
 }
 static void ph_report(uint32_t nl) {
@@ -99,7 +104,14 @@ static void ph_report(uint32_t nl) {
   }
   fprintf(stderr, "sum");
   for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9.1f", tot[p]);
+  fprintf(stderr, "\nphase peak GB (pool in use, max inside the phase):\nlvl");
+  for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9s", ph_name[p]);
   fprintf(stderr, "\n");
+  for (uint32_t l = 0; l < nl && l < PH_MAXL; l++) {
+    fprintf(stderr, "%3u", l);
+    for (int p = 0; p < PH_N; p++) fprintf(stderr, " %9.2f", g_phpk[l][p]);
+    fprintf(stderr, "\n");
+  }
   uint64_t nm, nr;
   double gb, ms;
   amgd_pool_stats(&nm, &gb, &ms, &nr);
@@ -1019,7 +1031,7 @@ static int setup_body(void *arg) {
   }
   h->nlevels = level + 1;
   ph_report(h->nlevels);
-  if (phases_on()) memset(g_ph, 0, sizeof g_ph);
+  if (phases_on()) { memset(g_ph, 0, sizeof g_ph); memset(g_phpk, 0, sizeof g_phpk); }
   amgd_sync();
   g_st.t_total_ms = (amgd_wtime() - t_start) * 1e3;
   g_st.rap_kernel_ms = amgd_timer_ms(0);

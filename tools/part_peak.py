@@ -87,6 +87,8 @@ def main():
     if r.returncode:
         sys.exit(r.stderr[-3000:])
     one = json.loads(r.stdout.strip().splitlines()[-1])
+    one["phase_peaks"] = [l for l in r.stderr.splitlines() if l[:3].strip().isdigit() or l.startswith("lvl")
+                          or "peak" in l][-24:]
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -104,7 +106,9 @@ def main():
             for x in ps:
                 x.kill()
             sys.exit(f"rank failed rc={q.returncode}: {e[-3000:]}")
-        ranks.append(json.loads(o.strip().splitlines()[-1]))
+        d = json.loads(o.strip().splitlines()[-1])
+        d["phase_peaks"] = [l for l in e.splitlines() if l.startswith("rank")][-20:]
+        ranks.append(d)
     peak = max(r["peak_bytes"] for r in ranks)
     res = {"workload": f"3D {a.stencil}-point Poisson {a.m}^3", "ranks": a.N, "one_gpu": one,
            "partitioned": ranks, "max_rank_peak_bytes": peak,
