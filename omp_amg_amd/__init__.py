@@ -100,6 +100,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
+        L.amgd_test_sg_xcd.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -410,6 +411,12 @@ def lmop_wave(n: int) -> None:
     walk one wavefront per (c, k) with 64 columns searched at once (default 64), 0 one
     thread per (c, k) always, -1 default / AMGD_LMOP_WAVE.  Same landings."""
     lib().amgd_test_lmop_wave(int(n))
+
+
+def sg_xcd(mask: int) -> None:
+    """SpGEMM work-groups in XCD-contiguous order (bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row;
+    0 the hardware's round-robin order, -1 back to AMGD_SG_XCD).  Same bits."""
+    lib().amgd_test_sg_xcd(int(mask))
 
 
 def sg_pattern(on: int) -> None:

@@ -109,7 +109,7 @@ static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t 
     cn[g_me] = c[r];
     amgd_pcomm_allgather_u64(cn, 1);
     for (int p = 0; p < g_N; p++) pre[p + 1] = pre[p] + cn[p];
-    if (pre[g_N] == c[r]) continue;                       /* nothing from the others */
+    if (pre[g_N] == 0) continue;          /* (a global condition: every rank takes part) */
     uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
     if (c[r]) amgd_d2d(ids + pre[g_me], front + hi, 4ull * c[r]);
     for (int p = 0; p <= g_N; p++) off[p] = 4 * pre[p];
@@ -498,7 +498,7 @@ static uint32_t p_fs_expand(const dcsr *gM, const uint32_t *list, uint32_t n, ui
   int over = 0;
   for (int p = 0; p < g_N; p++) { pre[p + 1] = pre[p] + cn[p]; if (cn[p] > cap) over = 1; }
   if (over) res = cap + 1;
-  else if (pre[g_N] > h) {
+  else if (pre[g_N] > 0) {                      /* global condition: every rank takes part */
     uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
     if (h) amgd_d2d(ids + pre[g_me], out, 4ull * h);
     uint64_t *off = (uint64_t *)malloc(((size_t)g_N + 1) * 8);

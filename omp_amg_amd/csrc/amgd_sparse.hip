@@ -24,6 +24,17 @@
 #include "amgd.h"
 #include "amgd_dev.h"
 
+// XCD-contiguous block order (AMGD_SG_XCD bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row): the
+// hardware deals work-groups to the 8 XCDs round robin (blockIdx % 8); remapped, XCD x runs
+// one contiguous run of the row list, so neighbouring output rows -- which read mostly the
+// same B rows -- share that XCD's L2 (RAP kernels at 7-29 % L2 hit rate)
+__device__ int d_sg_xcd = 0;
+__device__ __forceinline__ uint32_t xcd_block(int bit) {
+  const uint32_t b = blockIdx.x, G = gridDim.x;
+  if (!(d_sg_xcd & bit) || G < 16) return b;
+  const uint32_t x = b & 7, i = b >> 3, q = G >> 3, r = G & 7;
+  return x * q + (x < r ? x : r) + i;
+}
 static int bits_for(uint64_t v) {  // bits needed to represent v
   int b = 0;
   while (b < 64 && (v >> b) != 0) b++;
@@ -1630,7 +1641,7 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
   __shared__ unsigned nfill;
   __shared__ int ovf;
   const int t = threadIdx.x;
-  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+  for (uint32_t r = xcd_block(4); r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     for (uint32_t s = t; s < S; s += NT) {
       hk[s] = EMPTY_KEY;
@@ -1766,7 +1777,7 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
   __shared__ unsigned nfill;
   __shared__ int ovf;
   const int t = threadIdx.x;
-  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+  for (uint32_t r = xcd_block(2); r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     for (uint32_t s = t; s < S; s += NT) {
       hk[s] = EMPTY_KEY;
@@ -1954,6 +1965,14 @@ static bool sg_force_flat() {
   return g_sg_flat == 1;
 }
 extern "C" void amgd_spgemm_force_flat(int on) { g_sg_flat = on ? 1 : 0; }
+static int g_sg_xcd = -1;     // host copy of d_sg_xcd (-1: not yet read from AMGD_SG_XCD)
+extern "C" void amgd_spgemm_set_xcd(int m) {
+  if (m < 0) { const char *e = getenv("AMGD_SG_XCD"); m = e && *e ? atoi(e) : 0; }
+  if (m == g_sg_xcd) return;
+  g_sg_xcd = m;
+  HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_sg_xcd), &m, sizeof(int), 0, hipMemcpyHostToDevice, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+}
 static int g_sg_win_forced = 0; // tests: the window applies whatever the column count
 static int g_sg_win = -1;       // AMGD_SG_WIN: window of the dense-accumulator kernel (0: off)
 static int sg_win() {
@@ -2115,7 +2134,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
   // curs holds nnz(A) cursors from A's first entry: a row-range view of a larger matrix
   // (sharded products) keeps absolute row offsets
   const uint64_t cbase = aro[0];
-  for (uint32_t r = blockIdx.x * NWV + wv; r < nrows; r += gridDim.x * NWV) {
+  for (uint32_t r = xcd_block(1) * NWV + wv; r < nrows; r += gridDim.x * NWV) {
     const uint32_t i = rows[r];
     const uint64_t a0 = aro[i];
     const uint32_t nl = (uint32_t)(aro[i + 1] - a0);
@@ -2296,6 +2315,7 @@ __global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *ar
   }
 }
 static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
+  if (g_sg_xcd < 0) amgd_spgemm_set_xcd(-1);
   if (A->cn != B->rn) {
     fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
     abort();

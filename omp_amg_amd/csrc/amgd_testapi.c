@@ -193,6 +193,9 @@ void amgd_lmop_set_small(int n);
 API void amgd_test_lmop_small(int n) { amgd_lmop_set_small(n); }
 void amgd_lmop_set_wave(int n);
 API void amgd_test_lmop_wave(int n) { amgd_lmop_set_wave(n); }
+void amgd_spgemm_set_xcd(int m);
+/* XCD-contiguous block order of the SpGEMM kernels (bits 1 wwin, 2 kseq, 4 row; -1: env) */
+API void amgd_test_sg_xcd(int m) { amgd_spgemm_set_xcd(m); }
 void amgd_spgemm_set_pattern(int on);
 API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }
 /* Q factors taken by copy from the previous iteration / factored, since the last call */

@@ -24,10 +24,10 @@ def _free_port():
     return p
 
 
-def _run(size, case, crs="", timeout=110):
+def _run(size, case, crs="", timeout=110, extra_env=None):
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(size),
-               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8")
+               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8", **(extra_env or {}))
     ps = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "part_worker.py")],
                            env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            text=True) for r in range(size)]
@@ -41,6 +41,9 @@ def _run(size, case, crs="", timeout=110):
             raise
         outs.append((p.returncode, o, e[-3000:]))
     res = []
+    if any(rc != 0 for rc, _, _ in outs):
+        # every rank's tail: the first failing rank is usually not rank 0
+        raise AssertionError("\n".join(f"--- rank {r} rc={rc}\n{o[-1500:]}\n{e}" for r, (rc, o, e) in enumerate(outs)))
     for rc, o, e in outs:
         assert rc == 0, (o[-2000:], e)
         d = json.loads(o.strip().splitlines()[-1])
@@ -62,10 +65,12 @@ def test_partitioned_matches_reference_fixture(size, case):
 @pytest.mark.parametrize("size,case", [(3, "digest:p7_48"), (2, "digest:p27_20"), (3, "digest:sem_e4_N7"),
                                        (2, "digest:aniso_20")],
                          ids=lambda v: str(v).replace("digest:", ""))
-def test_partitioned_matches_digest(size, case):
+@pytest.mark.parametrize("inc", ["1", "0"], ids=["inc", "full_sweeps"])
+def test_partitioned_matches_digest(size, case, inc):
     """larger grids: the gathered partitioned hierarchy hashes to the stored oracle /
-    reference digest (every array of every level)"""
-    _run(size, case, timeout=240)
+    reference digest (every array of every level); incremental coarsening / find_support
+    sweeps across the ranks (default) and full sweeps"""
+    _run(size, case, timeout=240, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
 
 
 def test_partitioned_crs_setup():
