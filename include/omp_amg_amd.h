@@ -38,7 +38,11 @@ typedef struct {
   /* the long-row SpMV per shape: RW = 4 / 16 / 64 rows per wavefront (k_spmv_pipe<.., RW>) */
   double spmv_rw_ms[3];
   uint64_t spmv_rw_bytes_strict[3], spmv_rw_launches[3];
+  /* the first AMGD_UB_LOG reference-undefined events: site (1 find_support theta -> 0, 2 one-row R,
+     3 a sweep removed nothing, 4 selections past nnz(R) + nc, 5 skeleton stalled) and level */
+  uint8_t ub_site[8], ub_level[8];
 } amgd_stats;
+#define AMGD_UB_LOG 8
 
 int amgd_init(int device);                       /* 0 = ok; <0 = no usable HIP device */
 /* release every device buffer, event and the stream of the library (hierarchies

@@ -39,7 +39,8 @@ class AmgdStats(C.Structure):
                 ("spmv_bytes", C.c_uint64), ("spmv_bytes_strict", C.c_uint64),
                 ("spmv_launches", C.c_uint64), ("rap_launches", C.c_uint64),
                 ("spmv_rw_ms", C.c_double * 3), ("spmv_rw_bytes_strict", C.c_uint64 * 3),
-                ("spmv_rw_launches", C.c_uint64 * 3)]
+                ("spmv_rw_launches", C.c_uint64 * 3),
+                ("ub_site", C.c_uint8 * 8), ("ub_level", C.c_uint8 * 8)]
 
 
 class HCsr(C.Structure):

@@ -246,6 +246,8 @@ uint32_t *amgd_lmop_kpos(const dcsr *Wt, const uint64_t *perm);
 void amgd_lmop_stats(uint64_t *out);   /* fast, general, dirty-prefix calls, misses, pruned supports */
 void amgd_lmop_stats_reset(void);
 void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
+void amgd_lmop_spill_detect(int on);   /* partitioned mode: flag walks past the view's last row */
+int amgd_lmop_spilled(void);
 void amgd_qfactor_set_sparse(int m);   /* huge supports: 0 dense, 1 sparse first, 2 tiny capacity */
 void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] since the last call */
 /* one find_support sweep: select/remove, then re-sum rs (rows) and sumR (columns) that lost

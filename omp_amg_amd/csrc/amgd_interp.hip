@@ -1622,6 +1622,25 @@ extern "C" void amgd_qapply(const dcsr *Wt, const double *Q, const uint64_t *qof
 // here each step is a lower_bound inside the current row plus, when the row
 // is exhausted, a skip over whole rows using per-row / per-64-row /
 // per-4096-row column maxima -- the same landing, O(log) instead of O(nnz).
+// Partitioned mode (amgd_psetup.c p_lmop): S is a rank's global-row view (other ranks' rows
+// empty).  A walk that starts in another rank's row finds it empty and lands nowhere -- its
+// owner lands it -- but a walk that runs past this rank's last row would, in the whole S,
+// go on into the next rank's rows: it is flagged here (d_lmop_spill) and the caller redoes
+// the operator on gathered data.  Off on one GPU and on the last rank (the end of S is the
+// end of S there: the reference's UB, skipped as before).
+__device__ int d_lmop_spill_on = 0, d_lmop_spill = 0;
+extern "C" void amgd_lmop_spill_detect(int on) {
+  int z = 0;
+  HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_lmop_spill_on), &on, sizeof(int), 0, hipMemcpyHostToDevice, amgd_s()));
+  HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_lmop_spill), &z, sizeof(int), 0, hipMemcpyHostToDevice, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+}
+extern "C" int amgd_lmop_spilled(void) {
+  int v = 0;
+  HIPCK(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(d_lmop_spill), sizeof(int), 0, hipMemcpyDeviceToHost, amgd_s()));
+  HIPCK(hipStreamSynchronize(amgd_s()));
+  return v;
+}
 __device__ __forceinline__ uint64_t lower_bound_u32(const uint32_t *a, uint64_t lo, uint64_t hi,
                                                     uint32_t x) {
   while (lo < hi) {
@@ -1693,7 +1712,10 @@ __global__ void k_lmop_land(const uint32_t *erow, uint64_t e0, uint64_t e1, cons
           land = lower_bound_u32(scol, t, end, xm);
         } else {
           uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xm);
-          if (r2 >= srn) live = false;       // reference runs off the end of St (UB)
+          if (r2 >= srn) {                   // reference runs off the end of St (UB)
+            live = false;
+            if (d_lmop_spill_on) d_lmop_spill = 1;
+          }
           else { r = r2; land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xm); }
         }
         // next step starts after the landing; if that is the end of row r, the
@@ -1761,6 +1783,7 @@ __global__ __launch_bounds__(256) void k_lmop_land_wave(
         const uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xf);
         uint64_t land = snnz;
         if (r2 >= srn) {
+          if (d_lmop_spill_on) d_lmop_spill = 1;
           live = false;                               // reference runs off the end of St (UB)
         } else {
           r = r2;
@@ -1928,7 +1951,10 @@ __global__ void k_lmop_land_pr(const uint32_t *Qj, uint32_t nz, const uint64_t *
           land = lower_bound_u32(scol, t, end, xm);
         } else {
           const uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xm);
-          if (r2 >= srn) live = false;
+          if (r2 >= srn) {
+            live = false;
+            if (d_lmop_spill_on) d_lmop_spill = 1;
+          }
           else { r = r2; land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xm); }
         }
         if (live) t = land + 1;

@@ -423,18 +423,16 @@ extern "C" void amgd_lmop_stats(uint64_t *out) { for (int i = 0; i < 5; i++) out
 extern "C" void amgd_lmop_stats_reset(void) { for (int i = 0; i < 5; i++) g_lmop_stats[i] = 0; }
 extern "C" void amgd_lmop_note_pruned(void) { g_lmop_stats[4]++; }
 
-// Partitioned mode (amgd_comm_partitioned()): S and Wskel are a rank's rows, Wt / Q / qoff
-// the supports those rows reference (global coarse index); the general walk needs all of
-// S, so where it would run this returns 1 (before touching S) or 2 (a clean contribution
-// missed its column) and the caller redoes the operator on gathered data.  0: done.
+// Partitioned mode (amgd_psetup.c p_lmop): S and Wskel are global-row views of a rank's
+// rows, Wt / Q / qoff the supports those rows reference; every path below then computes
+// exactly this rank's rows (walks starting in other ranks' rows find them empty), and a walk
+// that would run into the next rank's rows is flagged (amgd_lmop_spill_detect).  Returns 0.
 extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt,
                          const double *Q, const uint64_t *qoff, const double *u) {
   hipStream_t s = amgd_s();
-  const bool part = amgd_comm_partitioned() != 0;
   amgd_memset(S->a, 0, S->nnz * 8);
   const uint32_t nc = Wt->rn;
   if (nc == 0 || Wt->nnz == 0 || S->nnz == 0) return 0;
-  if (part && (lmop_mode() == 1 || kpos == nullptr)) return 1;
   if (lmop_mode() == 1 || kpos == nullptr) {
     g_lmop_stats[1]++;
     amgd_lmop_general(S, Wt, Q, qoff, u, 0, nc);
@@ -448,10 +446,6 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
   KCHECK();
   amgd_d2h(hst, st, 8);
   const uint32_t dend = hst[0], cmin = hst[1];
-  if (part && (cmin == 0xffffffffu || dend > 0)) {
-    amgd_free(dirty); amgd_free(st);
-    return 1;
-  }
   if (cmin == 0xffffffffu || (dend > 0 && dend - 1 > cmin)) {
     // no clean point, or a dirty point after a clean one: order needs the general walk
     g_lmop_stats[1]++;
@@ -557,11 +551,6 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
       void *b = S->a;
       amgd_allgatherv(1, &b, off.data());
     }
-  }
-  if (hm && part) {
-    amgd_free(rl); amgd_free(rc); amgd_free(sz); amgd_free(lc); amgd_free(tp); amgd_free(lcnt);
-    amgd_free(miss); amgd_free(dirty); amgd_free(st);
-    return 2;
   }
   if (hm) {
     // a clean contribution missed its column: S is not W_skel*W_skel' -- redo exactly

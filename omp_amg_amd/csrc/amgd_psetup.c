@@ -44,6 +44,13 @@ static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0)
 
 static int g_me, g_N;
 static uint64_t g_ub;
+static amgd_stats *g_pst;             /* the stats being filled (ub sites) */
+static int g_plvl;
+static void ub_note(int site) {      /* site codes: amgd_setup.c ub_note */
+  if (g_ub < AMGD_UB_LOG) { g_pst->ub_site[g_ub] = (uint8_t)site; g_pst->ub_level[g_ub] = (uint8_t)g_plvl; }
+  g_ub++;
+}
+#define UB(site) ub_note(site)
 static int g_verbose = -1;
 static int verbose(void) {
   if (g_verbose < 0) { const char *e = getenv("AMGD_VERBOSE"); g_verbose = e && *e && *e != '0'; }
@@ -354,10 +361,17 @@ static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u
   pmat qp = {&qm, f->Wt->rp, f->Wt->cp};
   dcsr *QE = pm_halo_rows(&qp, Wskel->m);
   uint32_t *kpos = pm_kpos(Wskel, WtE);
-  const int st = amgd_lmop(S->m, Wskel->m, kpos, WtE, QE->a, QE->ro, u);
-  amgd_free(kpos);
-  dcsr_free(&WtE);
-  dcsr_free(&QE);
+  /* global-row views of the own rows of S and W_skel: the fast path, the dirty-prefix and
+     general walks all run on them; only a walk running into the next rank's rows needs
+     the whole operator (flagged; never on the last rank) */
+  dcsr gS = pm_gview(S), gW = pm_gview(Wskel);
+  const int last = S->rp->split[g_me + 1] == S->rp->n;
+  amgd_lmop_spill_detect(!last);
+  amgd_lmop(&gS, &gW, kpos, WtE, QE->a, QE->ro, u);
+  const int st = last ? 0 : amgd_lmop_spilled();
+  amgd_lmop_spill_detect(0);
+  pm_gview_free(&gS);
+  pm_gview_free(&gW);
   if (all_max((uint64_t)st) != 0) {
     g_lmop_full++;
     dcsr *Sf = pm_gather_full(S), *Wsf = pm_gather_full(Wskel), *Qf = pm_gather_full(&qp);
@@ -588,8 +602,8 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
     double mv = amgd_max_first(vv, nc, NULL), mw = mv;
     if (mv < goal || mw < goal) break;
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
-    if (theta == 0) { g_ub++; break; }
-    if (nf <= 1) { g_ub++; break; }
+    if (theta == 0) { UB(1); break; }
+    if (nf <= 1) { UB(2); break; }
     uint32_t nrem = 0;
     if (ns + nc + 16 > room) {                  /* a sweep selects at most nc entries */
       const uint64_t r2 = 2 * room + nc + 16;
@@ -602,8 +616,8 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
-    if (nrem == 0) { g_ub++; break; }
-    if (ns + nc > cap) { g_ub++; break; }
+    if (nrem == 0) { UB(3); break; }
+    if (ns + nc > cap) { UB(4); break; }
   }
   pmat *Sk = pm_coo_ones(si, sj, ns, R->rp, R->cp);
   if (verbose()) printf("    find_support: %d sweeps, %lu entries\n", it, (unsigned long)ns);
@@ -736,7 +750,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
       printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)wsk, (unsigned long)n, sqrt(gamma2),
              sqrt(maxr)), fflush(stdout);
     int stalled = prev_nnz == wsk;
-    if (stalled) g_ub++;
+    if (stalled) UB(5);
     prev_nnz = wsk;
     if (n == 0 || w1m <= gamma2 || stalled) {
       pm_free(&Rt);
@@ -820,6 +834,8 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
   g_me = amgd_pcomm_rank();
   g_N = amgd_pcomm_size();
   g_ub = 0;
+  g_pst = st;
+  g_plvl = 0;
   g_lmop_full = 0;
   (void)amgd_pool_ipeak_take();
   amgd_sync();
@@ -869,6 +885,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     }
     plevel *L = &h->lv[level];
     const uint32_t n = Pn->n;
+    g_plvl = (int)level;
     L->A = A;
     L->Pn = Pn;
     if (verbose()) printf("Level %u, dim(A) = %u, nnz(A)/dim(A) = %f\n", level + 1, n,

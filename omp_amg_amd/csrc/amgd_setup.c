@@ -39,6 +39,14 @@ static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0)
 
 static amgd_stats g_st;
 static uint64_t g_ub;                  /* reference-undefined events (non-termination) */
+/* where they fired (the first AMGD_UB_LOG of a setup): site 1 find_support theta -> 0, 2 a
+   one-row R, 3 a sweep that removed nothing, 4 the selection count past nnz(R) + nc, 5 the
+   interpolation loop's skeleton stalled (amg_setup.c:1316-1330, :700-860) */
+static void ub_note(int site, int level) {
+  if (g_ub < AMGD_UB_LOG) { g_st.ub_site[g_ub] = (uint8_t)site; g_st.ub_level[g_ub] = (uint8_t)level; }
+  g_ub++;
+}
+#define UB(site) ub_note((site), g_lvl)
 static int g_verbose = -1;
 static int verbose(void) {
   if (g_verbose < 0) { const char *e = getenv("AMGD_VERBOSE"); g_verbose = e && *e && *e != '0'; }
@@ -521,8 +529,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
     ph(PH_FS_MAX);
     if (mv < goal || mw < goal) break;
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
-    if (theta == 0) { g_ub++; break; }                   /* reference spins forever */
-    if (nf <= 1) { g_ub++; break; }                      /* maski = 1: never terminates */
+    if (theta == 0) { UB(1); break; }                   /* reference spins forever */
+    if (nf <= 1) { UB(2); break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
     uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     prev_off = ns;
@@ -535,8 +543,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
               n1, n2, n3, done ? (t1 - t0) * 1e3 : 0., (amgd_wtime() - (done ? t1 : t0)) * 1e3);
     }
     ph(PH_FS_SEL);
-    if (nrem == 0) { g_ub++; break; }                    /* no progress: reference loops */
-    if (ns + nc > cap) { g_ub++; break; }
+    if (nrem == 0) { UB(3); break; }                    /* no progress: reference loops */
+    if (ns + nc > cap) { UB(4); break; }
   }
   double *ones = dones(ns);
   dcsr *Sk = amgd_coo2csr(ns, si, sj, ones, nf, nc, 1);
@@ -765,7 +773,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
              (unsigned long)n, sqrt(gamma2), sqrt(maxr)), fflush(stdout);
     trace_limit(it);
     int stalled = prev_nnz == W_skel->nnz;   /* reference would loop forever */
-    if (stalled) g_ub++;
+    if (stalled) UB(5);
     prev_nnz = W_skel->nnz;
     ph(PH_R);
     if (n == 0 || w1m <= gamma2 || stalled) {

@@ -35,7 +35,10 @@ CONFIGS = {
                lambda: problems.sem_laplacian(22, 22, 21, 7)),
     "sem1k": ("SEM Laplacian, 10x10x10 hexes, N=7",
               lambda: problems.sem_laplacian(10, 10, 10, 7)),
+    "p27_32": ("3D 27-point Poisson 32^3", lambda: problems.poisson3d(32, 27)),
+    "p27_48": ("3D 27-point Poisson 48^3", lambda: problems.poisson3d(48, 27)),
     "p27_64": ("3D 27-point Poisson 64^3", lambda: problems.poisson3d(64, 27)),
+    "p27_80": ("3D 27-point Poisson 80^3", lambda: problems.poisson3d(80, 27)),
     "p27_96": ("3D 27-point Poisson 96^3", lambda: problems.poisson3d(96, 27)),
     "p27_128": ("3D 27-point Poisson 128^3", lambda: problems.poisson3d(128, 27)),
     "p27_256": ("3D 27-point Poisson 256^3", lambda: problems.poisson3d(256, 27)),
@@ -52,7 +55,11 @@ for name in [a for a in sys.argv[1:] if a in CONFIGS]:
     del Ai, Aj, Av
     for r in range(reps):
         t1 = time.perf_counter()
-        st = ds.run()
+        try:
+            st = ds.run()
+        except RuntimeError as e:                  # out of HBM: recorded, the probe goes on
+            print(json.dumps({"config": name, "workload": desc, "rows": rows, "error": str(e)}), flush=True)
+            break
         dt = time.perf_counter() - t1
         keep = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in st.items()}
         print(json.dumps({"config": name, "workload": desc, "rows": rows, "rep": r, "setup_s": round(dt, 3),
