@@ -248,6 +248,17 @@ void amgd_lmop_stats_reset(void);
 void amgd_lmop_set_mode(int m);        /* 0: row-pull fast path where exact, 1: general walk */
 void amgd_lmop_spill_detect(int on);   /* partitioned mode: flag walks past the view's last row */
 int amgd_lmop_spilled(void);
+/* partitioned mode: [0, d) already added to S (the dirty prefix walked on the whole S
+   pattern); amgd_lmop then adds [d, nc) only.  0: off */
+void amgd_lmop_set_prefix(uint32_t d);
+/* amgd_lmop_general keeps the values of S positions [lo, hi) only, in a (NULL: off) */
+void amgd_lmop_set_window(double *a, uint64_t lo, uint64_t hi);
+/* the exact (sp_add-walk) contributions of the coarse points [cb, ce) added to S */
+void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, const uint64_t *qoff, const double *u,
+                       uint32_t cb, uint32_t ce);
+void amgd_lmop_classify_view(const dcsr *Wt, uint32_t *dend, uint32_t *cmin);
+uint64_t amgd_lmop_qq_bytes(void);    /* QQ^t bytes of the last amgd_lmop call */
+int amgd_lmop_missed(void);            /* a clean contribution missed (prefix mode); clears */
 void amgd_qfactor_set_sparse(int m);   /* huge supports: 0 dense, 1 sparse first, 2 tiny capacity */
 void amgd_qfactor_stats(unsigned long *st); /* [sparse, dense fallback, split] since the last call */
 /* one find_support sweep: select/remove, then re-sum rs (rows) and sumR (columns) that lost

@@ -1834,16 +1834,30 @@ __global__ void k_lmop_val(uint64_t n, uint32_t c0, uint32_t c1, const uint64_t 
     val[o] = u[c] * q;
   }
 }
-__global__ void k_seg_accum(const uint64_t *key, const double *val, uint64_t n, uint64_t snnz,
-                            double *sa) {
+// sa holds the positions [lo, hi) of S (sa[0] = position lo); keys outside are dropped
+__global__ void k_seg_accum(const uint64_t *key, const double *val, uint64_t n, uint64_t lo,
+                            uint64_t hi, double *sa) {
   GRID_STRIDE(i, n) {
     uint64_t kk = key[i];
-    if (kk >= snnz) continue;
+    if (kk < lo || kk >= hi) continue;
     if (i > 0 && key[i - 1] == kk) continue;     // not the head of its run
-    double acc = sa[kk];
+    double acc = sa[kk - lo];
     for (uint64_t t = i; t < n && key[t] == kk; t++) acc = acc + val[t];
-    sa[kk] = acc;
+    sa[kk - lo] = acc;
   }
+}
+// Partitioned mode: the walks run on the whole S pattern, the values of positions [lo, hi)
+// only (a rank's rows) are kept, in `a` (amgd_lmop_set_window; off: S->a, all of S)
+static double *g_win_a = nullptr;
+static uint64_t g_win_lo = 0, g_win_hi = 0;
+extern "C" void amgd_lmop_set_window(double *a, uint64_t lo, uint64_t hi) {
+  g_win_a = a; g_win_lo = lo; g_win_hi = hi;
+}
+static void seg_accum(const uint64_t *key, const double *val, uint64_t n, const dcsr *S) {
+  if (g_win_a)
+    k_seg_accum<<<grid_for(n), 256, 0, amgd_s()>>>(key, val, n, g_win_lo, g_win_hi, g_win_a);
+  else
+    k_seg_accum<<<grid_for(n), 256, 0, amgd_s()>>>(key, val, n, 0, S->nnz, S->a);
 }
 __global__ void k_csq(const uint64_t *wro, uint32_t rn, uint64_t *sz) {
   GRID_STRIDE(c, rn) {
@@ -2054,7 +2068,7 @@ static bool lmop_pruned(dcsr *S, const dcsr *Wt, const double *Q, uint64_t qo, u
   HIPCK(rocprim::radix_sort_pairs(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
   tmp = amgd_alloc(tb + 16);
   HIPCK(rocprim::radix_sort_pairs(tmp, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
-  k_seg_accum<<<grid_for(n), 256, 0, s>>>(k2, v2, n, S->nnz, S->a);
+  seg_accum(k2, v2, n, S);
   KCHECK();
   amgd_free(tmp); amgd_free(k1); amgd_free(k2); amgd_free(v1); amgd_free(v2);
   amgd_free(compid); amgd_free(rank); amgd_free(members); amgd_free(cro); amgd_free(koff);
@@ -2152,7 +2166,7 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
       HIPCK(rocprim::radix_sort_pairs(nullptr, tb2, key, key2, val, val2, (size_t)n, 0, eb, s));
       if (tb2 > tb) { amgd_free(tmp); tmp = amgd_alloc(tb2 + 16); tb = tb2; }
       HIPCK(rocprim::radix_sort_pairs(tmp, tb2, key, key2, val, val2, (size_t)n, 0, eb, s));
-      k_seg_accum<<<grid_for(n), 256, 0, s>>>(key2, val2, n, S->nnz, S->a);
+      seg_accum(key2, val2, n, S);
       KCHECK();
     }
     c0 = c1;

@@ -426,16 +426,41 @@ extern "C" void amgd_lmop_note_pruned(void) { g_lmop_stats[4]++; }
 // Partitioned mode (amgd_psetup.c p_lmop): S and Wskel are global-row views of a rank's
 // rows, Wt / Q / qoff the supports those rows reference; every path below then computes
 // exactly this rank's rows (walks starting in other ranks' rows find them empty), and a walk
-// that would run into the next rank's rows is flagged (amgd_lmop_spill_detect).  Returns 0.
+// that would run into the next rank's rows is flagged (amgd_lmop_spill_detect).  With a
+// prefix set (amgd_lmop_set_prefix(D)), the contributions of the coarse points [0, D) --
+// every dirty one -- are already in S (p_lmop walks them on the whole S pattern): S is not
+// cleared and only [D, nc) is added, all clean.  Returns 0.
+static uint32_t g_lmop_prefix = 0;
+static int g_lmop_missed = 0;
+static uint64_t g_lmop_qq_bytes = 0;   // QQ^t bytes of the last call (all chunks)
+extern "C" uint64_t amgd_lmop_qq_bytes(void) { return g_lmop_qq_bytes; }
+extern "C" int amgd_lmop_missed(void) { const int m = g_lmop_missed; g_lmop_missed = 0; return m; }
+extern "C" void amgd_lmop_set_prefix(uint32_t d) { g_lmop_prefix = d; }
+extern "C" void amgd_lmop_classify_view(const dcsr *Wt, uint32_t *dend, uint32_t *cmin) {
+  const uint32_t nc = Wt->rn;
+  unsigned hst[4] = {0u, 0xffffffffu, 0u, 0u};
+  if (nc && Wt->nnz) {
+    uint8_t *dirty = (uint8_t *)amgd_alloc((size_t)nc + 1);
+    unsigned *st = (unsigned *)amgd_alloc(16);
+    amgd_h2d(st, hst, 16);
+    k_lmop_classify<<<grid_for(nc), 256, 0, amgd_s()>>>(Wt->ro, Wt->a, nc, dirty, st);
+    KCHECK();
+    amgd_d2h(hst, st, 8);
+    amgd_free(dirty); amgd_free(st);
+  }
+  *dend = hst[0];
+  *cmin = hst[1];
+}
 extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const dcsr *Wt,
                          const double *Q, const uint64_t *qoff, const double *u) {
   hipStream_t s = amgd_s();
-  amgd_memset(S->a, 0, S->nnz * 8);
+  const uint32_t pre = g_lmop_prefix;
+  if (!pre) amgd_memset(S->a, 0, S->nnz * 8);
   const uint32_t nc = Wt->rn;
-  if (nc == 0 || Wt->nnz == 0 || S->nnz == 0) return 0;
+  if (nc == 0 || Wt->nnz == 0 || S->nnz == 0 || pre >= nc) return 0;
   if (lmop_mode() == 1 || kpos == nullptr) {
     g_lmop_stats[1]++;
-    amgd_lmop_general(S, Wt, Q, qoff, u, 0, nc);
+    amgd_lmop_general(S, Wt, Q, qoff, u, pre, nc);
     return 0;
   }
   uint8_t *dirty = (uint8_t *)amgd_alloc((size_t)nc + 1);
@@ -445,15 +470,17 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
   k_lmop_classify<<<grid_for(nc), 256, 0, s>>>(Wt->ro, Wt->a, nc, dirty, st);
   KCHECK();
   amgd_d2h(hst, st, 8);
-  const uint32_t dend = hst[0], cmin = hst[1];
-  if (cmin == 0xffffffffu || (dend > 0 && dend - 1 > cmin)) {
+  uint32_t dend = hst[0];
+  const uint32_t cmin = hst[1];
+  if (pre) {
+    dend = pre;                       // [0, pre) done; every dirty point lies below pre
+  } else if (cmin == 0xffffffffu || (dend > 0 && dend - 1 > cmin)) {
     // no clean point, or a dirty point after a clean one: order needs the general walk
     g_lmop_stats[1]++;
     amgd_lmop_general(S, Wt, Q, qoff, u, 0, nc);
     amgd_free(dirty); amgd_free(st);
     return 0;
-  }
-  if (dend > 0) {                     // dirty prefix [0, dend): opens every sum it touches
+  } else if (dend > 0) {              // dirty prefix [0, dend): opens every sum it touches
     g_lmop_stats[2]++;
     amgd_lmop_general(S, Wt, Q, qoff, u, 0, dend);
   }
@@ -488,6 +515,7 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
   amgd_scan_u64(sz, nc);
   std::vector<uint64_t> hsz(nc + 1);
   amgd_d2h(hsz.data(), sz, ((size_t)nc + 1) * 8);
+  g_lmop_qq_bytes = hsz[nc] * 8;
   const uint64_t budget = qq_budget() / 8;
   uint32_t *lc = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
   uint64_t *tp = (uint64_t *)amgd_alloc(((size_t)nc + 1) * 8);
@@ -552,7 +580,11 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
       amgd_allgatherv(1, &b, off.data());
     }
   }
-  if (hm) {
+  if (hm && pre) {
+    // partitioned, prefix done: the caller redoes the operator (amgd_lmop_missed)
+    g_lmop_stats[3] += hm;
+    g_lmop_missed = 1;
+  } else if (hm) {
     // a clean contribution missed its column: S is not W_skel*W_skel' -- redo exactly
     g_lmop_stats[3] += hm;
     g_lmop_stats[1]++;

@@ -87,7 +87,8 @@ void pm_diag_op2(pmat *A, const double *Dl, const double *Dr, int op);  /* whole
 /* X = A*B with B's halo rows fetched; pattern = 1: amgd_spgemm_pattern */
 pmat *pm_spgemm(const pmat *A, const pmat *B, int pattern);
 /* B's rows referenced by the columns of L (local rows), beside B's own, in a global-row
-   view (row offsets for all B->rp->n rows).  Free with pm_ext_free. */
+   view (row offsets for all B->rp->n rows).  B->m->col == NULL: values only (E->col NULL).
+   Free with pm_ext_free. */
 dcsr *pm_halo_rows(const pmat *B, const dcsr *L);
 void pm_ext_free(dcsr **E);
 
@@ -96,6 +97,7 @@ void pm_ext_free(dcsr **E);
 uint64_t pm_route_coo(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V, const apart *P,
                       uint32_t **Io, uint32_t **Jo, double **Vo);
 dcsr *pm_gather_full(const pmat *A);
+dcsr *pm_gather_pattern(const pmat *A);     /* row offsets and columns only (a = NULL) */
 /* level-0 build helpers: max(I)+1, max(J)+1 over this rank's entries; a[i] += v (mod 2^32);
    out[i] = row i of T is not empty */
 void amgd_max_ij(uint64_t nz, const uint32_t *I, const uint32_t *J, uint32_t *mx);

@@ -380,7 +380,8 @@ __global__ void k_req_copy(const uint32_t *req, uint64_t n, uint32_t r0, const u
   GRID_STRIDE(t, n) {
     const uint32_t i = req[t] - r0;
     const uint64_t k0 = ro[i], l = ro[i + 1] - k0, o = off[t];
-    for (uint64_t q = 0; q < l; q++) { ocol[o + q] = col[k0 + q]; oa[o + q] = a[k0 + q]; }
+    if (col) for (uint64_t q = 0; q < l; q++) ocol[o + q] = col[k0 + q];
+    for (uint64_t q = 0; q < l; q++) oa[o + q] = a[k0 + q];
   }
 }
 // requester side: row lengths of the extended matrix
@@ -394,15 +395,8 @@ __global__ void k_ext_copy_own(const uint64_t *ro, const uint32_t *col, const do
                                uint32_t nl, const uint64_t *ero, uint32_t *ecol, double *ea) {
   GRID_STRIDE(i, nl) {
     const uint64_t k0 = ro[i], l = ro[i + 1] - k0, o = ero[r0 + i];
-    for (uint64_t q = 0; q < l; q++) { ecol[o + q] = col[k0 + q]; ea[o + q] = a[k0 + q]; }
-  }
-}
-__global__ void k_ext_copy_halo(const uint32_t *need, uint64_t n, const uint64_t *hoff, const uint32_t *hcol,
-                                const double *ha, const uint64_t *ero, uint32_t *ecol, double *ea) {
-  GRID_STRIDE(t, n) {
-    const uint32_t i = need[t];
-    const uint64_t o = ero[i], k0 = hoff[t], l = hoff[t + 1] - k0;
-    for (uint64_t q = 0; q < l; q++) { ecol[o + q] = hcol[k0 + q]; ea[o + q] = ha[k0 + q]; }
+    if (col) for (uint64_t q = 0; q < l; q++) ecol[o + q] = col[k0 + q];
+    for (uint64_t q = 0; q < l; q++) ea[o + q] = a[k0 + q];
   }
 }
 extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
@@ -467,18 +461,16 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
     gather_at(roff, qi.data(), N + 1, sb.data());
     gather_at(hoff, ni.data(), N + 1, rb.data());
   }
-  uint32_t *scol = (uint32_t *)amgd_alloc(4 * nsend + 8);
+  const bool cols = Bm->col != nullptr;     // NULL: a values-only pseudo-matrix (Q factors)
+  uint32_t *scol = cols ? (uint32_t *)amgd_alloc(4 * nsend + 8) : nullptr;
   double *sa = (double *)amgd_alloc(8 * nsend + 8);
   if (nreq) k_req_copy<<<grid_for(nreq), 256, 0, s>>>(req, nreq, r0, Bm->ro, Bm->col, Bm->a, roff, scol, sa);
   KCHECK();
-  uint32_t *hcol = (uint32_t *)amgd_alloc(4 * nhalo + 8);
-  double *ha = (double *)amgd_alloc(8 * nhalo + 8);
-  std::vector<uint64_t> s4(N + 1), r4(N + 1), s8(N + 1), r8(N + 1);
-  for (int p = 0; p <= N; p++) { s4[p] = 4 * sb[p]; s8[p] = 8 * sb[p]; r4[p] = 4 * rb[p]; r8[p] = 8 * rb[p]; }
-  amgd_pcomm_alltoallv(scol, s4.data(), hcol, r4.data());
-  amgd_pcomm_alltoallv(sa, s8.data(), ha, r8.data());
-  amgd_free(req); amgd_free(rlen); amgd_free(roff); amgd_free(scol); amgd_free(sa);
-  // 5. the extended matrix
+  // 5. the extended matrix: row offsets first, then the halo rows received straight into
+  //    it -- the rows of the ranks below come before the own rows, those above after them,
+  //    each rank's in ascending order (need is ascending), so the receive offsets are the
+  //    halo offsets shifted past the own entries for the ranks above
+  (void)nhalo;
   dcsr *E = (dcsr *)malloc(sizeof(dcsr));
   E->rn = n;
   E->cn = Bm->cn;
@@ -488,12 +480,20 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   if (nneed) k_ext_lens_halo<<<grid_for(nneed), 256, 0, s>>>(need, hlen, nneed, E->ro);
   KCHECK();
   E->nnz = amgd_scan_u64(E->ro, n);
-  E->col = (uint32_t *)amgd_alloc(4 * E->nnz + 8);
+  const uint64_t ownnz = Bm->nnz;
+  E->col = cols ? (uint32_t *)amgd_alloc(4 * E->nnz + 8) : nullptr;
   E->a = (double *)amgd_alloc(8 * E->nnz + 8);
+  std::vector<uint64_t> s4(N + 1), r4(N + 1), s8(N + 1), r8(N + 1);
+  for (int p = 0; p <= N; p++) {
+    const uint64_t at = rb[p] + (p > me ? ownnz : 0);
+    s4[p] = 4 * sb[p]; s8[p] = 8 * sb[p]; r4[p] = 4 * at; r8[p] = 8 * at;
+  }
+  if (cols) amgd_pcomm_alltoallv(scol, s4.data(), E->col, r4.data());
+  amgd_pcomm_alltoallv(sa, s8.data(), E->a, r8.data());
+  amgd_free(req); amgd_free(rlen); amgd_free(roff); amgd_free(scol); amgd_free(sa);
   if (nl) k_ext_copy_own<<<grid_for(nl), 256, 0, s>>>(Bm->ro, Bm->col, Bm->a, r0, nl, E->ro, E->col, E->a);
-  if (nneed) k_ext_copy_halo<<<grid_for(nneed), 256, 0, s>>>(need, nneed, hoff, hcol, ha, E->ro, E->col, E->a);
   KCHECK();
-  amgd_free(need); amgd_free(hlen); amgd_free(hoff); amgd_free(hcol); amgd_free(ha);
+  amgd_free(need); amgd_free(hlen); amgd_free(hoff);
   return E;
 }
 extern "C" void pm_ext_free(dcsr **E) { dcsr_free(E); }
@@ -513,33 +513,44 @@ extern "C" pmat *pm_spgemm(const pmat *A, const pmat *B, int pattern) {
 __global__ void k_ro_place(const uint64_t *lro, uint32_t nl, uint64_t base, uint64_t *dst) {
   GRID_STRIDE(i, nl) dst[i] = lro[i + 1] + base;
 }
-extern "C" dcsr *pm_gather_full(const pmat *A) {
+static dcsr *gather_rows(const pmat *A, bool vals) {
   const apart *P = A->rp;
   const int N = P->N, me = amgd_pcomm_rank();
+  const bool cols = A->m->col != nullptr;     // NULL: a values-only pseudo-matrix (Q factors)
   std::vector<uint64_t> nz(N, 0);
   nz[me] = A->m->nnz;
   amgd_pcomm_allgather_u64(nz.data(), 1);
   std::vector<uint64_t> base(N + 1, 0);
   for (int p = 0; p < N; p++) base[p + 1] = base[p] + nz[p];
-  dcsr *F = dcsr_new(P->n, A->m->cn, base[N]);
+  dcsr *F = (dcsr *)malloc(sizeof(dcsr));
+  F->rn = P->n; F->cn = A->m->cn; F->nnz = base[N];
+  F->ro = (uint64_t *)amgd_alloc(((size_t)P->n + 1) * 8);
+  F->col = cols ? (uint32_t *)amgd_alloc(base[N] * 4 + 4) : nullptr;
+  F->a = vals ? (double *)amgd_alloc(base[N] * 8 + 8) : nullptr;
   amgd_memset(F->ro, 0, 8);
   const uint32_t r0 = P->split[me], nl = A->m->rn;
   if (nl) k_ro_place<<<grid_for(nl), 256, 0, amgd_s()>>>(A->m->ro, nl, base[me], F->ro + r0 + 1);
   KCHECK();
   if (nz[me]) {
-    amgd_d2d(F->col + base[me], A->m->col, 4 * nz[me]);
-    amgd_d2d(F->a + base[me], A->m->a, 8 * nz[me]);
+    if (cols) amgd_d2d(F->col + base[me], A->m->col, 4 * nz[me]);
+    if (vals) amgd_d2d(F->a + base[me], A->m->a, 8 * nz[me]);
   }
   std::vector<uint64_t> off(3 * (N + 1));
-  for (int p = 0; p <= N; p++) {
-    off[p] = ((uint64_t)P->split[p] + 1) * 8;
-    off[(N + 1) + p] = base[p] * 4;
-    off[2 * (N + 1) + p] = base[p] * 8;
-  }
-  void *bufs[3] = {F->ro, F->col, F->a};
-  amgd_allgatherv(3, bufs, off.data());
+  void *bufs[3];
+  int nb = 0;
+  auto add = [&](void *buf, uint64_t elem, bool rows) {
+    for (int p = 0; p <= N; p++) off[nb * (N + 1) + p] = rows ? ((uint64_t)P->split[p] + 1) * 8 : base[p] * elem;
+    bufs[nb++] = buf;
+  };
+  add(F->ro, 8, true);
+  if (cols) add(F->col, 4, false);
+  if (vals) add(F->a, 8, false);
+  amgd_allgatherv(nb, bufs, off.data());
   return F;
 }
+extern "C" dcsr *pm_gather_full(const pmat *A) { return gather_rows(A, true); }
+extern "C" dcsr *pm_gather_pattern(const pmat *A) { return gather_rows(A, false); }
+
 
 // kpos[e] of W_skel entry e = (row i, column c): the position of i in support c (row c of
 // the extended W_skel^T): the support is sorted, so a binary search (the one-GPU path reads

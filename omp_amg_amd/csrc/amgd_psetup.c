@@ -344,9 +344,80 @@ static void pfactor_free(pfactor *f) {
   pm_free(&f->S); pm_free(&f->W0); pm_free(&f->W0t);
 }
 
-/* interp_lmop (amg_setup.c:1589) on the own rows of S: the supports and Q factors of the
-   coarse points those rows meet are fetched (halo); where the general walk is needed the
-   operator is formed on gathered data and each rank keeps its rows */
+/* AMGD_PHASES=1: per level the pool peak (GB) inside coarsen / smoother / the parts of the
+   interpolation / RAP on every rank (stderr) -- where a rank's HBM peak sits */
+enum { PK_COARSEN, PK_SMOOTH, PK_INTERP, PK_RAP, PK_QF, PK_WEIGHTS, PK_AFW_R, PK_EXPAND, PK_LMOP, PK_N };
+static const char *pk_name[PK_N] = {"coarsen", "smoother", "interp", "rap", "qfactor", "weights", "AfW_R", "expand", "lmop"};
+static int g_pph = -1;
+static uint32_t g_pklvl;
+static double g_pk[64][PK_N];
+static void pk_mark(uint32_t level, int ph) {
+  if (g_pph < 0) { const char *e = getenv("AMGD_PHASES"); g_pph = e && *e && *e != '0'; }
+  if (!g_pph || level >= 64) return;
+  const double pk = amgd_pool_ipeak_take() / 1e9;
+  if (pk > g_pk[level][ph]) g_pk[level][ph] = pk;
+}
+static void pk_report(uint32_t nl) {
+  if (g_pph <= 0) return;
+  fprintf(stderr, "rank %d pool peak GB per level:", g_me);
+  for (int p = 0; p < PK_N; p++) fprintf(stderr, " %8s", pk_name[p]);
+  fprintf(stderr, "\n");
+  for (uint32_t l = 0; l < nl && l < 64; l++) {
+    fprintf(stderr, "rank %d L%u", g_me, l);
+    for (int p = 0; p < PK_N; p++) fprintf(stderr, " %8.3f", g_pk[l][p]);
+    fprintf(stderr, "\n");
+  }
+  fprintf(stderr, "rank %d interp_lmop calls on gathered data: %lu\n", g_me, (unsigned long)g_lmop_full);
+  memset(g_pk, 0, sizeof g_pk);
+}
+
+/* interp_lmop (amg_setup.c:1589) on the own rows of S.  The supports and Q factors of the
+   coarse points those rows meet are fetched (halo) and the one-GPU paths run on global-row
+   views of the own rows of S and W_skel.  The dirty coarse points (a zero skeleton weight:
+   their sp_add walks leave the row, amg_setup.c:1665-1677, and may run into the next
+   rank's rows) form a prefix [0, D) of the coarse points; their contributions are walked on
+   every rank over the whole S pattern with the supports and Q factors of [0, D) only, each
+   rank keeping its rows' values, and the clean points [D, nc) -- sums that stay in their
+   row -- follow on the views.  Only a walk of the views running past the rank's last row
+   (a clean contribution missing its column) falls back to the whole operator. */
+static dcsr prefix_view(const dcsr *M, uint32_t r0, uint32_t D, apart *Pd, const apart *P) {
+  /* the rows of M (local rows from r0) below global row D, and the partition of [0, D) */
+  dcsr v = *M;
+  const uint32_t r1 = r0 + M->rn;
+  v.rn = D <= r0 ? 0 : (D >= r1 ? M->rn : D - r0);
+  v.nnz = 0;
+  if (v.rn) amgd_d2h(&v.nnz, M->ro + v.rn, 8);
+  Pd->N = P->N;
+  Pd->n = D;
+  for (int p = 0; p <= P->N; p++) Pd->split[p] = P->split[p] < D ? P->split[p] : D;
+  return v;
+}
+static void p_lmop_prefix(pmat *S, const pfactor *f, const pmat *qp, const double *u, uint32_t D) {
+  const apart *Pc = f->Wt->rp;
+  uint32_t *spl = (uint32_t *)malloc(2 * sizeof(uint32_t) * (Pc->N + 1));
+  apart Pd[2] = {{0, 0, spl}, {0, 0, spl + Pc->N + 1}};
+  dcsr wv = prefix_view(f->Wt->m, Pc->split[g_me], D, &Pd[0], Pc);
+  dcsr qv = prefix_view(qp->m, Pc->split[g_me], D, &Pd[1], Pc);
+  pmat wp = {&wv, &Pd[0], f->Wt->cp}, qq = {&qv, &Pd[1], Pc};
+  dcsr *WtD = pm_gather_full(&wp), *QD = pm_gather_full(&qq);
+  /* the whole S pattern (row offsets, columns); the values of the own rows only */
+  dcsr sv = *S->m;
+  sv.a = NULL;
+  pmat sp = {&sv, S->rp, S->cp};
+  dcsr *Sf = pm_gather_pattern(&sp);
+  const uint32_t r0 = S->rp->split[g_me];
+  uint64_t off = 0;
+  amgd_d2h(&off, Sf->ro + r0, 8);
+  amgd_memset(S->m->a, 0, S->m->nnz * 8);
+  amgd_lmop_set_window(S->m->a, off, off + S->m->nnz);
+  amgd_lmop_general(Sf, WtD, QD->a, QD->ro, u, 0, D);
+  amgd_lmop_set_window(NULL, 0, 0);
+  if (g_pph > 0 && g_me == 0)
+    fprintf(stderr, "rank 0 L%u lmop prefix D=%u: whole S pattern %.3f GB, supports %.3f GB, Q %.3f GB\n", g_pklvl,
+            D, (Sf->nnz * 4.0 + Sf->rn * 8.0) / 1e9, WtD->nnz * 12.0 / 1e9, QD->nnz * 12.0 / 1e9);
+  dcsr_free(&Sf); dcsr_free(&WtD); dcsr_free(&QD);
+  free(spl);
+}
 static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u) {
   dcsr *WtE = pm_halo_rows(f->Wt, Wskel->m);
   /* the Q factors as a matrix whose row c holds Q_c (offsets qoff): halo rows of it */
@@ -355,21 +426,32 @@ static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u
   qm.cn = 1;
   qm.nnz = f->qtot;
   qm.ro = f->qoff;
-  qm.col = (uint32_t *)amgd_alloc(4 * f->qtot + 8);
-  amgd_memset(qm.col, 0, 4 * f->qtot + 8);
+  qm.col = NULL;                                      /* values only */
   qm.a = f->Q;
   pmat qp = {&qm, f->Wt->rp, f->Wt->cp};
+  /* the dirty prefix: every dirty point of every rank (its own coarse points) lies below D */
+  uint32_t dl, cl;
+  amgd_lmop_classify_view(f->Wt->m, &dl, &cl);
+  dl = dl ? f->Wt->rp->split[g_me] + dl : 0;
+  const uint32_t D = (uint32_t)all_max(dl);
+  if (D) {
+    p_lmop_prefix(S, f, &qp, u, D);
+    amgd_lmop_set_prefix(D);
+  }
   dcsr *QE = pm_halo_rows(&qp, Wskel->m);
   uint32_t *kpos = pm_kpos(Wskel, WtE);
-  /* global-row views of the own rows of S and W_skel: the fast path, the dirty-prefix and
-     general walks all run on them; only a walk running into the next rank's rows needs
-     the whole operator (flagged; never on the last rank) */
   dcsr gS = pm_gview(S), gW = pm_gview(Wskel);
   const int last = S->rp->split[g_me + 1] == S->rp->n;
   amgd_lmop_spill_detect(!last);
   amgd_lmop(&gS, &gW, kpos, WtE, QE->a, QE->ro, u);
-  const int st = last ? 0 : amgd_lmop_spilled();
+  if (g_pph > 0 && g_me == 0)
+    fprintf(stderr, "rank 0 L%u lmop views: S %.3f GB, W_skel %.3f GB, supports %.3f GB (%lu own), Q %.3f GB "
+            "(%lu own), QQ %.3f GB\n", g_pklvl, S->m->nnz * 12.0 / 1e9, Wskel->m->nnz * 12.0 / 1e9,
+            WtE->nnz * 12.0 / 1e9, (unsigned long)f->Wt->m->nnz, QE->nnz * 12.0 / 1e9, (unsigned long)f->qtot,
+            amgd_lmop_qq_bytes() / 1e9);
+  const int st = (last ? 0 : amgd_lmop_spilled()) | amgd_lmop_missed();
   amgd_lmop_spill_detect(0);
+  amgd_lmop_set_prefix(0);
   pm_gview_free(&gS);
   pm_gview_free(&gW);
   if (all_max((uint64_t)st) != 0) {
@@ -389,7 +471,11 @@ static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u
     amgd_free(kp);
     dcsr_free(&Sf); dcsr_free(&Wsf); dcsr_free(&Wtf); dcsr_free(&Qf);
   }
+  amgd_free(kpos);
+  pm_ext_free(&WtE);
+  pm_ext_free(&QE);
   amgd_free(qm.col);
+  pk_mark(g_pklvl, PK_LMOP);
 }
 
 static void p_solve_constraint(double *lam, const pmat *W_skel, pfactor *fac, const pmat *W0,
@@ -681,6 +767,7 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
   return out;
 }
 
+
 static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, double gamma2, double tol) {
   const uint32_t rnf = Af->rp->n, cnc = Ac->rp->n;
   double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
@@ -719,9 +806,11 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     dcsr *AfE = pm_halo_rows(Af, fac.Wt->m);             /* the Af rows of the supports */
     fac.Q = amgd_qfactor_reuse(fac.Wt->m, AfE, &fac.qoff, &fac.qtot, prevWt ? prevWt->m : NULL, prevQ, prevQoff);
     dcsr_free(&AfE);
+    pk_mark(g_pklvl, PK_QF);
     if (prevWt) { pm_free(&prevWt); amgd_free(prevQ); amgd_free(prevQoff); prevQ = NULL; prevQoff = NULL; }
     const pmat *W0;
     pmat *Wtmp = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
+    pk_mark(g_pklvl, PK_WEIGHTS);
     pmat *AfW = pm_spgemm(Af, Wtmp, 0);
     pmat *Arhat = pm_mpm(1., AfW, 1., Ar);
     pm_free(&AfW);
@@ -745,6 +834,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     double maxr = 0;
     uint64_t n = amgd_count_gt(r, cnc, gamma2, &maxr);
     double w1m = amgd_max_first(w1, cnc, NULL);
+    pk_mark(g_pklvl, PK_AFW_R);
     const uint64_t wsk = gnnz(W_skel);
     if (verbose())
       printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)wsk, (unsigned long)n, sqrt(gamma2),
@@ -770,6 +860,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     pr0_ctx r0c = {Af, W0, Ar, Dfsqrti, Dcs};
     const pfs_first f1 = {rs1, w1, tmp, w2};
     pmat *nsk = p_expand_support(W_skel, R, Rt, &r0c, gamma2, &f1);
+    pk_mark(g_pklvl, PK_EXPAND);
     pm_free(&W_skel);
     W_skel = nsk;
     pm_free(&Wtmp);
@@ -809,23 +900,6 @@ static void add_time(double *acc, double *t0) {
   double t = amgd_wtime();
   *acc += (t - *t0) * 1e3;
   *t0 = t;
-}
-/* AMGD_PHASES=1: per level the pool peak (GB) inside coarsen / smoother / interpolation /
-   RAP on every rank (stderr) -- where a rank's HBM peak sits */
-static int g_pph = -1;
-static double g_pk[64][4];
-static void pk_mark(uint32_t level, int ph) {
-  if (g_pph < 0) { const char *e = getenv("AMGD_PHASES"); g_pph = e && *e && *e != '0'; }
-  if (!g_pph || level >= 64) return;
-  const double pk = amgd_pool_ipeak_take() / 1e9;
-  if (pk > g_pk[level][ph]) g_pk[level][ph] = pk;
-}
-static void pk_report(uint32_t nl) {
-  if (g_pph <= 0) return;
-  fprintf(stderr, "rank %d pool peak GB per level: coarsen smoother interp rap\n", g_me);
-  for (uint32_t l = 0; l < nl && l < 64; l++)
-    fprintf(stderr, "rank %d L%u %8.3f %8.3f %8.3f %8.3f\n", g_me, l, g_pk[l][0], g_pk[l][1], g_pk[l][2], g_pk[l][3]);
-  memset(g_pk, 0, sizeof g_pk);
 }
 
 __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const uint32_t *dAi,
@@ -900,7 +974,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     amgd_u8_not(vc, vf, n);
     L->vc = vc;
     add_time(&st->t_coarsen_ms, &t0);
-    pk_mark(level, 0);
+    pk_mark(level, PK_COARSEN);
     apart *Pf = apart_induced(Pn, vf), *Pc = apart_induced(Pn, vc);
     L->Pf = Pf;
     pmat *Af = pm_sub_mat(A, vf, vf, Pf, Pf);
@@ -932,16 +1006,17 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     L->D = D;
     L->Af = Af;
     add_time(&st->t_smoother_ms, &t0);
-    pk_mark(level, 1);
+    pk_mark(level, PK_SMOOTH);
     pmat *Afc = pm_sub_mat(A, vf, vc, Pf, Pc), *Ac = pm_sub_mat(A, vc, vc, Pc, Pc);
     const uint32_t rnc = Pc->n;
     L->idc = (unsigned long *)amgd_alloc((size_t)rnc * 8 + 8);
     L->idf = (unsigned long *)amgd_alloc((size_t)rnf * 8 + 8);
     amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, n, L->idc, L->idf);
+    g_pklvl = level;
     pmat *W = p_interpolation(Af, Ac, Afc, gamma2, itol);
     L->W = W;
     add_time(&st->t_interp_ms, &t0);
-    pk_mark(level, 2);
+    pk_mark(level, PK_INTERP);
     /* Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) (amg_setup.c:339-372) */
     pmat *Acf = pm_transpose(Afc);
     amgd_spgemm_set_timer(0);
@@ -960,7 +1035,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     pm_free(&Afc); pm_free(&Ac);
     amgd_free(vf);
     add_time(&st->t_rap_ms, &t0);
-    pk_mark(level, 3);
+    pk_mark(level, PK_RAP);
     Pn = Pc;
     level++;
   }

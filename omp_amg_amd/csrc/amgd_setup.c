@@ -378,6 +378,10 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
     dcsr_free(&Wn); dcsr_free(&Wnt);
     ph(PH_SPAT);
     amgd_lmop(fac->S, W_skel, fac->kpos, fac->Wt, fac->Q, fac->qoff, au2);
+    if (phases_on())
+      fprintf(stderr, "L%u lmop: S %.3f GB, W_skel %.3f GB, supports %.3f GB, Q %.0f, QQ %.3f GB\n", g_lvl,
+              fac->S->nnz * 12.0 / 1e9, W_skel->nnz * 12.0 / 1e9, fac->Wt->nnz * 12.0 / 1e9, 0.0,
+              amgd_lmop_qq_bytes() / 1e9);
     ph(PH_LMOP);
   }
   dcsr *S = fac->S;

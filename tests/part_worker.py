@@ -6,7 +6,9 @@ rank passes only ITS slice of the COO entries (a contiguous 1/N of them, or -- w
 PART_CRS -- its block of rows as a crs_setup local matrix); the library routes them to
 the row owners, builds the row-partitioned hierarchy, and the exported (gathered)
 hierarchy is compared bit for bit with the reference fixture or the stored digest.
-Prints one JSON line (per-rank peak HBM bytes included); exit code 0 = pass."""
+Prints one JSON line (per-rank peak HBM bytes and the device bytes left allocated after
+the setup returned -- 0 -- included); exit code 0 = pass."""
+import ctypes as C
 import json
 import os
 import sys
@@ -25,6 +27,9 @@ def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=size)
     oa.init(0)
+    L = oa.lib()
+    L.amgd_test_pool_inuse.restype = C.c_uint64
+    before = L.amgd_test_pool_inuse()
     case = os.environ["PART_CASE"]
     out = {"rank": rank, "case": case, "size": size}
     ref = digest = None
@@ -56,6 +61,7 @@ def main():
     st = shard.stats()
     out["peak_bytes"] = int(oa.stats()["peak_bytes"])
     shard.free()
+    out["leak_bytes"] = int(L.amgd_test_pool_inuse()) - int(before)
     if ref is not None:
         bad = parity.compare(ref, h, exact=True)
     else:
@@ -66,7 +72,7 @@ def main():
     out.update(calls=st["calls"], bytes=st["bytes"], bad=bad[:5], levels=h.nlevels)
     print(json.dumps(out), flush=True)
     dist.destroy_process_group()
-    sys.exit(0 if not bad and st["calls"] > 0 else 1)
+    sys.exit(0 if not bad and st["calls"] > 0 and out["leak_bytes"] == 0 else 1)
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@ def _run(size, case, crs="", timeout=110, extra_env=None):
     for rc, o, e in outs:
         assert rc == 0, (o[-2000:], e)
         d = json.loads(o.strip().splitlines()[-1])
-        assert not d["bad"] and d["calls"] > 0, d
+        assert not d["bad"] and d["calls"] > 0 and d["leak_bytes"] == 0, d
         res.append(d)
     return res
 

@@ -1,0 +1,18 @@
+# partition tests (lmop on views), per-rank peak 128^3 N=2/3, 27-point one-GPU peaks, aniso 256^3 ub sites
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+D=$GRAFT_REPO_ROOT/gpurun_out/r04g
+rm -rf $D; mkdir -p $D
+export PYTHONPATH=$GRAFT_REPO_ROOT
+timeout -k 10 700 python3 -u -m pytest tests/test_gpu_partition.py -m gpu -v --timeout 300 --timeout-method thread > $D/parttests.log 2>&1; r=$?; echo "part tests rc=$r"; grep -E "PASSED|FAILED|passed|failed" $D/parttests.log | tail -25
+[ $r -eq 0 ] || { grep -E "omp_amg_amd|rank [0-9] rc" $D/parttests.log | head -20; exit 1; }
+AMGD_PHASES=1 timeout -k 10 400 python3 -u tools/part_peak.py 128 2 $D/part_peak_128_n2.json > $D/peak2.log 2>&1; r=$?; echo "peak n2 rc=$r"; grep -E "over_one|bit_id" $D/peak2.log; [ $r -eq 0 ] || exit 1
+AMGD_PHASES=1 timeout -k 10 400 python3 -u tools/part_peak.py 128 3 $D/part_peak_128_n3.json > $D/peak3.log 2>&1; r=$?; echo "peak n3 rc=$r"; grep -E "over_one|bit_id" $D/peak3.log; [ $r -eq 0 ] || exit 1
+timeout -k 10 400 python3 -u tools/probe_configs.py p27_32 p27_48 p27_64 > $D/p27.json 2> $D/p27.err; echo "p27 rc=$?"; python3 -c "
+import json
+for l in open('$D/p27.json'):
+    d=json.loads(l); print(d['config'], d.get('setup_s'), d.get('peak_bytes'), d.get('nlevels'), d.get('error',''))"
+timeout -k 10 300 python3 -u tools/probe_configs.py aniso256 > $D/aniso.json 2> $D/aniso.err; echo "aniso rc=$?"; python3 -c "
+import json
+for l in open('$D/aniso.json'):
+    d=json.loads(l); print(d['config'], d.get('setup_s'), d.get('ub_events'), d.get('ub_site'), d.get('ub_level'))"

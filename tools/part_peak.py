@@ -65,6 +65,9 @@ def rank_main(m, stencil):
                       "levels": h.nlevels, "digest": digest(h) if rank == 0 else None}), flush=True)
     ds.close()
     shard.free()
+    L = oa.lib()
+    L.amgd_test_pool_inuse.restype = __import__("ctypes").c_uint64
+    print(json.dumps({"rank": rank, "leak_bytes": int(L.amgd_test_pool_inuse())}), flush=True)
     dist.destroy_process_group()
 
 
@@ -106,8 +109,11 @@ def main():
             for x in ps:
                 x.kill()
             sys.exit(f"rank failed rc={q.returncode}: {e[-3000:]}")
-        d = json.loads(o.strip().splitlines()[-1])
-        d["phase_peaks"] = [l for l in e.splitlines() if l.startswith("rank")][-20:]
+        d = {}
+        for line in o.strip().splitlines():
+            if line.startswith("{"):
+                d.update(json.loads(line))
+        d["phase_peaks"] = [l for l in e.splitlines() if l.startswith("rank")][-60:]
         ranks.append(d)
     peak = max(r["peak_bytes"] for r in ranks)
     res = {"workload": f"3D {a.stencil}-point Poisson {a.m}^3", "ranks": a.N, "one_gpu": one,
@@ -115,6 +121,7 @@ def main():
            "max_rank_peak_over_one_gpu": peak / one["peak_bytes"],
            "target_1p5_over_N": 1.5 / a.N,
            "bit_identical": ranks[0]["digest"] == one["digest"],
+           "max_rank_leak_bytes": max(r.get("leak_bytes", -1) for r in ranks),
            "transport": "host (gloo, N processes on one GPU)"}
     js = json.dumps(res, indent=1)
     print(js)
