@@ -73,9 +73,9 @@ def parse():
                    help="cap on the total time of the CPU baseline (all child runs)")
     p.add_argument("--cpu-child", nargs=2, type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic", type=float, default=None,
-                   help="long-row SpMV HBM bytes per setup from rocprofv3 PMC passes (profiles/)")
+                   help="long-row SpMV L2->fabric bytes per setup from rocprofv3 PMC passes (profiles/)")
     p.add_argument("--rap-traffic", type=float, default=None,
-                   help="RAP SpGEMM HBM bytes per setup from rocprofv3 PMC passes (profiles/)")
+                   help="RAP SpGEMM L2->fabric bytes per setup from rocprofv3 PMC passes (profiles/)")
     return p.parse_args()
 
 
@@ -149,7 +149,8 @@ def gpu_sample(m, reps=5):
 
 
 def pmc_traffic(m, stencil, world):
-    """HBM bytes per setup of the two roofline kernels from the committed rocprofv3
+    """L2->fabric bytes (FETCH_SIZE / WRITE_SIZE: an upper bound on HBM bytes, MALL hits
+    included) per setup of the two roofline kernels from the committed rocprofv3
     PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass, gfx950 correction;
     tools/gpurun_round.sh), only when they were measured on this same workload (grid,
     stencil, one GPU): (spmv, rap, source) or Nones"""
@@ -343,7 +344,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": mv_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": mv_achieved / HBM_PEAK_GBS,
                          "traffic": t_mv / mv_lps if (t_mv and mv_lps) else None,
-                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE / WRITE_SIZE, calibrated; "
+                         "traffic_unit": "L2->fabric bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, calibrated; "
+                                         "MALL hits included, so an upper bound on HBM bytes; "
                                          "traffic_per_setup / launches_per_setup)",
                          "traffic_per_setup": t_mv,
                          "traffic_source": t_src,
@@ -371,7 +373,8 @@ def main():
             "rap_roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": t_rap / rap_lps if (t_rap and rap_lps) else None,
-                         "traffic_unit": "HBM bytes per launch (PMC, calibrated; traffic_per_setup / launches)",
+                         "traffic_unit": "L2->fabric bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, calibrated; MALL hits "
+                                         "included: an upper bound on HBM bytes; traffic_per_setup / launches)",
                          "traffic_per_setup": t_rap,
                          "traffic_source": t_src,
                          "traffic_over_algorithmic": t_rap * steps / rap_bytes if (t_rap and rap_bytes) else None,

@@ -104,6 +104,8 @@ void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_
 /* partitioned mode (amgd_psetup.c): ranks own row blocks; amgd_nshards() is 1 there */
 int amgd_comm_partitioned(void);
 void amgd_comm_suspend_partition(int on);
+/* calls, bytes of: data allgatherv, alltoallv, small u64 allgathers (since the last reset) */
+void amgd_comm_stats_kind(uint64_t *out6);
 int amgd_pcomm_rank(void);
 int amgd_pcomm_size(void);
 void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m);   /* vals_h[N*m]: own m -> all */

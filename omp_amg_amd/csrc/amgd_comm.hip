@@ -48,6 +48,10 @@ static amgd_allgatherv_fn g_cb = nullptr;
 static void *g_user = nullptr;
 static double g_min_scale = 1.0;      // work thresholds x this (0: shard everything)
 static uint64_t g_bytes = 0, g_calls = 0;
+// by kind: [0] allgatherv of data (vector segments, gathered rows), [1] alltoallv (halo rows,
+// transposes, routed entries), [2] allgathers of a few u64 (counts, flags, maxima); calls, bytes
+static uint64_t g_kstat[3][2];
+static int g_kind_small = 0;
 static double g_ms = 0;
 
 // ---- RCCL entry points (dlopen'ed) ----
@@ -162,7 +166,12 @@ extern "C" API void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms
   *bytes = g_bytes;
   *ms = g_ms;
 }
-extern "C" API void amgd_comm_stats_reset(void) { g_calls = g_bytes = 0; g_ms = 0; }
+extern "C" API void amgd_comm_stats_reset(void) {
+  g_calls = g_bytes = 0;
+  g_ms = 0;
+  memset(g_kstat, 0, sizeof g_kstat);
+}
+void amgd_comm_stats_kind(uint64_t *out6) { memcpy(out6, g_kstat, sizeof g_kstat); }
 
 // ---- internal API (amgd.h) ----
 int amgd_nshards(void) { return g_kind == COMM_NONE || g_part ? 1 : g_size; }
@@ -190,8 +199,12 @@ void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off) {
   const int N = g_size;
   if (g_kind == COMM_NONE || g_kind == COMM_SIM || N == 1) return;
   double t0 = amgd_wtime();
-  for (int b = 0; b < nbuf; b++) g_bytes += off[b * (N + 1) + N] - off[b * (N + 1)];
+  uint64_t nb = 0;
+  for (int b = 0; b < nbuf; b++) nb += off[b * (N + 1) + N] - off[b * (N + 1)];
+  g_bytes += nb;
   g_calls++;
+  g_kstat[g_kind_small ? 2 : 0][0]++;
+  g_kstat[g_kind_small ? 2 : 0][1] += nb;
   if (g_kind == COMM_HOST) {
     amgd_sync();
     if (g_cb(g_user, nbuf, bufs, off, g_rank, N) != 0) {
@@ -297,7 +310,9 @@ void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m) {
   std::vector<uint64_t> off(N + 1);
   for (int s = 0; s <= N; s++) off[s] = 8ull * s * m;
   void *b = d;
+  g_kind_small = 1;
   amgd_allgatherv(1, &b, off.data());
+  g_kind_small = 0;
   amgd_d2h(vals_h, d, 8ull * N * m);
   amgd_free(d);
 }
@@ -315,6 +330,8 @@ void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, co
   if (N == 1) return;
   double t0 = amgd_wtime();
   g_calls++;
+  g_kstat[1][0]++;
+  for (int p = 0; p < N; p++) if (p != me) g_kstat[1][1] += roff[p + 1] - roff[p];
   if (g_kind == COMM_RCCL) {
     hipStream_t s = amgd_s();
     NCCK(R.GroupStart());

@@ -368,6 +368,11 @@ static void pk_report(uint32_t nl) {
     fprintf(stderr, "\n");
   }
   fprintf(stderr, "rank %d interp_lmop calls on gathered data: %lu\n", g_me, (unsigned long)g_lmop_full);
+  uint64_t k[6];
+  amgd_comm_stats_kind(k);
+  fprintf(stderr, "rank %d exchanges: allgatherv %lu calls %.3f GB, alltoallv %lu calls %.3f GB received, "
+          "u64 allgathers %lu calls\n", g_me, (unsigned long)k[0], k[1] / 1e9, (unsigned long)k[2], k[3] / 1e9,
+          (unsigned long)k[4]);
   memset(g_pk, 0, sizeof g_pk);
 }
 

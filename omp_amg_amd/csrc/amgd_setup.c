@@ -1159,15 +1159,21 @@ API void amgd_hier_free(amgd_hier **hp) {
 /* ------------------------------------------------------------------------ */
 API void amg_setup(amg_uint n, const amg_uint *Ai, const amg_uint *Aj, const double *Av,
                    struct amg_setup_data *data) {
+  /* amg_setup has no status (amg_setup.h:5): every failure leaves data with nlevels = 0
+     and the reason in amgd_error() */
   if (amgd_rt_init(0) != 0) {
     fprintf(stderr, "omp_amg_amd: amg_setup needs a HIP device: %s\n", amgd_last_error());
-    abort();
+    memset(data, 0, sizeof *data);
+    return;
   }
   uint32_t *hi = (uint32_t *)malloc((size_t)n * 4 + 4), *hj = (uint32_t *)malloc((size_t)n * 4 + 4);
   for (amg_uint k = 0; k < n; k++) {
     if (Ai[k] > 0xfffffffeul || Aj[k] > 0xfffffffeul) {
-      fprintf(stderr, "omp_amg_amd: index %lu exceeds 32-bit range\n", (unsigned long)k);
-      abort();
+      amgd_set_error("amg_setup: an index exceeds the 32-bit range of the device CSR");
+      fprintf(stderr, "omp_amg_amd: entry %lu: index exceeds 32-bit range\n", (unsigned long)k);
+      free(hi); free(hj);
+      memset(data, 0, sizeof *data);
+      return;
     }
     hi[k] = (uint32_t)Ai[k];
     hj[k] = (uint32_t)Aj[k];

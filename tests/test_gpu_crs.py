@@ -167,3 +167,16 @@ def test_crs_setup_rejects_bad_local_index():
     hd = abi.crs_setup(oa.lib(), 4, [1, 2, 3, 4], Ai, CRS_J, CRS_A)
     assert hd is None
     assert b"local index" in oa.lib().amgd_error()
+
+
+def test_amg_setup_rejects_index_past_32_bits():
+    """amg_setup (no status in amg_setup.h:5) with an index past the device CSR's 32-bit
+    range: nlevels = 0 and the reason in amgd_error(), then a valid call works"""
+    oa.init()
+    Ai = np.asarray(CRS_I, np.uint64).copy()
+    Ai[3] = 1 << 32
+    h = abi.run_setup(oa.lib(), Ai, CRS_J, CRS_A)
+    assert h.nlevels == 0
+    assert b"32-bit" in oa.lib().amgd_error()
+    h = abi.run_setup(oa.lib(), CRS_I, CRS_J, CRS_A)
+    assert h.nlevels > 0

@@ -63,7 +63,7 @@ def test_partitioned_matches_reference_fixture(size, case):
 
 
 @pytest.mark.parametrize("size,case", [(3, "digest:p7_48"), (2, "digest:p27_20"), (3, "digest:sem_e4_N7"),
-                                       (2, "digest:aniso_20")],
+                                       (2, "digest:aniso_20"), (4, "digest:p7_64")],
                          ids=lambda v: str(v).replace("digest:", ""))
 @pytest.mark.parametrize("inc", ["1", "0"], ids=["inc", "full_sweeps"])
 def test_partitioned_matches_digest(size, case, inc):
@@ -71,6 +71,13 @@ def test_partitioned_matches_digest(size, case, inc):
     reference digest (every array of every level); incremental coarsening / find_support
     sweeps across the ranks (default) and full sweeps"""
     _run(size, case, timeout=240, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
+
+
+@pytest.mark.parametrize("case", ["gold:amgdmp", "gold:p27_8"], ids=lambda v: v[5:])
+def test_partitioned_eight_ranks(case):
+    """8 ranks -- the north_star's GPU count -- on small fixtures: coarse levels leave
+    ranks with no rows (empty blocks, empty halos, empty segments in every exchange)"""
+    _run(8, case, timeout=180)
 
 
 def test_partitioned_crs_setup():

@@ -37,11 +37,13 @@ CONFIGS = {
               lambda: problems.sem_laplacian(10, 10, 10, 7)),
     "p27_32": ("3D 27-point Poisson 32^3", lambda: problems.poisson3d(32, 27)),
     "p27_48": ("3D 27-point Poisson 48^3", lambda: problems.poisson3d(48, 27)),
+    "p27_56": ("3D 27-point Poisson 56^3", lambda: problems.poisson3d(56, 27)),
     "p27_64": ("3D 27-point Poisson 64^3", lambda: problems.poisson3d(64, 27)),
     "p27_80": ("3D 27-point Poisson 80^3", lambda: problems.poisson3d(80, 27)),
     "p27_96": ("3D 27-point Poisson 96^3", lambda: problems.poisson3d(96, 27)),
     "p27_128": ("3D 27-point Poisson 128^3", lambda: problems.poisson3d(128, 27)),
     "p27_256": ("3D 27-point Poisson 256^3", lambda: problems.poisson3d(256, 27)),
+    "p7_256": ("3D 7-point Poisson 256^3 (BASELINE configs[1])", lambda: problems.poisson3d(256, 7)),
 }
 
 reps = int(os.environ.get("PROBE_REPS", "1"))
