@@ -102,6 +102,7 @@ def lib() -> C.CDLL:
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
         L.amgd_test_sg_xcd.argtypes = [C.c_int]
+        L.amgd_test_sg_symbits.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -418,6 +419,12 @@ def sg_xcd(mask: int) -> None:
     """SpGEMM work-groups in XCD-contiguous order (bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row;
     0 the hardware's round-robin order, -1 back to AMGD_SG_XCD).  Same bits."""
     lib().amgd_test_sg_xcd(int(mask))
+
+
+def sg_symbits(on: int) -> None:
+    """symbolic pass of wide long-B-row SpGEMM rows: 1 bit-map windows of 32768 columns
+    (default), 0 byte-map windows of 4096, -1 back to AMGD_SG_SYMBITS.  Same counts."""
+    lib().amgd_test_sg_symbits(int(on))
 
 
 def sg_pattern(on: int) -> None:

@@ -2105,7 +2105,8 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
 // more than 64 layers keep their cursors in global scratch indexed by the A entry.
 // Every output is the sum, from +0 in ascending k, of its products -- mxm's order
 // (amg_setup.c:1894-1960) -- and the window is emitted in column order, coalesced.
-// MODE 0: distinct columns per row (byte map, W columns); MODE 1: values (W doubles).
+// MODE 0: distinct columns per row (byte map, W columns); MODE 2: the same with a bit map
+// (W columns in W / 8 bytes: 8x fewer windows over a wide row); MODE 1: values (W doubles).
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -2123,7 +2124,8 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
                                                  uint64_t *cnt, const uint64_t *xro,
                                                  uint32_t *xcol, double *xa, uint32_t *curs) {
   constexpr int NWV = 4, D = 4;
-  constexpr int WB = MODE ? W * 8 : W;              // LDS bytes per wavefront
+  constexpr bool NUM = MODE == 1;
+  constexpr int WB = NUM ? W * 8 : MODE == 2 ? W / 8 : W;   // LDS bytes per wavefront
   constexpr uint32_t NONE = 0xffffffffu;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NWV * WB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2164,23 +2166,23 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
         if (!(e + 1 < nl && acol[a0 + e + 1] == k)) {   // duplicate columns: the last one wins
           lb0 = bro[k];
           llen = (uint32_t)(bro[k + 1] - lb0);
-          if (MODE) lav = aa[a0 + e];
+          if (NUM) lav = aa[a0 + e];
           if (!first) lcur = curs[a0 - cbase + e];
           if (lcur < llen) lpk = bcol[lb0 + lcur];
         }
       }
     };
     if (single) load_layer(0, true);
-    const uint64_t ob = MODE ? xro[i] : 0;
+    const uint64_t ob = NUM ? xro[i] : 0;
     uint64_t nout = 0;
     bool first = true;
     uint32_t wb = mn;
     while (mn <= mx) {
       const uint32_t we = (uint32_t)min((uint64_t)mx, (uint64_t)wb + W - 1);   // inclusive
-      if (MODE) {
+      if (NUM) {
         for (int q = lane; q < W; q += 64) acc[q] = 0.0;
       } else {
-        for (int q = lane; q < W / 4; q += 64) mp32[q] = 0u;
+        for (int q = lane; q < WB / 4; q += 64) mp32[q] = 0u;
       }
       uint32_t nmin = NONE;
       for (uint32_t c0 = 0; c0 < nl; c0 += 64) {
@@ -2201,7 +2203,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
             qe[s] = e;
             if (j < ln) {
               qc[s] = bcol[b0 + j];
-              if (MODE) qv[s] = ba[b0 + j];
+              if (NUM) qv[s] = ba[b0 + j];
             }
           }
         };
@@ -2214,14 +2216,16 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
 #pragma unroll
           for (int s = 0; s + 1 < D; s++) { qe[s] = qe[s + 1]; qc[s] = qc[s + 1]; qv[s] = qv[s + 1]; }
           issue(D - 1);
-          const double av = MODE ? rld(lav, e) : 0.0;
+          const double av = NUM ? rld(lav, e) : 0.0;
           uint32_t cu = rl32(lcur, e);
           for (;;) {
             const bool in = col <= we;                 // a prefix of the lanes (sorted row)
             if (in) {
-              if (MODE) {
+              if (NUM) {
                 double *p = acc + (col - wb);
                 *p = *p + val * av;
+              } else if (MODE == 2) {
+                atomicOr(&mp32[(col - wb) >> 5], 1u << ((col - wb) & 31));
               } else {
                 mp[col - wb] = 1;
               }
@@ -2239,7 +2243,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
             col = NONE;
             if (j < ln) {
               col = bcol[b0 + j];
-              if (MODE) val = ba[b0 + j];
+              if (NUM) val = ba[b0 + j];
             }
           }
         }
@@ -2248,7 +2252,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
         nmin = min(nmin, m);
         if (!single && c0 + lane < nl) curs[a0 - cbase + c0 + lane] = lcur;
       }
-      if (MODE) {                                      // emit in column order
+      if (NUM) {                                      // emit in column order
         for (int q = 0; q < W; q += 64) {
           const double v = acc[q + lane];
           const bool nz = v != 0.0;
@@ -2262,7 +2266,8 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
         }
       } else {
         uint32_t c = 0;
-        for (int q = lane; q < W / 4; q += 64) c += (uint32_t)__popc(mp32[q] & 0x01010101u);
+        for (int q = lane; q < WB / 4; q += 64)
+          c += (uint32_t)__popc(MODE == 2 ? mp32[q] : mp32[q] & 0x01010101u);
         for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
         nout += c;
       }
@@ -2313,6 +2318,14 @@ __global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *ar
     const unsigned q = wave_append(&cnt[1], valid && !w);
     if (valid && !w) hl[q] = i;
   }
+}
+// symbolic wide rows: bit-map windows (MODE 2, 32768 columns) or byte maps (MODE 0, 4096);
+// AMGD_SG_SYMBITS=0 / amgd_spgemm_set_symbits (tests) select the byte maps
+static int g_symbits = -1;
+extern "C" void amgd_spgemm_set_symbits(int on) { g_symbits = on; }
+static int sg_symbits() {
+  if (g_symbits < 0) { const char *e = getenv("AMGD_SG_SYMBITS"); g_symbits = e && *e ? atoi(e) : 1; }
+  return g_symbits;
 }
 static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (g_sg_xcd < 0) amgd_spgemm_set_xcd(-1);
@@ -2374,9 +2387,14 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (hc[1]) {
     if (kseq) {
       amgd_route_hit(AMGD_R_SG_WSYM);
-      k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
-          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
-          nullptr, curs);
+      if (sg_symbits())
+        k_sg_wwin<32768, 2><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+            lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+            nullptr, curs);
+      else
+        k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+            lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+            nullptr, curs);
     } else {
       k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,

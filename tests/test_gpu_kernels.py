@@ -250,11 +250,13 @@ def _rows_masked(B, m):
     return np.array(ro), np.array(cols, dtype=np.int64), np.array(vals)
 
 
+@pytest.mark.parametrize("bits", [1, 0], ids=["bitmap", "bytemap"])
 @pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
-def test_spgemm_symbolic_windows(case):
-    """symbolic pass of rows with many products: the wave-private 4096-column byte windows
-    (k_sg_wwin MODE 0: several windows per row, A rows past 64 layers with cursors in
-    scratch, column clusters far apart)"""
+def test_spgemm_symbolic_windows(case, bits):
+    """symbolic pass of rows with many products: the wave-private windows -- 32768-column
+    bit maps (k_sg_wwin MODE 2, default) or 4096-column byte maps (MODE 0) -- several
+    windows per row, A rows past 64 layers with cursors in scratch, column clusters far
+    apart"""
     rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54,
                                  "gapped": 55}[case])
     if case == "wide":
@@ -277,7 +279,11 @@ def test_spgemm_symbolic_windows(case):
     assert B.a.size >= 64 * B.rn
     R = refops.spgemm(A, B)
     oa.route_stats(reset=True)
-    X = oa.test_csr_op(0, A, B)
+    oa.sg_symbits(bits)
+    try:
+        X = oa.test_csr_op(0, A, B)
+    finally:
+        oa.sg_symbits(-1)
     assert oa.route_stats(reset=True)["sg_wsym"] > 0
     assert refops.same(X, R)
 
