@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
         L.amgd_test_sg_xcd.argtypes = [C.c_int]
         L.amgd_test_sg_symbits.argtypes = [C.c_int]
+        L.amgd_test_sg_ww.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -419,6 +420,12 @@ def sg_xcd(mask: int) -> None:
     """SpGEMM work-groups in XCD-contiguous order (bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row;
     0 the hardware's round-robin order, -1 back to AMGD_SG_XCD).  Same bits."""
     lib().amgd_test_sg_xcd(int(mask))
+
+
+def sg_ww(w: int) -> None:
+    """numeric wave-private SpGEMM windows of 1024 (default) or 2048 doubles, -1 back to
+    AMGD_SG_WW.  Same sums in the same order."""
+    lib().amgd_test_sg_ww(int(w))
 
 
 def sg_symbits(on: int) -> None:

@@ -2327,6 +2327,15 @@ static int sg_symbits() {
   if (g_symbits < 0) { const char *e = getenv("AMGD_SG_SYMBITS"); g_symbits = e && *e ? atoi(e) : 1; }
   return g_symbits;
 }
+// numeric wave-private windows: 1024 doubles (8 KB per wavefront, default), 2048 (half
+// the window passes, half the resident blocks: slower, 256^3 AfW 981 -> 1235 ms) or 512
+// (AMGD_SG_WW / amgd_spgemm_set_ww)
+static int g_ww = -1;
+extern "C" void amgd_spgemm_set_ww(int w) { g_ww = w; }
+static int sg_ww() {
+  if (g_ww < 0) { const char *e = getenv("AMGD_SG_WW"); g_ww = e && *e ? atoi(e) : 1024; }
+  return g_ww;
+}
 static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (g_sg_xcd < 0) amgd_spgemm_set_xcd(-1);
   if (A->cn != B->rn) {
@@ -2521,8 +2530,16 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
 #undef SG_NUM
   // windowed rows: wave-private 1024-column windows (k_sg_wwin, round 3)
-  if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
-  if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
+  if (sg_ww() == 2048) {
+    if (win && wn[0]) SG_WW(2048, wlists, wn[0]);
+    if (win && wn[2]) SG_WW(2048, wlists + L, wn[2]);
+  } else if (sg_ww() == 512) {
+    if (win && wn[0]) SG_WW(512, wlists, wn[0]);
+    if (win && wn[2]) SG_WW(512, wlists + L, wn[2]);
+  } else {
+    if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
+    if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
+  }
   if (hn[4]) {
     if (rap)
       k_spgemm_long<1, 1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,

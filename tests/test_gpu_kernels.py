@@ -142,13 +142,14 @@ def _banded(rng, rn, kn, cn, width, dens, blen, span, ints=True, dups=False, emp
     return A, B
 
 
+@pytest.mark.parametrize("ww", [1024, 2048, 512])
 @pytest.mark.parametrize("win", [0, 1024, 2048, 8192, -1])
 @pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
                                   "huge_a", "gapped", "dense_rows"])
-def test_spgemm_wave_windows(case, win):
+def test_spgemm_wave_windows(case, win, ww):
     """wave-private windowed kernel (k_sg_wwin: one wavefront per row, its own LDS window,
     no barrier per layer; 4096-column byte windows for the symbolic counts, 1024-column
-    numeric windows) with every wide row routed to it (win > 0, at several routing
+    (or 2048-column) numeric windows) with every wide row routed to it (win > 0, at several routing
     widths), none (0: LDS hash kernels) or the default routing (-1): vs the host
     restatement, bit for bit -- rows of more than 64 layers (cursors in scratch),
     duplicate A columns, exact cancellation, empty rows, column clusters far apart
@@ -177,14 +178,18 @@ def test_spgemm_wave_windows(case, win):
         A = refops.rand_csr(rng, 20, 200, 0.3)
         B = refops.rand_csr(rng, 200, 9000, 0.2)
     assert B.a.size >= 64 * B.rn
+    if win == 0 and ww != 1024:
+        pytest.skip("no windowed rows")
     R = refops.spgemm(A, B)
     oa.spgemm_flat(False)
     oa.spgemm_win(win)
+    oa.sg_ww(ww)
     oa.route_stats(reset=True)
     try:
         X = oa.test_csr_op(0, A, B)
     finally:
         oa.spgemm_win(-1)
+        oa.sg_ww(-1)
     routes = oa.route_stats(reset=True)
     if win > 0:
         assert routes["sg_win"] > 0

@@ -1,0 +1,12 @@
+# kernel stats of one 256^3 setup: default, byte-map symbolic windows, 2048-wide numeric windows
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+D=$GRAFT_REPO_ROOT/gpurun_out/r04q
+rm -rf $D; mkdir -p $D
+export PYTHONPATH=$GRAFT_REPO_ROOT
+for v in ww512 default; do
+  case $v in default) E="";; sb0) E="AMGD_SG_SYMBITS=0";; ww2048) E="AMGD_SG_WW=2048";; ww512) E="AMGD_SG_WW=512";; esac
+  ( [ -n "$E" ] && export "$E"; exec timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/$v -o p -- python3 tools/probe_configs.py p7_256 > $D/$v.log 2>&1 ); r=$?; echo "$v rc=$r"; [ $r -eq 0 ] || exit 1
+  f=$(find $D/$v -name "*kernel_stats.csv" | head -1); python3 tools/kstats.py $f 12 > $D/$v.top.txt; grep -E "total|wwin" $D/$v.top.txt; grep -o '"setup_s": [0-9.]*' $D/$v.log || true
+  find $D/$v -name "*kernel_trace.csv" -delete
+done
