@@ -101,9 +101,6 @@ def lib() -> C.CDLL:
         L.amgd_test_spgemm_win.argtypes = [C.c_int]
         L.amgd_test_qf_reuse.argtypes = [C.c_int]
         L.amgd_test_sg_pattern.argtypes = [C.c_int]
-        L.amgd_test_sg_xcd.argtypes = [C.c_int]
-        L.amgd_test_sg_symbits.argtypes = [C.c_int]
-        L.amgd_test_sg_ww.argtypes = [C.c_int]
         L.amgd_test_lmop_wave.argtypes = [C.c_int]
         L.amgd_test_lmop_small.argtypes = [C.c_int]
         L.amgd_test_lmop_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -414,24 +411,6 @@ def lmop_wave(n: int) -> None:
     walk one wavefront per (c, k) with 64 columns searched at once (default 64), 0 one
     thread per (c, k) always, -1 default / AMGD_LMOP_WAVE.  Same landings."""
     lib().amgd_test_lmop_wave(int(n))
-
-
-def sg_xcd(mask: int) -> None:
-    """SpGEMM work-groups in XCD-contiguous order (bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row;
-    0 the hardware's round-robin order, -1 back to AMGD_SG_XCD).  Same bits."""
-    lib().amgd_test_sg_xcd(int(mask))
-
-
-def sg_ww(w: int) -> None:
-    """numeric wave-private SpGEMM windows of 1024 (default) or 2048 doubles, -1 back to
-    AMGD_SG_WW.  Same sums in the same order."""
-    lib().amgd_test_sg_ww(int(w))
-
-
-def sg_symbits(on: int) -> None:
-    """symbolic pass of wide long-B-row SpGEMM rows: 1 bit-map windows of 32768 columns
-    (default), 0 byte-map windows of 4096, -1 back to AMGD_SG_SYMBITS.  Same counts."""
-    lib().amgd_test_sg_symbits(int(on))
 
 
 def sg_pattern(on: int) -> None:

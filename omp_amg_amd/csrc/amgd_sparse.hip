@@ -24,17 +24,6 @@
 #include "amgd.h"
 #include "amgd_dev.h"
 
-// XCD-contiguous block order (AMGD_SG_XCD bits: 1 k_sg_wwin, 2 k_sg_kseq, 4 k_sg_row): the
-// hardware deals work-groups to the 8 XCDs round robin (blockIdx % 8); remapped, XCD x runs
-// one contiguous run of the row list, so neighbouring output rows -- which read mostly the
-// same B rows -- share that XCD's L2 (RAP kernels at 7-29 % L2 hit rate)
-__device__ int d_sg_xcd = 0;
-__device__ __forceinline__ uint32_t xcd_block(int bit) {
-  const uint32_t b = blockIdx.x, G = gridDim.x;
-  if (!(d_sg_xcd & bit) || G < 16) return b;
-  const uint32_t x = b & 7, i = b >> 3, q = G >> 3, r = G & 7;
-  return x * q + (x < r ? x : r) + i;
-}
 static int bits_for(uint64_t v) {  // bits needed to represent v
   int b = 0;
   while (b < 64 && (v >> b) != 0) b++;
@@ -1641,7 +1630,7 @@ __global__ __launch_bounds__(NT) void k_sg_row(const uint32_t *rows, uint32_t nr
   __shared__ unsigned nfill;
   __shared__ int ovf;
   const int t = threadIdx.x;
-  for (uint32_t r = xcd_block(4); r < nrows; r += gridDim.x) {
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     for (uint32_t s = t; s < S; s += NT) {
       hk[s] = EMPTY_KEY;
@@ -1777,7 +1766,7 @@ __global__ __launch_bounds__(NT) void k_sg_kseq(const uint32_t *rows, uint32_t n
   __shared__ unsigned nfill;
   __shared__ int ovf;
   const int t = threadIdx.x;
-  for (uint32_t r = xcd_block(2); r < nrows; r += gridDim.x) {
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     const uint32_t i = rows[r];
     for (uint32_t s = t; s < S; s += NT) {
       hk[s] = EMPTY_KEY;
@@ -1965,14 +1954,6 @@ static bool sg_force_flat() {
   return g_sg_flat == 1;
 }
 extern "C" void amgd_spgemm_force_flat(int on) { g_sg_flat = on ? 1 : 0; }
-static int g_sg_xcd = -1;     // host copy of d_sg_xcd (-1: not yet read from AMGD_SG_XCD)
-extern "C" void amgd_spgemm_set_xcd(int m) {
-  if (m < 0) { const char *e = getenv("AMGD_SG_XCD"); m = e && *e ? atoi(e) : 0; }
-  if (m == g_sg_xcd) return;
-  g_sg_xcd = m;
-  HIPCK(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_sg_xcd), &m, sizeof(int), 0, hipMemcpyHostToDevice, amgd_s()));
-  HIPCK(hipStreamSynchronize(amgd_s()));
-}
 static int g_sg_win_forced = 0; // tests: the window applies whatever the column count
 static int g_sg_win = -1;       // AMGD_SG_WIN: window of the dense-accumulator kernel (0: off)
 static int sg_win() {
@@ -2105,8 +2086,8 @@ __global__ void k_span_hist(const uint64_t *ro, const uint32_t *col, uint32_t rn
 // more than 64 layers keep their cursors in global scratch indexed by the A entry.
 // Every output is the sum, from +0 in ascending k, of its products -- mxm's order
 // (amg_setup.c:1894-1960) -- and the window is emitted in column order, coalesced.
-// MODE 0: distinct columns per row (byte map, W columns); MODE 2: the same with a bit map
-// (W columns in W / 8 bytes: 8x fewer windows over a wide row); MODE 1: values (W doubles).
+// MODE 2: distinct columns per row (a bit map: W columns in W / 8 bytes); MODE 1: values
+// (W doubles).
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -2124,8 +2105,9 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
                                                  uint64_t *cnt, const uint64_t *xro,
                                                  uint32_t *xcol, double *xa, uint32_t *curs) {
   constexpr int NWV = 4, D = 4;
+  static_assert(MODE == 1 || MODE == 2, "k_sg_wwin: MODE 1 (values) or 2 (bit-map counts)");
   constexpr bool NUM = MODE == 1;
-  constexpr int WB = NUM ? W * 8 : MODE == 2 ? W / 8 : W;   // LDS bytes per wavefront
+  constexpr int WB = NUM ? W * 8 : W / 8;           // LDS bytes per wavefront
   constexpr uint32_t NONE = 0xffffffffu;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NWV * WB];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2136,7 +2118,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
   // curs holds nnz(A) cursors from A's first entry: a row-range view of a larger matrix
   // (sharded products) keeps absolute row offsets
   const uint64_t cbase = aro[0];
-  for (uint32_t r = xcd_block(1) * NWV + wv; r < nrows; r += gridDim.x * NWV) {
+  for (uint32_t r = blockIdx.x * NWV + wv; r < nrows; r += gridDim.x * NWV) {
     const uint32_t i = rows[r];
     const uint64_t a0 = aro[i];
     const uint32_t nl = (uint32_t)(aro[i + 1] - a0);
@@ -2224,10 +2206,8 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
               if (NUM) {
                 double *p = acc + (col - wb);
                 *p = *p + val * av;
-              } else if (MODE == 2) {
-                atomicOr(&mp32[(col - wb) >> 5], 1u << ((col - wb) & 31));
               } else {
-                mp[col - wb] = 1;
+                atomicOr(&mp32[(col - wb) >> 5], 1u << ((col - wb) & 31));
               }
             }
             const uint32_t n = (uint32_t)__popcll(__ballot(in));
@@ -2266,8 +2246,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
         }
       } else {
         uint32_t c = 0;
-        for (int q = lane; q < WB / 4; q += 64)
-          c += (uint32_t)__popc(MODE == 2 ? mp32[q] : mp32[q] & 0x01010101u);
+        for (int q = lane; q < WB / 4; q += 64) c += (uint32_t)__popc(mp32[q]);
         for (int o = 32; o; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
         nout += c;
       }
@@ -2319,25 +2298,7 @@ __global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *ar
     if (valid && !w) hl[q] = i;
   }
 }
-// symbolic wide rows: bit-map windows (MODE 2, 32768 columns) or byte maps (MODE 0, 4096);
-// AMGD_SG_SYMBITS=0 / amgd_spgemm_set_symbits (tests) select the byte maps
-static int g_symbits = -1;
-extern "C" void amgd_spgemm_set_symbits(int on) { g_symbits = on; }
-static int sg_symbits() {
-  if (g_symbits < 0) { const char *e = getenv("AMGD_SG_SYMBITS"); g_symbits = e && *e ? atoi(e) : 1; }
-  return g_symbits;
-}
-// numeric wave-private windows: 1024 doubles (8 KB per wavefront, default), 2048 (half
-// the window passes, half the resident blocks: slower, 256^3 AfW 981 -> 1235 ms) or 512
-// (AMGD_SG_WW / amgd_spgemm_set_ww)
-static int g_ww = -1;
-extern "C" void amgd_spgemm_set_ww(int w) { g_ww = w; }
-static int sg_ww() {
-  if (g_ww < 0) { const char *e = getenv("AMGD_SG_WW"); g_ww = e && *e ? atoi(e) : 1024; }
-  return g_ww;
-}
 static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
-  if (g_sg_xcd < 0) amgd_spgemm_set_xcd(-1);
   if (A->cn != B->rn) {
     fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
     abort();
@@ -2389,21 +2350,18 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_row<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
-  // wide symbolic rows of long-B-row products: wave-private 4096-column byte windows
-  // (k_sg_wwin MODE 0, round 3); their cursors live in `curs` (one per A entry)
+  // wide symbolic rows of long-B-row products: wave-private bit-map windows (k_sg_wwin
+  // MODE 2); their cursors live in `curs` (one per A entry)
   uint32_t *curs = nullptr;
   if (kseq) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
   if (hc[1]) {
     if (kseq) {
       amgd_route_hit(AMGD_R_SG_WSYM);
-      if (sg_symbits())
-        k_sg_wwin<32768, 2><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
-            lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
-            nullptr, curs);
-      else
-        k_sg_wwin<4096, 0><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
-            lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
-            nullptr, curs);
+      // bit-map windows of 32768 columns in 4 KB (round 4; the 4096-column byte maps
+      // took 1239 against 909 ms per 256^3 setup, profiles/r04/ab_sym_ww)
+      k_sg_wwin<32768, 2><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
+          lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
+          nullptr, curs);
     } else {
       k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
@@ -2530,16 +2488,10 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
 #undef SG_NUM
   // windowed rows: wave-private 1024-column windows (k_sg_wwin, round 3)
-  if (sg_ww() == 2048) {
-    if (win && wn[0]) SG_WW(2048, wlists, wn[0]);
-    if (win && wn[2]) SG_WW(2048, wlists + L, wn[2]);
-  } else if (sg_ww() == 512) {
-    if (win && wn[0]) SG_WW(512, wlists, wn[0]);
-    if (win && wn[2]) SG_WW(512, wlists + L, wn[2]);
-  } else {
-    if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
-    if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
-  }
+  // (1024 doubles per wavefront: 512 and 2048 measured slower at 256^3 -- 1081 / 1235
+  // against 987 ms for the interpolation's windowed products, profiles/r04/ab_sym_ww)
+  if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
+  if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
   if (hn[4]) {
     if (rap)
       k_spgemm_long<1, 1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,

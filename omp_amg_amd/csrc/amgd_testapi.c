@@ -193,15 +193,6 @@ void amgd_lmop_set_small(int n);
 API void amgd_test_lmop_small(int n) { amgd_lmop_set_small(n); }
 void amgd_lmop_set_wave(int n);
 API void amgd_test_lmop_wave(int n) { amgd_lmop_set_wave(n); }
-void amgd_spgemm_set_xcd(int m);
-/* XCD-contiguous block order of the SpGEMM kernels (bits 1 wwin, 2 kseq, 4 row; -1: env) */
-API void amgd_test_sg_xcd(int m) { amgd_spgemm_set_xcd(m); }
-void amgd_spgemm_set_ww(int w);
-/* numeric wave-private SpGEMM windows: 1024 or 2048 doubles, -1 env */
-API void amgd_test_sg_ww(int w) { amgd_spgemm_set_ww(w); }
-void amgd_spgemm_set_symbits(int on);
-/* symbolic wide rows: 1 bit-map windows (default), 0 byte maps, -1 env */
-API void amgd_test_sg_symbits(int on) { amgd_spgemm_set_symbits(on); }
 void amgd_spgemm_set_pattern(int on);
 API void amgd_test_sg_pattern(int on) { amgd_spgemm_set_pattern(on); }
 /* Q factors taken by copy from the previous iteration / factored, since the last call */

@@ -142,14 +142,13 @@ def _banded(rng, rn, kn, cn, width, dens, blen, span, ints=True, dups=False, emp
     return A, B
 
 
-@pytest.mark.parametrize("ww", [1024, 2048, 512])
 @pytest.mark.parametrize("win", [0, 1024, 2048, 8192, -1])
 @pytest.mark.parametrize("case", ["banded", "long_a", "dups_cancel", "ragged", "wide_span",
                                   "huge_a", "gapped", "dense_rows"])
-def test_spgemm_wave_windows(case, win, ww):
+def test_spgemm_wave_windows(case, win):
     """wave-private windowed kernel (k_sg_wwin: one wavefront per row, its own LDS window,
-    no barrier per layer; 4096-column byte windows for the symbolic counts, 1024-column
-    (or 2048-column) numeric windows) with every wide row routed to it (win > 0, at several routing
+    no barrier per layer; 32768-column bit-map windows for the symbolic counts, 1024-column
+    numeric windows) with every wide row routed to it (win > 0, at several routing
     widths), none (0: LDS hash kernels) or the default routing (-1): vs the host
     restatement, bit for bit -- rows of more than 64 layers (cursors in scratch),
     duplicate A columns, exact cancellation, empty rows, column clusters far apart
@@ -178,18 +177,14 @@ def test_spgemm_wave_windows(case, win, ww):
         A = refops.rand_csr(rng, 20, 200, 0.3)
         B = refops.rand_csr(rng, 200, 9000, 0.2)
     assert B.a.size >= 64 * B.rn
-    if win == 0 and ww != 1024:
-        pytest.skip("no windowed rows")
     R = refops.spgemm(A, B)
     oa.spgemm_flat(False)
     oa.spgemm_win(win)
-    oa.sg_ww(ww)
     oa.route_stats(reset=True)
     try:
         X = oa.test_csr_op(0, A, B)
     finally:
         oa.spgemm_win(-1)
-        oa.sg_ww(-1)
     routes = oa.route_stats(reset=True)
     if win > 0:
         assert routes["sg_win"] > 0
@@ -255,13 +250,11 @@ def _rows_masked(B, m):
     return np.array(ro), np.array(cols, dtype=np.int64), np.array(vals)
 
 
-@pytest.mark.parametrize("bits", [1, 0], ids=["bitmap", "bytemap"])
 @pytest.mark.parametrize("case", ["wide", "dense_rows", "wide_span", "long_a_rows", "gapped"])
-def test_spgemm_symbolic_windows(case, bits):
-    """symbolic pass of rows with many products: the wave-private windows -- 32768-column
-    bit maps (k_sg_wwin MODE 2, default) or 4096-column byte maps (MODE 0) -- several
-    windows per row, A rows past 64 layers with cursors in scratch, column clusters far
-    apart"""
+def test_spgemm_symbolic_windows(case):
+    """symbolic pass of rows with many products: the wave-private 32768-column bit-map
+    windows (k_sg_wwin MODE 2) -- several windows per row, A rows past 64 layers with
+    cursors in scratch, column clusters far apart"""
     rng = np.random.default_rng({"wide": 51, "dense_rows": 52, "wide_span": 53, "long_a_rows": 54,
                                  "gapped": 55}[case])
     if case == "wide":
@@ -284,11 +277,7 @@ def test_spgemm_symbolic_windows(case, bits):
     assert B.a.size >= 64 * B.rn
     R = refops.spgemm(A, B)
     oa.route_stats(reset=True)
-    oa.sg_symbits(bits)
-    try:
-        X = oa.test_csr_op(0, A, B)
-    finally:
-        oa.sg_symbits(-1)
+    X = oa.test_csr_op(0, A, B)
     assert oa.route_stats(reset=True)["sg_wsym"] > 0
     assert refops.same(X, R)
 
