@@ -1310,6 +1310,10 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
                                const amg_uint *Aj, const double *A, amg_uint null_space,
                                const struct comm *comm) {
   const int np = comm ? (int)comm->np : 1, me = comm ? (int)comm->id : 0;
+  if (amgd_rt_init(0) != 0) {
+    fprintf(stderr, "omp_amg_amd: crs_setup needs a HIP device: %s\n", amgd_last_error());
+    return NULL;
+  }
   if (np > 1 && (amgd_comm_procs() != np || amgd_comm_rank() != me)) {
     fprintf(stderr, "omp_amg_amd: crs_setup with np = %d needs the library communicator of the same "
             "ranks (amgd_comm_init_rccl / amgd_comm_init_host; have %d processes, rank %d)\n", np,

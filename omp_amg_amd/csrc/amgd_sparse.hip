@@ -1212,6 +1212,9 @@ __global__ __launch_bounds__(256) void k_mpm_flag(const uint64_t *aro, const uin
     if (lane == 0) longrow[i] = anyd ? 0 : 1;
   }
 }
+// The other row's columns are staged in LDS when they fit (MPM_LDS per wavefront): the
+// binary searches then read LDS instead of issuing ~log2(n) dependent global loads each.
+#define MPM_LDS 2048
 template <bool FILL>
 __global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uint32_t *acol,
                                                   const double *aa, const uint64_t *bro,
@@ -1220,14 +1223,28 @@ __global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uin
                                                   const uint8_t *longrow, uint64_t *cnt,
                                                   const uint64_t *xro, uint32_t *xcol,
                                                   double *xa) {
-  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t stage[4][MPM_LDS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // the columns of a row [k, k + n) where the searches read them: LDS if they fit
+  auto stage_cols = [&](const uint32_t *colv, uint64_t k, uint32_t n) -> const uint32_t * {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (n > MPM_LDS) return colv + k;
+    for (uint32_t e = lane; e < n; e += 64) stage[w][e] = colv[k + e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return stage[w];
+  };
   for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6; i < rn;
        i += (uint64_t)gridDim.x * 4) {
     if (!longrow[i]) continue;
     const uint64_t ka = aro[i], kb = bro[i];
     const uint32_t na = (uint32_t)(aro[i + 1] - ka), nb = (uint32_t)(bro[i + 1] - kb);
     const uint64_t o = FILL ? xro[i] : 0;
+    const uint32_t *sb = stage_cols(bcol, kb, nb);
     uint32_t cm = 0, cd = 0;                      // matched / dropped so far (A side)
     for (uint32_t p0 = 0; p0 < na; p0 += 64) {
       const uint32_t p = p0 + lane;
@@ -1236,8 +1253,8 @@ __global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uin
       double v = 0.0;
       if (has) {
         c = acol[ka + p];
-        bs = lower_bound_u32(bcol + kb, nb, c);
-        m = bs < nb && bcol[kb + bs] == c;
+        bs = lower_bound_u32(sb, nb, c);
+        m = bs < nb && sb[bs] == c;
         if (m) {
           v = alpha * aa[ka + p] + beta * ba[kb + bs];
           d = !(v != 0.0);
@@ -1258,6 +1275,7 @@ __global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uin
       if (lane == 0) cnt[i] = (uint64_t)na + nb - cm - cd;
       continue;
     }
+    const uint32_t *sa = stage_cols(acol, ka, na);
     uint32_t bmc = 0, bdc = 0;                    // matched / dropped so far (B side)
     for (uint32_t q0 = 0; q0 < nb; q0 += 64) {
       const uint32_t q = q0 + lane;
@@ -1265,8 +1283,8 @@ __global__ __launch_bounds__(256) void k_mpm_wave(const uint64_t *aro, const uin
       uint32_t c = 0, as = 0;
       if (has) {
         c = bcol[kb + q];
-        as = lower_bound_u32(acol + ka, na, c);
-        m = as < na && acol[ka + as] == c;
+        as = lower_bound_u32(sa, na, c);
+        m = as < na && sa[as] == c;
         if (m) d = !((alpha * aa[ka + as] + beta * ba[kb + q]) != 0.0);
       }
       const uint64_t bm = __ballot(m), bd = __ballot(d);

@@ -851,14 +851,19 @@ def test_expand_pick(case):
     assert refops.same(oa.test_csr_op(6, X), refops.expand_pick(X))
 
 
-@pytest.mark.parametrize("seed", [0, 1])
+@pytest.mark.parametrize("seed", [0, 1, 2])
 def test_mpm_long_rows_rank_placement(seed):
     """rows of >= 64 merged entries take the wave-per-row rank placement:
     disjoint, overlapping and cancelling (exact-zero dropped) entries, short rows
-    mixed in, and a row with a repeated column (left to the sequential merge)"""
+    mixed in, and a row with a repeated column (left to the sequential merge); seed 2:
+    rows of 1 000 - 5 000 entries, around the 2048 columns staged in LDS for the searches"""
     rng = np.random.default_rng(seed)
-    A = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
-    C = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
+    if seed == 2:
+        A = refops.rand_csr(rng, 60, 30000, 0.1, ints=True)
+        C = refops.rand_csr(rng, 60, 30000, 0.05, ints=True)
+    else:
+        A = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
+        C = refops.rand_csr(rng, 300, 3000, 0.03, ints=True)
     # B: A's pattern, half the values equal (A - B cancels there), plus C's entries
     a2 = A.a.copy()
     flip = rng.random(len(a2)) < 0.5
