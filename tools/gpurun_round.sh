@@ -3,12 +3,12 @@
 # usage: bash tools/gpurun_round.sh <tag>    (SKIP_TESTS=1: bench + profile only)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=${1:-r03}
+TAG=${1:-r04}
 D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 rm -rf $D; mkdir -p $D
 export PYTHONPATH=$GRAFT_REPO_ROOT
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $D/gputests.log 2>&1 || { tail -30 $D/gputests.log; exit 1; }
+timeout -k 10 1080 python3 -u -m pytest tests -m gpu -x -q --durations=15 --timeout 300 --timeout-method thread > $D/gputests.log 2>&1 || { tail -30 $D/gputests.log; exit 1; }
 tail -2 $D/gputests.log
 fi
 t0=$(date +%s)
