@@ -752,9 +752,14 @@ static int lane_rw(uint64_t n) {
 }
 // Long-row products: k_spmv_pipe, 16 entries per lane per round (round 3: 256^3 SpMV
 // 6.26 -> 5.46 s against the round-2 lane kernel; 8 per lane 5.64 s, 4: 6.98 s, 12:
-// 7.95 s -- tools/ab_setup.py, r03m).  The round-2 lane kernel, the contiguous-chunk
-// kernel, nontemporal loads and the fused selection / column-sum variants measured
-// slower and were removed in round 4.
+// 7.95 s -- tools/ab_setup.py, r03m) -- except 8 for 4 rows per wavefront (round 4, per
+// shape: RW=4 2041 -> 1580 ms and its list form 400 -> 309 ms per setup, half the
+// registers, twice the wavefronts in flight on the coarse levels' few long rows; RW=16
+// with 8 per lane: 2604 -> 2804 ms, RW=64 with 8: 723 -> 1132 ms, 8 rows x 8 in place of
+// RW=16: 2639 -> 2727 ms; the RW 4 / 16 boundary at 2^16 rows stays: 2^18 / 2^20 /
+// everywhere RW=4 measured slower, profiles/r04/ab_spmv_per).  The round-2
+// lane kernel, the contiguous-chunk kernel, nontemporal loads and the fused selection /
+// column-sum variants measured slower and were removed in round 4.
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
@@ -768,8 +773,8 @@ static int lane_rw(uint64_t n) {
       k_spmv_pipe<LIST, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,     \
                                                        z_, al, y_, be, f_, ml_);              \
     else                                                                                      \
-      k_spmv_pipe<LIST, 4><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,      \
-                                                      z_, al, y_, be, f_, ml_);               \
+      k_spmv_pipe<LIST, 4, 8><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,   \
+                                                         z_, al, y_, be, f_, ml_);            \
   } while (0)
 // ordered sums (x == nullptr) or products of the listed rows only (rows longer than
 // maxlen are skipped: k_rows_exact does them)
