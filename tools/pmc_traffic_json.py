@@ -29,7 +29,7 @@ fk, fn = counter(f"{d0}/calib_FETCH_SIZE", "FETCH_SIZE")
 wk, wn = counter(f"{d0}/calib_WRITE_SIZE", "WRITE_SIZE")
 f_fetch = cal["read_bytes_per_product"] / (fk * 1024 / fn)
 f_write = cal["write_bytes_per_product"] / (wk * 1024 / wn)
-names = {"spmv": "k_spmv_pipe<false,RW,16> (roofline kernel)",
+names = {"spmv": "k_spmv_pipe<false,RW,PER> (roofline kernel)",
          "rap": "RAP SpGEMM numeric kernels (rap_roofline)"}
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per pass (tools/gpurun_pmc.sh), "
                  f"one 256^3 setup (tools/probe_scale.py 256), tree of {tag}",
@@ -47,6 +47,9 @@ for k in ("spmv", "rap"):
         v, n = counter(f"{d0}/traffic_{k}_{c}", c)
         d[c + "_raw_KB"] = v
         d["dispatches"] = n
+    # L2->fabric bytes (MALL hits included: an upper bound on HBM bytes); the key keeps its
+    # round-2 name for the files already committed
     d["hbm_bytes"] = (f_fetch * d["FETCH_SIZE_raw_KB"] + f_write * d["WRITE_SIZE_raw_KB"]) * 1024
+    d["bytes_are"] = "L2->fabric (FETCH_SIZE/WRITE_SIZE, calibrated): an upper bound on HBM bytes"
     out[k] = d
 print(json.dumps(out, indent=1))
