@@ -2321,6 +2321,26 @@ __global__ void k_win_split(const uint32_t *list, uint32_t n, const uint64_t *ar
     if (valid && !w) hl[q] = i;
   }
 }
+// Row lists in ascending row order.  The binning appends a wavefront's rows as one run,
+// the runs in whatever order the wavefronts finished, so the rows in flight at once were
+// spread over the whole matrix; sorted, the work-groups in flight (and each XCD's share of
+// them) cover a narrow band of rows, whose products read mostly the same B rows.  Rows
+// are independent: the order changes no value.  256^3 (profiles/r04/ab_sg_sort): symbolic
+// windows 913 -> 813 ms, numeric windows 989 -> 803 and 505 -> 411 ms (RAP), the 8192-slot
+// hash bins 364 -> 349 and 221 -> 211 ms; sorting the cheap bins as well changed nothing.
+static void sort_list(uint32_t *list, unsigned n, uint32_t rn) {
+  if (n < 2048) return;
+  hipStream_t s = amgd_s();
+  uint32_t *tmpk = (uint32_t *)amgd_alloc((size_t)n * 4 + 4);
+  size_t tb = 0;
+  const int eb = bits_for(rn);
+  HIPCK(rocprim::radix_sort_keys(nullptr, tb, list, tmpk, (size_t)n, 0, eb, s));
+  void *tmp = amgd_alloc(tb + 16);
+  HIPCK(rocprim::radix_sort_keys(tmp, tb, list, tmpk, (size_t)n, 0, eb, s));
+  HIPCK(hipMemcpyAsync(list, tmpk, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+  amgd_free(tmp);
+  amgd_free(tmpk);
+}
 static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (A->cn != B->rn) {
     fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
@@ -2354,6 +2374,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     if (tiny_on) k_tiny_list<<<grid_for(rn), 256, 0, s>>>(ub, rn, tlist, counts + 5);
     KCHECK();
     amgd_d2h(hc, counts, 24);
+    sort_list(lists + L, hc[1], rn);           // the wide rows (cheap ones: no gain measured)
   }
   const unsigned ntiny = hc[5];
   if (ntiny) amgd_route_hit(AMGD_R_SG_TINY);
@@ -2402,6 +2423,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     k_bin_rows<<<grid_for(rn), 256, 0, s>>>(cnt, rn, b, 5, 1, lists, counts, tsk, SG_TINY);
     KCHECK();
     amgd_d2h(hn, counts, 20);
+    for (int q = 1; q < 5; q++) sort_list(lists + q * L, hn[q], rn);
   }
   double *slab_v = nullptr;
   uint32_t *slab_s = nullptr;
@@ -2461,6 +2483,10 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       amgd_free(tmp);
     }
     amgd_d2h(wn, wc, 16);
+    sort_list(wlists, wn[0], rn);
+    sort_list(wlists + L, wn[2], rn);
+    sort_list(lists + 3 * L, wn[1], rn);
+    sort_list(lists + 4 * L, wn[3], rn);
     amgd_free(wc);
     hn[3] = wn[1];
     hn[4] = wn[3];
