@@ -327,11 +327,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"3D {args.stencil}-point Poisson {args.m}^3 CSR, full AMG setup "
-                                   f"(BASELINE configs[1])",
+            "config": {"workload": f"3D {args.stencil}-point Poisson {args.m}^3 CSR, full AMG setup"
+                                   + (" (BASELINE configs[1])" if (args.m, args.stencil) == (256, 7) else ""),
                        "rows": rows, "nnz": int(st["nnz0"]), "levels": int(st["nlevels"]),
                        "parallelism": (f"rows partitioned x{world} (row blocks of every matrix per rank, "
-                                       f"halo rows before each product, {args.transport.upper()} over xGMI)"
+                                       + ("halo rows before each product, RCCL over xGMI)" if args.transport == "rccl"
+                                          else "halo rows before each product, host-staged gloo rehearsal)")
                                        if part else
                                        f"rows sharded x{world} (replicated hierarchy, RCCL allgatherv over xGMI)"
                                        if sharded and args.transport == "rccl" else
