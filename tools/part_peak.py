@@ -102,6 +102,13 @@ def main():
     ps = [subprocess.Popen([sys.executable, "-u", __file__, str(a.m), str(a.N), "--role", "rank",
                             "--stencil", str(a.stencil)], env=dict(env, RANK=str(r)),
                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(a.N)]
+    t_start = time.time()
+    while any(q.poll() is None for q in ps):           # heartbeat: long runs print progress
+        time.sleep(30)
+        print(f"[part_peak] {time.time() - t_start:.0f} s, {sum(q.poll() is None for q in ps)} ranks running",
+              flush=True)
+        if time.time() - t_start > a.timeout:
+            break
     ranks = []
     for q in ps:
         o, e = q.communicate(timeout=a.timeout)
