@@ -336,10 +336,16 @@ typedef struct {
   double *Q;           /* packed Q factors of those coarse points */
   uint64_t *qoff, qtot;
   pmat *S, *W0, *W0t;
+  dcsr *Qbuf;          /* when set, Q points into it (the halo view of interp_lmop) */
 } pfactor;
+/* the buffer a factor's Q lives in */
+static void q_release(double *Q, dcsr **Qbuf) {
+  if (*Qbuf) pm_ext_free(Qbuf);
+  else if (Q) amgd_free(Q);
+}
 static void pfactor_free(pfactor *f) {
   pm_free(&f->Wt);
-  if (f->Q) amgd_free(f->Q);
+  q_release(f->Q, &f->Qbuf);
   if (f->qoff) amgd_free(f->qoff);
   pm_free(&f->S); pm_free(&f->W0); pm_free(&f->W0t);
 }
@@ -423,7 +429,7 @@ static void p_lmop_prefix(pmat *S, const pfactor *f, const pmat *qp, const doubl
   dcsr_free(&Sf); dcsr_free(&WtD); dcsr_free(&QD);
   free(spl);
 }
-static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u) {
+static void p_lmop(pmat *S, const pmat *Wskel, pfactor *f, const double *u) {
   dcsr *WtE = pm_halo_rows(f->Wt, Wskel->m);
   /* the Q factors as a matrix whose row c holds Q_c (offsets qoff): halo rows of it */
   dcsr qm;
@@ -444,6 +450,17 @@ static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u
     amgd_lmop_set_prefix(D);
   }
   dcsr *QE = pm_halo_rows(&qp, Wskel->m);
+  {
+    /* the own Q factors now sit in the view too (a contiguous copy at the own rows):
+       the factor keeps that copy and its own buffer goes, instead of two copies of the
+       own share through interp_lmop's peak */
+    uint64_t o = 0;
+    amgd_d2h(&o, QE->ro + f->Wt->rp->split[g_me], 8);
+    q_release(f->Q, &f->Qbuf);
+    f->Q = QE->a + o;
+    f->Qbuf = QE;
+    qm.a = f->Q;
+  }
   uint32_t *kpos = pm_kpos(Wskel, WtE);
   dcsr gS = pm_gview(S), gW = pm_gview(Wskel);
   const int last = S->rp->split[g_me + 1] == S->rp->n;
@@ -478,7 +495,6 @@ static void p_lmop(pmat *S, const pmat *Wskel, const pfactor *f, const double *u
   }
   amgd_free(kpos);
   pm_ext_free(&WtE);
-  pm_ext_free(&QE);
   amgd_free(qm.col);
   pk_mark(g_pklvl, PK_LMOP);
 }
@@ -803,6 +819,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
   uint64_t prev_nnz = (uint64_t)-1;
   pmat *prevWt = NULL;
   double *prevQ = NULL;
+  dcsr *prevQbuf = NULL;
   uint64_t *prevQoff = NULL;
   for (;;) {
     pfactor fac;
@@ -812,7 +829,10 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     fac.Q = amgd_qfactor_reuse(fac.Wt->m, AfE, &fac.qoff, &fac.qtot, prevWt ? prevWt->m : NULL, prevQ, prevQoff);
     dcsr_free(&AfE);
     pk_mark(g_pklvl, PK_QF);
-    if (prevWt) { pm_free(&prevWt); amgd_free(prevQ); amgd_free(prevQoff); prevQ = NULL; prevQoff = NULL; }
+    if (prevWt) {
+      pm_free(&prevWt); q_release(prevQ, &prevQbuf); amgd_free(prevQoff);
+      prevQ = NULL; prevQoff = NULL;
+    }
     const pmat *W0;
     pmat *Wtmp = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
     pk_mark(g_pklvl, PK_WEIGHTS);
@@ -870,8 +890,8 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     W_skel = nsk;
     pm_free(&Wtmp);
     pm_free(&R);
-    prevWt = fac.Wt; prevQ = fac.Q; prevQoff = fac.qoff;
-    fac.Wt = NULL; fac.Q = NULL; fac.qoff = NULL;
+    prevWt = fac.Wt; prevQ = fac.Q; prevQoff = fac.qoff; prevQbuf = fac.Qbuf;
+    fac.Wt = NULL; fac.Q = NULL; fac.qoff = NULL; fac.Qbuf = NULL;
     pfactor_free(&fac);
   }
   pm_free(&W_skel); pm_free(&Amt);
