@@ -53,10 +53,12 @@ def parse():
     p.add_argument("--budget-s", type=float, default=450.0,
                    help="wall-time budget of the whole run (s): warmup and timed steps stop early "
                         "when one more step would pass it; `steps`/`warmup` report what ran")
-    p.add_argument("--mode", choices=["part", "shard", "replicas"], default="part",
-                   help="N>1: one row-partitioned setup (each rank holds its row blocks of every "
-                        "matrix, halo exchange; strong scaling), the round-2 replicated-hierarchy "
-                        "sharding, or N independent replicas")
+    p.add_argument("--mode", choices=["part", "shard", "replicas"], default=None,
+                   help="N>1 (default part): one row-partitioned setup (each rank holds its row "
+                        "blocks of every matrix, halo exchange; strong scaling), the round-2 "
+                        "replicated-hierarchy sharding, or N independent replicas.  N=1: the "
+                        "one-GPU driver unless --mode part is given, which runs the partitioned "
+                        "driver on a one-rank RCCL communicator (its N=1 baseline)")
     p.add_argument("--transport", choices=["rccl", "host"], default="rccl",
                    help="shard mode data path: RCCL over xGMI, or host-staged gloo (rehearsal "
                         "of N ranks on fewer GPUs; ranks share devices round-robin)")
@@ -209,8 +211,8 @@ def main():
     from omp_amg_amd import problems, shard
 
     oa.lib().amgd_init(device)
-    sharded = world > 1 and args.mode in ("shard", "part")
-    part = world > 1 and args.mode == "part"
+    part = args.mode == "part" or (world > 1 and args.mode is None)
+    sharded = part or (world > 1 and args.mode == "shard")
     if sharded and args.transport == "host":
         shard.init_host(rank, world)
     elif sharded:
@@ -250,11 +252,18 @@ def main():
     t_step = 0.0
     warm = 0
     warm_deadline = time.time() + 0.25 * max(0.0, deadline - time.time())
+    # the warmup setups run with the collective-consistency guard on (every collective's
+    # kind, call site and sizes checked across the ranks first; a mismatch aborts with both
+    # sites instead of hanging RCCL); the timed ones without its extra record exchange
+    if world > 1:
+        oa.lib().amgd_comm_set_check(1)
     while warm < args.warmup and (warm == 0 or not agree(time.time() + t_step > warm_deadline)):
         t1 = time.perf_counter()
         ds.run(exact_dots=not args.fast_dots)
         t_step = time.perf_counter() - t1
         warm += 1
+    if world > 1:
+        oa.lib().amgd_comm_set_check(0)
     barrier()
     rap_ms, rap_bytes, rap_nnz, mv_ms, mv_bytes, mv_strict, st = 0.0, 0, 0, 0.0, 0, 0, None
     mv_n, rap_n = 0, 0

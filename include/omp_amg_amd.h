@@ -31,7 +31,7 @@ typedef struct {
   uint64_t rows0, nnz0;
   uint32_t nlevels, ub_events;   /* ub_events: inputs outside the reference's defined domain */
   size_t peak_bytes;
-  double spmv_kernel_ms;         /* whole-matrix long-row SpMV kernels (k_spmv_lane), event-timed */
+  double spmv_kernel_ms;         /* whole-matrix long-row SpMV kernels (k_spmv_pipe), event-timed */
   uint64_t spmv_bytes;           /* their bytes with x gathered once per entry */
   uint64_t spmv_bytes_strict;    /* their algorithmic HBM bytes: x read once per product */
   uint64_t spmv_launches, rap_launches;   /* kernel launches behind spmv_/rap_kernel_ms */
@@ -90,10 +90,20 @@ int amgd_comm_rank(void);
    only its row blocks: rows of A, Af, W and AfP of every level and of every intermediate;
    products fetch the halo rows they reference, transposes exchange row pieces, vectors
    stay whole.  amgd_hier_export gathers the whole hierarchy to every rank (bit-identical
-   to the one-GPU hierarchy); crs_setup with np > 1 passes the local entries through.
-   amgd_comm_set_partitioned(1) after amgd_comm_init_*; amgd_comm_free resets it. */
+   to the one-GPU hierarchy).  amgd_comm_set_partitioned(1) after amgd_comm_init_* turns
+   it on for amgd_setup_device; crs_setup with np > 1 runs partitioned unless
+   amgd_comm_set_partitioned(0) chose the round-2 replicated mode; amg_setup always takes
+   the whole matrix on the calling process (amg_setup.h:5) and runs the one-GPU setup
+   there.  amgd_comm_free resets the choice. */
 void amgd_comm_set_partitioned(int on);
 int amgd_comm_partitioned(void);
+/* Collective-consistency guard (also AMGD_COMM_CHECK=1): before every collective the
+   ranks exchange (sequence number, kind, call site, sizes) and abort naming both ranks'
+   call sites on a mismatch; an out-of-HBM on one rank inside a setup is announced the
+   same way and every rank's setup returns -2 (without the guard it aborts the job).
+   1 on, 0 off, -1 back to the environment.  amgd_comm_guard_calls: record exchanges so far. */
+void amgd_comm_set_check(int on);
+uint64_t amgd_comm_guard_calls(void);
 /* scale of the per-op minimum work below which an op runs unsharded (1 = default, 0 = always shard) */
 void amgd_comm_set_min_work(double scale);
 void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms);

@@ -365,7 +365,7 @@ def qf_stats() -> dict:
     return {"sparse": int(out[0]), "fallback": int(out[1]), "split": int(out[2])}
 
 
-ROUTES = ("spmv_lane", "mv_long", "sg_tiny", "sg_kseq", "sg_win", "sg_wsym", "sg_long",
+ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
           "qf_t512", "qf_t1024")
 

@@ -76,8 +76,8 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
 
 /* kernel-route counters (which default paths a setup took; read by the parity tests
    at sizes where the default routing engages) */
-enum { AMGD_R_SPMV_LANE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WIN,
-       AMGD_R_SG_WSYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
+enum { AMGD_R_SPMV_PIPE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WWIN,
+       AMGD_R_SG_WWIN_SYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
        AMGD_R_MV_RW4, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_MV_RW16, AMGD_R_MV_RW64,
        AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_N };
 extern uint64_t amgd_route_ctr[32];
@@ -89,6 +89,12 @@ uint32_t amgd_scan_u32(uint32_t *counts, uint64_t n);
 /* compaction map for a u8 mask: map[i] = rank of i among set entries (or ~0) */
 uint32_t amgd_mask_rank(const uint8_t *mask, uint32_t n, uint32_t *map);
 
+/* AMGD_PHASES=1 phase profile (amgd_setup.c): time of the phase just ended on a level */
+enum { PH_COARSEN, PH_SMOOTH, PH_IPRE, PH_QF, PH_W0, PH_SPAT, PH_LMOP, PH_PCG, PH_W, PH_AFW, PH_R,
+       PH_FS, PH_FS_MV, PH_FS_MAX, PH_FS_SEL, PH_EXP, PH_EXP_R0, PH_FINAL, PH_RAP, PH_N };
+void amgd_ph_mark(int lvl, int id);      /* -1: restart the clock */
+void amgd_ph_report(uint32_t nlevels);
+
 /* ---------------- row sharding over GPUs (amgd_comm.hip) ---------------- */
 int amgd_nshards(void);                          /* 1: sharding off */
 int amgd_comm_procs(void);                       /* processes of the communicator (sim: 1) */
@@ -96,21 +102,37 @@ void amgd_my_shards(int *first, int *last);      /* shard ranges this process co
 int amgd_shard_worth(uint64_t work, uint64_t min_work);
 /* contiguous ranges of equal work: split_h[0..N] from an exclusive prefix of n+1 entries */
 void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h);
+/* Collectives.  Each records its call site (file:line of the outermost caller) for the
+   collective-consistency guard (AMGD_COMM_CHECK=1 / amgd_comm_set_check): before every
+   collective the ranks exchange (sequence number, kind, call site, offsets signature,
+   send lengths) in a fixed-size record and abort naming both ranks' sites on any
+   mismatch -- a rank-local skip or a size disagreement cannot go unnoticed (RCCL would
+   hang or corrupt).  The same record carries an out-of-HBM on one rank to all of them,
+   so every rank unwinds its setup together (amgd_comm_fail_agree). */
+void amgd_comm_site(const char *file, int line);
+int amgd_comm_fail_agree(void);    /* 1: every rank was told of this rank's failure */
 /* range s of buffer b = bytes [off[b*(N+1)+s], off[b*(N+1)+s+1]), completed on every rank */
-void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off);
-void amgd_allgather_u64(uint64_t *vals_h);       /* vals_h[s] of the own shards -> all */
+void amgd_allgatherv_(int nbuf, void *const *bufs, const uint64_t *off);
+#define amgd_allgatherv(...) (amgd_comm_site(__FILE__, __LINE__), amgd_allgatherv_(__VA_ARGS__))
+void amgd_allgather_u64_(uint64_t *vals_h);      /* vals_h[s] of the own shards -> all */
+#define amgd_allgather_u64(...) (amgd_comm_site(__FILE__, __LINE__), amgd_allgather_u64_(__VA_ARGS__))
 void amgd_gather_u64_at(const uint64_t *a, const uint32_t *idx_h, int n, uint64_t *out_h);
 
 /* partitioned mode (amgd_psetup.c): ranks own row blocks; amgd_nshards() is 1 there */
 int amgd_comm_partitioned(void);
 void amgd_comm_suspend_partition(int on);
+int amgd_comm_part_default(void);
+int amgd_comm_part_get(void);          /* raw flag: -1 unset, 0 off, 1 on */
+void amgd_comm_part_set(int v);
 /* calls, bytes of: data allgatherv, alltoallv, small u64 allgathers (since the last reset) */
 void amgd_comm_stats_kind(uint64_t *out6);
 int amgd_pcomm_rank(void);
 int amgd_pcomm_size(void);
-void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m);   /* vals_h[N*m]: own m -> all */
+void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m);  /* vals_h[N*m]: own m -> all */
+#define amgd_pcomm_allgather_u64(...) (amgd_comm_site(__FILE__, __LINE__), amgd_pcomm_allgather_u64_(__VA_ARGS__))
 /* rank sends send[soff[p]..soff[p+1]) to p, receives p's into recv[roff[p]..roff[p+1]) (bytes) */
-void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff);
+void amgd_pcomm_alltoallv_(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff);
+#define amgd_pcomm_alltoallv(...) (amgd_comm_site(__FILE__, __LINE__), amgd_pcomm_alltoallv_(__VA_ARGS__))
 
 /* ---------------- reductions (return host values, sync) ---------------- */
 void amgd_set_exact(int on);     /* 1: reference-order (sequential) dots -- default; 0: tree */

@@ -42,8 +42,11 @@ enum { COMM_NONE = 0, COMM_RCCL = 1, COMM_HOST = 2, COMM_SIM = 3 };
 static int g_kind = COMM_NONE, g_rank = 0, g_size = 1;
 // partitioned mode (amgd_psetup.c): the ranks own row blocks of every matrix; the
 // replicated-hierarchy sharding of the kernels below is switched off (amgd_nshards() = 1)
-// and the partitioned ops exchange rows / vectors through amgd_pcomm_* directly
-static int g_part = 0, g_part_susp = 0;
+// and the partitioned ops exchange rows / vectors through amgd_pcomm_* directly.
+// g_part: -1 not chosen (crs_setup with np > 1 then runs partitioned), 0 off (the
+// round-2 replicated hierarchy), 1 on.  The sim transport is never partitioned.
+static int g_part = -1, g_part_susp = 0;
+static int part_on(void) { return g_part == 1 && g_kind != COMM_SIM; }
 static amgd_allgatherv_fn g_cb = nullptr;
 static void *g_user = nullptr;
 static double g_min_scale = 1.0;      // work thresholds x this (0: shard everything)
@@ -52,6 +55,7 @@ static uint64_t g_bytes = 0, g_calls = 0;
 // transposes, routed entries), [2] allgathers of a few u64 (counts, flags, maxima); calls, bytes
 static uint64_t g_kstat[3][2];
 static int g_kind_small = 0;
+static uint64_t g_seq = 0, g_guard_calls = 0;   // collective guard: records exchanged (below)
 static double g_ms = 0;
 
 // ---- RCCL entry points (dlopen'ed) ----
@@ -151,14 +155,19 @@ extern "C" API void amgd_comm_free(void) {
   g_kind = COMM_NONE;
   g_rank = 0;
   g_size = 1;
-  g_part = 0;
+  g_seq = 0;
+  g_part = -1;
   g_cb = nullptr;
   g_user = nullptr;
 }
 
 extern "C" API int amgd_comm_size(void) { return g_size; }
 extern "C" API void amgd_comm_set_partitioned(int on) { g_part = on ? 1 : 0; }
-extern "C" API int amgd_comm_partitioned(void) { return g_part && !g_part_susp && g_kind != COMM_SIM; }
+extern "C" API int amgd_comm_partitioned(void) { return part_on() && !g_part_susp; }
+// crs_setup's choice for np > 1: partitioned unless amgd_comm_set_partitioned(0) was called
+int amgd_comm_part_default(void) { return g_part != 0 && g_kind != COMM_SIM; }
+int amgd_comm_part_get(void) { return g_part; }
+void amgd_comm_part_set(int v) { g_part = v; }
 extern "C" API int amgd_comm_rank(void) { return g_rank; }
 extern "C" API void amgd_comm_set_min_work(double scale) { g_min_scale = scale < 0 ? 1.0 : scale; }
 extern "C" API void amgd_comm_stats(uint64_t *calls, uint64_t *bytes, double *ms) {
@@ -174,7 +183,7 @@ extern "C" API void amgd_comm_stats_reset(void) {
 void amgd_comm_stats_kind(uint64_t *out6) { memcpy(out6, g_kstat, sizeof g_kstat); }
 
 // ---- internal API (amgd.h) ----
-int amgd_nshards(void) { return g_kind == COMM_NONE || g_part ? 1 : g_size; }
+int amgd_nshards(void) { return g_kind == COMM_NONE || part_on() ? 1 : g_size; }
 // a partitioned setup running one operation on gathered (whole) data on every rank:
 // the kernels see neither partitioning nor sharding meanwhile
 void amgd_comm_suspend_partition(int on) { g_part_susp = on ? 1 : 0; }
@@ -193,11 +202,154 @@ int amgd_shard_worth(uint64_t work, uint64_t min_work) {
   return (double)work >= (double)min_work * env * g_min_scale;
 }
 
+
+// ---------------------------------------------------------------------------
+// Collective-consistency guard (AMGD_COMM_CHECK=1, amgd_comm_set_check).  Every rank must
+// enter the same collectives in the same order with matching sizes; a rank-local branch
+// that skips one (round 4's r04e fault) leaves gloo failing on a size check and RCCL
+// hanging or corrupting memory.  With the guard on, every collective first exchanges one
+// fixed-size record per rank over the raw transport:
+//   [seq, kind, call-site line, call-site file hash, offsets signature, send lengths[N],
+//    receive lengths[N]]
+// and every rank checks all records: same seq / kind / site / signature everywhere, and
+// for an alltoallv the bytes any rank q sends any rank p equal the bytes p expects from
+// q.  Every rank sees every record, so all of them abort together, naming the sites.  A record of kind FAIL is a rank that ran out
+// of HBM inside its setup: every rank then unwinds (amgd_oom_error) and returns the same
+// error, instead of the failing rank aborting the job.
+// ---------------------------------------------------------------------------
+enum { GK_AGV = 1, GK_A2A = 2, GK_FAIL = 3 };
+static int g_check = -1;
+static const char *g_site_f = nullptr;
+static int g_site_l = 0, g_depth = 0;
+static uint64_t *g_grec_d = nullptr;          // device records: N x (5 + N) u64 (outside the arena)
+static int g_grec_n = 0;
+extern "C" void amgd_comm_site(const char *f, int l) {
+  if (!g_depth) { g_site_f = f; g_site_l = l; }
+}
+struct SiteScope {          // the outermost collective owns the recorded site
+  SiteScope() { g_depth++; }
+  ~SiteScope() { if (--g_depth == 0) { g_site_f = nullptr; g_site_l = 0; } }
+};
+extern "C" API void amgd_comm_set_check(int on) { g_check = on < 0 ? -1 : on ? 1 : 0; }
+static int check_on(void) {
+  if (g_check < 0) {
+    const char *e = getenv("AMGD_COMM_CHECK");
+    g_check = e && *e && atoi(e) ? 1 : 0;
+  }
+  return g_check;
+}
+extern "C" API uint64_t amgd_comm_guard_calls(void) { return g_guard_calls; }
+static uint64_t fnv(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
+  const unsigned char *c = (const unsigned char *)p;
+  for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+  return h;
+}
+static const char *gk_name(uint64_t k) {
+  return k == GK_AGV ? "allgatherv" : k == GK_A2A ? "alltoallv" : k == GK_FAIL ? "FAIL" : "?";
+}
+// every rank's record to every rank (fixed size: cannot itself mismatch); out: N x RL
+static void guard_exchange(const uint64_t *mine, int RL, std::vector<uint64_t> &all) {
+  const int N = g_size;
+  all.assign((size_t)N * RL, 0);
+  if (!g_grec_d || g_grec_n < N * RL) {
+    if (g_grec_d) (void)hipFree(g_grec_d);
+    HIPCK(hipMalloc(&g_grec_d, 8ull * N * RL));
+    g_grec_n = N * RL;
+  }
+  HIPCK(hipMemcpyAsync(g_grec_d + (size_t)g_rank * RL, mine, 8ull * RL, hipMemcpyHostToDevice, amgd_s()));
+  if (g_kind == COMM_HOST) {
+    amgd_sync();
+    std::vector<uint64_t> off(N + 1);
+    for (int q = 0; q <= N; q++) off[q] = 8ull * q * RL;
+    void *b = g_grec_d;
+    if (g_cb(g_user, 1, &b, off.data(), g_rank, N) != 0) {
+      fprintf(stderr, "omp_amg_amd: host transport failed in the collective guard\n");
+      abort();
+    }
+  } else {
+    hipStream_t st = amgd_s();
+    NCCK(R.GroupStart());
+    for (int p = 0; p < N; p++) {
+      if (p == g_rank) continue;
+      NCCK(R.Send(g_grec_d + (size_t)g_rank * RL, 8ull * RL, ncclChar, p, g_nc, st));
+      NCCK(R.Recv(g_grec_d + (size_t)p * RL, 8ull * RL, ncclChar, p, g_nc, st));
+    }
+    NCCK(R.GroupEnd());
+  }
+  HIPCK(hipMemcpyAsync(all.data(), g_grec_d, 8ull * N * RL, hipMemcpyDeviceToHost, amgd_s()));
+  amgd_sync();
+  g_guard_calls++;
+}
+extern "C" void amgd_throw_oom(void);   // amgd_rt.hip: unwind the setup (inside amgd_try), abort elsewhere
+// kind, offsets signature; A2A: send[p] / recv[p] byte counts
+static void guard(int kind, uint64_t sig, const uint64_t *sendl, const uint64_t *recvl) {
+  const int N = g_size;
+  if (!check_on() || N == 1 || (g_kind != COMM_RCCL && g_kind != COMM_HOST)) return;
+  const int RL = 5 + 2 * N;
+  std::vector<uint64_t> mine(RL, 0), all;
+  mine[0] = g_seq++;
+  mine[1] = (uint64_t)kind;
+  mine[2] = (uint64_t)g_site_l;
+  mine[3] = g_site_f ? fnv(g_site_f, strlen(g_site_f)) : 0;
+  mine[4] = sig;
+  if (sendl) for (int p = 0; p < N; p++) { mine[5 + p] = sendl[p]; mine[5 + N + p] = recvl[p]; }
+  guard_exchange(mine.data(), RL, all);
+  for (int q = 0; q < N; q++) {
+    const uint64_t *r = all.data() + (size_t)q * RL;
+    if (r[1] == GK_FAIL) {
+      char msg[256];
+      snprintf(msg, sizeof msg, "rank %d failed (out of HBM) at collective %lu; rank %d unwinds with it", q,
+               (unsigned long)r[0], g_rank);
+      amgd_set_error(msg);
+      fprintf(stderr, "omp_amg_amd: %s\n", msg);
+      if (kind != GK_FAIL) amgd_throw_oom();
+      return;
+    }
+  }
+  for (int q = 0; q < N; q++) {
+    const uint64_t *r = all.data() + (size_t)q * RL;
+    bool bad = r[0] != mine[0] || r[1] != mine[1] || r[2] != mine[2] || r[3] != mine[3] ||
+               (kind == GK_AGV && r[4] != mine[4]);
+    uint64_t got = 0, want = 0;
+    int to = -1;
+    for (int p = 0; p < N && !bad && kind == GK_A2A; p++) {   // q -> p: sent == expected
+      const uint64_t *rp = all.data() + (size_t)p * RL;
+      if (p != q && r[5 + p] != rp[5 + N + q]) {
+        bad = true;
+        got = r[5 + p];
+        want = rp[5 + N + q];
+        to = p;
+      }
+    }
+    if (bad) {
+      fprintf(stderr,
+              "omp_amg_amd: COLLECTIVE MISMATCH: rank %d at %s:%d (seq %lu, %s) vs rank %d at line %lu "
+              "(seq %lu, %s)%s",
+              g_rank, g_site_f ? g_site_f : "?", g_site_l, (unsigned long)mine[0], gk_name(mine[1]), q,
+              (unsigned long)r[2], (unsigned long)r[0], gk_name(r[1]),
+              r[3] != mine[3] ? ", other file" : r[4] != mine[4] && kind == GK_AGV ? ", offsets differ" : "");
+      if (to >= 0) fprintf(stderr, ": rank %d sends %lu bytes to rank %d, which expects %lu", q,
+                           (unsigned long)got, to, (unsigned long)want);
+      fprintf(stderr, "\n");
+      abort();
+    }
+  }
+}
+// out of HBM on this rank inside a setup: with the guard on, tell every rank (they are
+// in, or will enter, their next collective's record exchange) and unwind together
+extern "C" int amgd_comm_fail_agree(void) {
+  if (g_size <= 1 || (g_kind != COMM_RCCL && g_kind != COMM_HOST) || !check_on()) return 0;
+  guard(GK_FAIL, 0, nullptr, nullptr);
+  return 1;
+}
+
 // Range s of the shards holds bytes [off[b*(N+1)+s], off[b*(N+1)+s+1]) of buffer b;
 // every rank holds its own ranges, after the call every rank holds all of them.
-void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off) {
+void amgd_allgatherv_(int nbuf, void *const *bufs, const uint64_t *off) {
+  SiteScope site_;
   const int N = g_size;
   if (g_kind == COMM_NONE || g_kind == COMM_SIM || N == 1) return;
+  guard(GK_AGV, fnv(off, 8ull * nbuf * (N + 1), (uint64_t)nbuf), nullptr, nullptr);
   double t0 = amgd_wtime();
   uint64_t nb = 0;
   for (int b = 0; b < nbuf; b++) nb += off[b * (N + 1) + N] - off[b * (N + 1)];
@@ -226,7 +378,8 @@ void amgd_allgatherv(int nbuf, void *const *bufs, const uint64_t *off) {
       }
     }
     NCCK(R.GroupEnd());
-    amgd_sync();
+    // no host sync: the send/recv pairs run on the library stream, so every consumer
+    // (kernels, copies, frees of the arena) is ordered after them already
   }
   g_ms += (amgd_wtime() - t0) * 1e3;
 }
@@ -258,9 +411,9 @@ void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h) {
 }
 
 // per-shard u64 values gathered to every rank (in-place on a device buffer)
-void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m);
-void amgd_allgather_u64(uint64_t *vals_h) {
-  if (g_part) {                                  // partitioned mode: one value per process
+void amgd_allgather_u64_(uint64_t *vals_h) {
+  SiteScope site_;
+  if (part_on()) {                               // partitioned mode: one value per process
     amgd_pcomm_allgather_u64(vals_h, 1);
     return;
   }
@@ -302,7 +455,8 @@ int amgd_pcomm_rank(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? 
 int amgd_pcomm_size(void) { return g_kind == COMM_RCCL || g_kind == COMM_HOST ? g_size : 1; }
 
 // vals_h[N * rank .. N * rank + m) of this rank -> every rank (m u64 per rank)
-void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m) {
+void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m) {
+  SiteScope site_;
   const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
   if (N == 1) return;
   uint64_t *d = (uint64_t *)amgd_alloc(8ull * N * m + 8);
@@ -322,8 +476,14 @@ void amgd_pcomm_allgather_u64(uint64_t *vals_h, int m) {
 // both sides must agree: callers exchange counts first).  RCCL: one group of send/recv
 // pairs with every peer (each xGMI link carries its own pair).  Host transport: staged
 // through the allgatherv callback (every rank sees every send buffer; tests only).
-void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+void amgd_pcomm_alltoallv_(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+  SiteScope site_;
   const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  if (N > 1 && check_on()) {
+    std::vector<uint64_t> sl(N), rl(N);
+    for (int p = 0; p < N; p++) { sl[p] = soff[p + 1] - soff[p]; rl[p] = roff[p + 1] - roff[p]; }
+    guard(GK_A2A, 0, sl.data(), rl.data());
+  }
   const uint64_t own = soff[me + 1] - soff[me];
   if (own) HIPCK(hipMemcpyAsync((char *)recv + roff[me], (const char *)send + soff[me], own,
                                 hipMemcpyDeviceToDevice, amgd_s()));
@@ -342,8 +502,7 @@ void amgd_pcomm_alltoallv(const void *send, const uint64_t *soff, void *recv, co
       if (rl) NCCK(R.Recv((char *)recv + roff[p], rl, ncclChar, p, g_nc, s));
       g_bytes += rl;
     }
-    NCCK(R.GroupEnd());
-    amgd_sync();
+    NCCK(R.GroupEnd());          // stream-ordered like amgd_allgatherv: no host sync
   } else {
     // host transport (tests, several ranks on one GPU): N-1 rounds; in round k every rank
     // contributes its piece for rank (r + k) mod N to one allgatherv and takes the piece

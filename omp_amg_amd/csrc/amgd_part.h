@@ -91,6 +91,7 @@ pmat *pm_spgemm(const pmat *A, const pmat *B, int pattern);
    Free with pm_ext_free. */
 dcsr *pm_halo_rows(const pmat *B, const dcsr *L);
 void pm_ext_free(dcsr **E);
+int pm_ext_is_view(const dcsr *E);   /* 1: one rank, E aliases B's arrays (no copy) */
 
 /* this rank's COO entries (global indices) to the owners of their rows (P); returns the
    count received, the arrays in source-rank order (free with amgd_free) */

@@ -265,18 +265,22 @@ __global__ void k_sum_lens(const uint32_t *lens, int N, uint32_t n, uint64_t *cn
   }
 }
 // piece of source s: rows j with lens_s[j] entries at src (consecutive rows), placed after
-// the pieces of the earlier sources (cur[j] = entries already placed in row j)
+// the pieces of the earlier sources (cur[j] = entries already placed in row j); one
+// wavefront per row, lanes copying consecutive entries (coalesced for long rows)
 __global__ void k_place_piece(const uint32_t *lens, const uint64_t *soff, uint32_t n, const uint32_t *scol,
                               const double *sa, uint32_t cadd, const uint64_t *ro, uint32_t *cur,
                               uint32_t *col, double *a) {
-  GRID_STRIDE(j, n) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t j = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; j < n;
+       j += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
     const uint32_t l = lens[j];
     if (!l) continue;
     const uint64_t s0 = soff[j], d0 = ro[j] + cur[j];
-    for (uint32_t t = 0; t < l; t++) { col[d0 + t] = scol[s0 + t] + cadd; a[d0 + t] = sa[s0 + t]; }
-    cur[j] += l;
+    for (uint32_t t = lane; t < l; t += 64) { col[d0 + t] = scol[s0 + t] + cadd; a[d0 + t] = sa[s0 + t]; }
+    if (lane == 0) cur[j] += l;
   }
 }
+static inline int wave_rows_grid(uint64_t n) { return grid_for(n * 64, 256, 65536); }
 static void gather_at(const uint64_t *d, const uint32_t *idx, int n, uint64_t *out) {
   amgd_gather_u64_at(d, idx, n, out);
 }
@@ -285,6 +289,10 @@ extern "C" pmat *pm_transpose(const pmat *A) {
   const int N = RP->N, me = amgd_pcomm_rank();
   hipStream_t s = amgd_s();
   dcsr *T = amgd_transpose(A->m, nullptr);                // rows: all columns of A
+  if (N == 1) {                     // one rank: the local transpose is the whole one
+    T->cn = RP->n;
+    return pm_new(T, CP, RP);
+  }
   const uint32_t nc = CP->n, c0 = CP->split[me], c1 = CP->split[me + 1], nl = c1 - c0;
   // entry ranges of the pieces
   std::vector<uint64_t> tro(N + 1);
@@ -334,7 +342,7 @@ extern "C" pmat *pm_transpose(const pmat *A) {
     // offsets of source q's rows inside its piece
     k_len_to_u64<<<grid_for(nl), 256, 0, s>>>(rlens + (size_t)q * nl, nl, soff);
     amgd_scan_u64(soff, nl);
-    k_place_piece<<<grid_for(nl), 256, 0, s>>>(rlens + (size_t)q * nl, soff, nl, rcol + rpre[q], ra + rpre[q],
+    k_place_piece<<<wave_rows_grid(nl), 256, 0, s>>>(rlens + (size_t)q * nl, soff, nl, rcol + rpre[q], ra + rpre[q],
                                                RP->split[q], X->ro, cur, X->col, X->a);
     KCHECK();
   }
@@ -377,11 +385,13 @@ __global__ void k_req_lens(const uint32_t *req, uint64_t n, uint32_t r0, const u
 }
 __global__ void k_req_copy(const uint32_t *req, uint64_t n, uint32_t r0, const uint64_t *ro,
                            const uint32_t *col, const double *a, const uint64_t *off, uint32_t *ocol, double *oa) {
-  GRID_STRIDE(t, n) {
+  const int lane = threadIdx.x & 63;       // one wavefront per requested row
+  for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < n;
+       t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
     const uint32_t i = req[t] - r0;
     const uint64_t k0 = ro[i], l = ro[i + 1] - k0, o = off[t];
-    if (col) for (uint64_t q = 0; q < l; q++) ocol[o + q] = col[k0 + q];
-    for (uint64_t q = 0; q < l; q++) oa[o + q] = a[k0 + q];
+    if (col) for (uint64_t q = lane; q < l; q += 64) ocol[o + q] = col[k0 + q];
+    for (uint64_t q = lane; q < l; q += 64) oa[o + q] = a[k0 + q];
   }
 }
 // requester side: row lengths of the extended matrix
@@ -391,19 +401,22 @@ __global__ void k_ext_lens_own(const uint64_t *ro, uint32_t r0, uint32_t nl, uin
 __global__ void k_ext_lens_halo(const uint32_t *need, const uint32_t *hlen, uint64_t n, uint64_t *len) {
   GRID_STRIDE(t, n) len[need[t]] = hlen[t];
 }
-__global__ void k_ext_copy_own(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t r0,
-                               uint32_t nl, const uint64_t *ero, uint32_t *ecol, double *ea) {
-  GRID_STRIDE(i, nl) {
-    const uint64_t k0 = ro[i], l = ro[i + 1] - k0, o = ero[r0 + i];
-    if (col) for (uint64_t q = 0; q < l; q++) ecol[o + q] = col[k0 + q];
-    for (uint64_t q = 0; q < l; q++) ea[o + q] = a[k0 + q];
-  }
-}
+// Halo views that are B itself (one rank: no row is another rank's) alias B's arrays;
+// pm_ext_free releases only their header.
+#include <unordered_set>
+static std::unordered_set<const dcsr *> g_views;
+extern "C" int pm_ext_is_view(const dcsr *E) { return g_views.count(E) ? 1 : 0; }
 extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   const apart *P = B->rp;
   const int N = P->N, me = amgd_pcomm_rank();
   const uint32_t n = P->n, r0 = P->split[me], r1 = P->split[me + 1], nl = r1 - r0;
   hipStream_t s = amgd_s();
+  if (N == 1) {
+    dcsr *E = (dcsr *)malloc(sizeof(dcsr));
+    *E = *B->m;
+    g_views.insert(E);
+    return E;
+  }
   // 1. the rows L references outside the own range, ascending
   uint8_t *mark = (uint8_t *)amgd_alloc((size_t)n + 8);
   uint32_t *rank = (uint32_t *)amgd_alloc(4ull * n + 8);
@@ -464,7 +477,7 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   const bool cols = Bm->col != nullptr;     // NULL: a values-only pseudo-matrix (Q factors)
   uint32_t *scol = cols ? (uint32_t *)amgd_alloc(4 * nsend + 8) : nullptr;
   double *sa = (double *)amgd_alloc(8 * nsend + 8);
-  if (nreq) k_req_copy<<<grid_for(nreq), 256, 0, s>>>(req, nreq, r0, Bm->ro, Bm->col, Bm->a, roff, scol, sa);
+  if (nreq) k_req_copy<<<wave_rows_grid(nreq), 256, 0, s>>>(req, nreq, r0, Bm->ro, Bm->col, Bm->a, roff, scol, sa);
   KCHECK();
   // 5. the extended matrix: row offsets first, then the halo rows received straight into
   //    it -- the rows of the ranks below come before the own rows, those above after them,
@@ -491,12 +504,25 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   if (cols) amgd_pcomm_alltoallv(scol, s4.data(), E->col, r4.data());
   amgd_pcomm_alltoallv(sa, s8.data(), E->a, r8.data());
   amgd_free(req); amgd_free(rlen); amgd_free(roff); amgd_free(scol); amgd_free(sa);
-  if (nl) k_ext_copy_own<<<grid_for(nl), 256, 0, s>>>(Bm->ro, Bm->col, Bm->a, r0, nl, E->ro, E->col, E->a);
-  KCHECK();
+  // the own rows: one contiguous block of B's arrays into one contiguous block of E's
+  if (ownnz) {
+    uint64_t at = 0;
+    amgd_d2h(&at, E->ro + r0, 8);
+    if (cols) HIPCK(hipMemcpyAsync(E->col + at, Bm->col, 4 * ownnz, hipMemcpyDeviceToDevice, s));
+    HIPCK(hipMemcpyAsync(E->a + at, Bm->a, 8 * ownnz, hipMemcpyDeviceToDevice, s));
+  }
   amgd_free(need); amgd_free(hlen); amgd_free(hoff);
   return E;
 }
-extern "C" void pm_ext_free(dcsr **E) { dcsr_free(E); }
+extern "C" void pm_ext_free(dcsr **E) {
+  if (!E || !*E) return;
+  if (g_views.erase(*E)) {
+    free(*E);
+    *E = nullptr;
+    return;
+  }
+  dcsr_free(E);
+}
 
 extern "C" pmat *pm_spgemm(const pmat *A, const pmat *B, int pattern) {
   dcsr *E = pm_halo_rows(B, A->m);

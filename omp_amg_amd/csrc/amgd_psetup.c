@@ -51,6 +51,7 @@ static void ub_note(int site) {      /* site codes: amgd_setup.c ub_note */
   g_ub++;
 }
 #define UB(site) ub_note(site)
+static void ph(int id) { amgd_ph_mark(g_plvl, id); }     /* AMGD_PHASES=1 time table */
 static int g_verbose = -1;
 static int verbose(void) {
   if (g_verbose < 0) { const char *e = getenv("AMGD_VERBOSE"); g_verbose = e && *e && *e != '0'; }
@@ -450,7 +451,8 @@ static void p_lmop(pmat *S, const pmat *Wskel, pfactor *f, const double *u) {
     amgd_lmop_set_prefix(D);
   }
   dcsr *QE = pm_halo_rows(&qp, Wskel->m);
-  {
+  const int qview = pm_ext_is_view(QE);      /* one rank: QE is the factor's own buffer */
+  if (!qview) {
     /* the own Q factors now sit in the view too (a contiguous copy at the own rows):
        the factor keeps that copy and its own buffer goes, instead of two copies of the
        own share through interp_lmop's peak */
@@ -495,6 +497,7 @@ static void p_lmop(pmat *S, const pmat *Wskel, pfactor *f, const double *u) {
   }
   amgd_free(kpos);
   pm_ext_free(&WtE);
+  if (qview) pm_ext_free(&QE);
   amgd_free(qm.col);
   pk_mark(g_pklvl, PK_LMOP);
 }
@@ -509,7 +512,9 @@ static void p_solve_constraint(double *lam, const pmat *W_skel, pfactor *fac, co
     pmat *Wn = pm_drop_zeros(W_skel), *Wnt = pm_drop_zeros(fac->Wt);
     fac->S = pm_spgemm(Wn, Wnt, 1);
     pm_free(&Wn); pm_free(&Wnt);
+    ph(PH_SPAT);
     p_lmop(fac->S, W_skel, fac, au2);
+    ph(PH_LMOP);
   }
   pmat *S = fac->S;
   double *resid = dalloc(nf), *d = dalloc(nf);
@@ -547,6 +552,7 @@ static void p_solve_constraint(double *lam, const pmat *W_skel, pfactor *fac, co
     amgd_vop(lam, lam, xx, nf, AMGD_V_ADD);
   }
   amgd_free(au2); amgd_free(resid); amgd_free(d); amgd_free(dl); amgd_free(q); amgd_free(xx);
+  ph(PH_PCG);
 }
 
 /* solve_weights (amg_setup.c:1437) */
@@ -564,6 +570,7 @@ static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, p
   if (!fac->W0) {
     fac->W0t = p_qapply(fac, Amt, au, zeros);
     fac->W0 = pm_transpose(fac->W0t);
+    ph(PH_W0);
   }
   *W0 = fac->W0;
   p_solve_constraint(lam, W_skel, fac, *W0, alpha, u, v, tol);
@@ -571,6 +578,7 @@ static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, p
   pmat *W = pm_transpose(Wt);
   pm_free(&Wt);
   amgd_free(au); amgd_free(zeros);
+  ph(PH_W);
   return W;
 }
 
@@ -672,6 +680,7 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
   }
   uint64_t prev_off = 0;
   uint32_t prev_nsel = 0;
+  ph(PH_FS);
   for (;;) {
     it++;
     int done = 0;
@@ -705,8 +714,10 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
       pm_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       pm_spmvt(Rt, tmp, w2);
     }
+    ph(PH_FS_MV);
     amgd_vdiv_guard(vv, w2, w, nc);
     double mv = amgd_max_first(vv, nc, NULL), mw = mv;
+    ph(PH_FS_MAX);
     if (mv < goal || mw < goal) break;
     while (mw <= (1 + theta) * goal && theta > 0) theta = theta / 2.;
     if (theta == 0) { UB(1); break; }
@@ -720,6 +731,7 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
       si = a; sj = b; room = r2;
     }
     const uint32_t nsel = p_fs_select(Rl, Rt, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    ph(PH_FS_SEL);
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
@@ -757,6 +769,7 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
                               const pfs_first *f1) {
   const uint32_t nf = W_skel->rp->n, r0 = W_skel->rp->split[g_me];
   pmat *M = p_find_support(R, Rt, gamma, f1);
+  ph(PH_FS);
   pmat *ns = pm_mpm(1., M, 1., W_skel);
   pm_free(&M);
   uint32_t nb_local = 0;
@@ -765,6 +778,7 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
   if (nbad == 0) {
     amgd_skel_binarize(ns->m, 0);
     amgd_free(badl);
+    ph(PH_EXP);
     return ns;
   }
   uint8_t *bad = (uint8_t *)amgd_alloc(nf + 8);
@@ -773,7 +787,9 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
   amgd_free(badl);
   pm_allgather_vec(bad, 1, W_skel->rp);
   if (verbose()) printf("    expand_support: %lu bad rows of %u\n", (unsigned long)nbad, nf);
+  ph(PH_EXP);
   pmat *R0 = p_r0_rows(r0c, bad);
+  ph(PH_EXP_R0);
   pmat *R0W = pm_mxmpoint(R0, W_skel);
   pmat *Xf = pm_mpm(1., R0, -1., R0W);
   pm_free(&R0W); pm_free(&R0);
@@ -785,6 +801,7 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
   amgd_skel_binarize(out->m, 1);
   pm_free(&N); pm_free(&ns); pm_free(&Xf);
   amgd_free(ones); amgd_free(pi); amgd_free(pj); amgd_free(bad);
+  ph(PH_EXP);
   return out;
 }
 
@@ -821,14 +838,16 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
   double *prevQ = NULL;
   dcsr *prevQbuf = NULL;
   uint64_t *prevQoff = NULL;
+  ph(PH_IPRE);
   for (;;) {
     pfactor fac;
     memset(&fac, 0, sizeof fac);
     fac.Wt = pm_transpose(W_skel);
     dcsr *AfE = pm_halo_rows(Af, fac.Wt->m);             /* the Af rows of the supports */
     fac.Q = amgd_qfactor_reuse(fac.Wt->m, AfE, &fac.qoff, &fac.qtot, prevWt ? prevWt->m : NULL, prevQ, prevQoff);
-    dcsr_free(&AfE);
+    pm_ext_free(&AfE);
     pk_mark(g_pklvl, PK_QF);
+    ph(PH_QF);
     if (prevWt) {
       pm_free(&prevWt); q_release(prevQ, &prevQbuf); amgd_free(prevQoff);
       prevQ = NULL; prevQoff = NULL;
@@ -839,6 +858,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     pmat *AfW = pm_spgemm(Af, Wtmp, 0);
     pmat *Arhat = pm_mpm(1., AfW, 1., Ar);
     pm_free(&AfW);
+    ph(PH_AFW);
     pmat *Arr = pm_mpm(1.0, Arhat, 1.0, Ar);
     pmat *ArW = pm_mxmpoint(Wtmp, Arr);
     pm_free(&Arr);
@@ -860,6 +880,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     uint64_t n = amgd_count_gt(r, cnc, gamma2, &maxr);
     double w1m = amgd_max_first(w1, cnc, NULL);
     pk_mark(g_pklvl, PK_AFW_R);
+    ph(PH_R);
     const uint64_t wsk = gnnz(W_skel);
     if (verbose())
       printf("   %lu nzs, %lu cols > %g, worst = %g\n", (unsigned long)wsk, (unsigned long)n, sqrt(gamma2),
@@ -879,6 +900,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
       pm_free(&Wtmp);
       pm_free(&R);
       pfactor_free(&fac);
+      ph(PH_FINAL);
       break;
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
@@ -995,9 +1017,11 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
       break;
     }
     uint8_t *vc = (uint8_t *)amgd_alloc(n + 1), *vf = (uint8_t *)amgd_alloc(n + 1);
+    ph(-1);
     p_coarsen(A, vc, ctol);
     amgd_u8_not(vc, vf, n);
     L->vc = vc;
+    ph(PH_COARSEN);
     add_time(&st->t_coarsen_ms, &t0);
     pk_mark(level, PK_COARSEN);
     apart *Pf = apart_induced(Pn, vf), *Pc = apart_induced(Pn, vc);
@@ -1030,6 +1054,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     }
     L->D = D;
     L->Af = Af;
+    ph(PH_SMOOTH);
     add_time(&st->t_smoother_ms, &t0);
     pk_mark(level, PK_SMOOTH);
     pmat *Afc = pm_sub_mat(A, vf, vc, Pf, Pc), *Ac = pm_sub_mat(A, vc, vc, Pc, Pc);
@@ -1059,6 +1084,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     pm_free(&Wt); pm_free(&WtAfP); pm_free(&Acf); pm_free(&AcfW); pm_free(&Atmp);
     pm_free(&Afc); pm_free(&Ac);
     amgd_free(vf);
+    ph(PH_RAP);
     add_time(&st->t_rap_ms, &t0);
     pk_mark(level, PK_RAP);
     Pn = Pc;
@@ -1068,6 +1094,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
   amgd_sync();
   st->t_total_ms = (amgd_wtime() - t_start) * 1e3;
   pk_report(h->nlevels);
+  if (g_me == 0) amgd_ph_report(h->nlevels);
   st->ub_events = (uint32_t)g_ub;
   st->nlevels = h->nlevels;
   if (verbose() && g_lmop_full)
@@ -1151,6 +1178,29 @@ __attribute__((visibility("hidden"))) void amgd_phier_free(amgd_phier **hp) {
     apart_free(&L->Pf);
   }
   if (h->id) amgd_free(h->id);
+  free(h->lv);
+  free(h);
+  *hp = NULL;
+}
+/* after an unwound (out-of-HBM) setup: the host side of a partial hierarchy -- pmat and
+   dcsr headers, partitions, the level array.  Its device blocks were released by the
+   unwind already (amgd_try), so nothing here touches the device pool. */
+static void pm_free_host(pmat **A) {
+  if (!A || !*A) return;
+  free((*A)->m);
+  free(*A);
+  *A = NULL;
+}
+__attribute__((visibility("hidden"))) void amgd_phier_free_host(amgd_phier **hp) {
+  amgd_phier *h = *hp;
+  if (!h) return;
+  for (uint32_t l = 0; h->lv && l < h->cap; l++) {
+    plevel *L = &h->lv[l];
+    if (!L->A && !L->Pn) continue;
+    pm_free_host(&L->A); pm_free_host(&L->Af); pm_free_host(&L->W); pm_free_host(&L->AfP);
+    apart_free(&L->Pn);
+    apart_free(&L->Pf);
+  }
   free(h->lv);
   free(h);
   *hp = NULL;

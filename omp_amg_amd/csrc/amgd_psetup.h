@@ -18,5 +18,6 @@ int amgd_psetup_body(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj, cons
 /* the whole hierarchy (gathered) on every rank */
 int amgd_phier_export(const amgd_phier *h, struct amg_setup_data *data);
 void amgd_phier_free(amgd_phier **h);
+void amgd_phier_free_host(amgd_phier **h);   /* after an unwind: host structs only */
 void amgd_phier_info(const amgd_phier *h, uint32_t *nlevels, uint32_t *r0, uint32_t *r1);
 #endif

@@ -159,7 +159,14 @@ static void oom(size_t sz) {
   fprintf(stderr, "omp_amg_amd: %s\n", g_err);
   // One rank unwinding alone would leave its peers blocked in the next collective:
   // with a multi-process communicator out of HBM stays fatal.
-  if (g_try_depth > 0 && amgd_comm_procs() <= 1) throw amgd_oom_error();
+  // With the collective guard on (AMGD_COMM_CHECK) the failure is first announced to the
+  // peers through it, and every rank unwinds together.
+  if (g_try_depth > 0 && (amgd_comm_procs() <= 1 || amgd_comm_fail_agree())) throw amgd_oom_error();
+  abort();
+}
+// a peer announced its failure through the collective guard: unwind this rank as well
+extern "C" void amgd_throw_oom(void) {
+  if (g_try_depth > 0) throw amgd_oom_error();
   abort();
 }
 extern "C" int amgd_try(int (*fn)(void *), void *arg) {

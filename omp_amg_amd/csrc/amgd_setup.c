@@ -74,9 +74,8 @@ static void dump_csr(const char *name, const dcsr *A) {
 }
 
 /* phase profile (AMGD_PHASES=1): device-synchronised time per (level, phase),
-   printed at the end of the setup; costs one stream sync per mark */
-enum { PH_COARSEN, PH_SMOOTH, PH_IPRE, PH_QF, PH_W0, PH_SPAT, PH_LMOP, PH_PCG, PH_W, PH_AFW, PH_R,
-       PH_FS, PH_FS_MV, PH_FS_MAX, PH_FS_SEL, PH_EXP, PH_EXP_R0, PH_FINAL, PH_RAP, PH_N };
+   printed at the end of the setup; costs one stream sync per mark.  Shared with the
+   partitioned driver (amgd_psetup.c) through amgd_ph_mark / amgd_ph_report (amgd.h). */
 static const char *ph_name[PH_N] = {"coarsen", "smoother", "interp0", "qfactor", "W0", "S_pat",
                                     "lmop", "pcg", "W", "AfW", "R", "fs_setup", "fs_spmv",
                                     "fs_max", "fs_sel", "expand", "exp_R0", "final", "rap"};
@@ -88,18 +87,19 @@ static int phases_on(void) {
   if (g_phases < 0) { const char *e = getenv("AMGD_PHASES"); g_phases = e && *e && *e != '0'; }
   return g_phases;
 }
-static void ph(int id) {
+__attribute__((visibility("hidden"))) void amgd_ph_mark(int lvl, int id) {
   if (!phases_on()) return;
   amgd_sync();
   double t = amgd_wtime();
   const double pk = amgd_pool_ipeak_take() / 1e9;
-  if (id >= 0 && g_lvl < PH_MAXL) {
-    g_ph[g_lvl][id] += (t - g_ph_t) * 1e3;
-    if (pk > g_phpk[g_lvl][id]) g_phpk[g_lvl][id] = pk;
+  if (id >= 0 && lvl >= 0 && lvl < PH_MAXL) {
+    g_ph[lvl][id] += (t - g_ph_t) * 1e3;
+    if (pk > g_phpk[lvl][id]) g_phpk[lvl][id] = pk;
   }
   g_ph_t = t;
 }
-static void ph_report(uint32_t nl) {
+static void ph(int id) { amgd_ph_mark(g_lvl, id); }
+__attribute__((visibility("hidden"))) void amgd_ph_report(uint32_t nl) {
   if (!phases_on()) return;
   double tot[PH_N] = {0};
   fprintf(stderr, "phase ms per level:\nlvl");
@@ -125,6 +125,8 @@ static void ph_report(uint32_t nl) {
   amgd_pool_stats(&nm, &gb, &ms, &nr);
   fprintf(stderr, "pool: %lu driver allocations, %.1f GB, %.1f ms in hipMalloc, %lu cache flushes\n",
           (unsigned long)nm, gb, ms, (unsigned long)nr);
+  memset(g_ph, 0, sizeof g_ph);
+  memset(g_phpk, 0, sizeof g_phpk);
 }
 
 /* X = A*B, given At = A' and Bt = B'.  When A has long columns (mean row of At
@@ -914,7 +916,12 @@ API int amgd_setup_device(uint64_t nz, const uint32_t *dAi, const uint32_t *dAj,
   setup_args a = {nz, dAi, dAj, dAv, NULL};
   int rc = amgd_try(amgd_comm_partitioned() ? psetup_try : setup_body, &a);
   if (rc != 0) {
-    if (a.h) { free(a.h->lv); free(a.h); }   /* device blocks: released by the unwind */
+    /* device blocks: released by the unwind; the host structs of a partial hierarchy here */
+    if (a.h) {
+      if (a.h->ph) amgd_phier_free_host(&a.h->ph);
+      free(a.h->lv);
+      free(a.h);
+    }
     return rc;
   }
   *out = a.h;
@@ -1042,8 +1049,7 @@ static int setup_body(void *arg) {
     level++;
   }
   h->nlevels = level + 1;
-  ph_report(h->nlevels);
-  if (phases_on()) { memset(g_ph, 0, sizeof g_ph); memset(g_phpk, 0, sizeof g_phpk); }
+  amgd_ph_report(h->nlevels);
   amgd_sync();
   g_st.t_total_ms = (amgd_wtime() - t_start) * 1e3;
   g_st.rap_kernel_ms = amgd_timer_ms(0);
@@ -1185,7 +1191,14 @@ API void amg_setup(amg_uint n, const amg_uint *Ai, const amg_uint *Aj, const dou
   amgd_h2d(dv, Av, (size_t)n * 8);
   free(hi); free(hj);
   amgd_hier *h = NULL;
+  /* amg_setup takes the WHOLE matrix on the calling process (amg_setup.h:5): with a
+     multi-process communicator in partitioned mode (where amgd_setup_device takes this
+     rank's share) it runs the one-GPU setup on this process alone -- no collective, so
+     one rank calling it cannot hang in an exchange the others never enter */
+  const int susp = amgd_comm_partitioned() && amgd_comm_procs() > 1;
+  if (susp) amgd_comm_suspend_partition(1);
   const int rc = amgd_setup_device(n, di, dj, dv, &h, 0);
+  if (susp) amgd_comm_suspend_partition(0);
   amgd_free(di); amgd_free(dj); amgd_free(dv);
   if (rc != 0) {
     /* no hierarchy: data is left with nlevels = 0 and amgd_error() says why */
@@ -1298,14 +1311,17 @@ struct crs_data { amgd_hier *h; amg_uint un; amg_uint null_space; };
    matrix -- n local dofs with global ids id[0..n), nz entries in local indices.  The
    reference hands the assembled matrix, keyed by global id (its amg_dump,
    amg.c:1048-1072, drops entries touching id 0 and exact zeros), to the setup.  Here
-   every rank's entries are mapped to global ids on the host, uploaded, and -- for
-   np > 1 -- completed into one COO on every rank by an allgatherv over the library's
-   communicator (amgd_comm_init_rccl / _host, rank = comm->id, size = comm->np), in
-   rank order; duplicates (dofs shared between ranks) are summed by build_csr in that
-   order.  The setup then runs row-sharded over the ranks (amgd_comm.hip) and every
-   rank keeps the hierarchy.  Global ids must be 1..N (row id-1 of the assembled
-   matrix).  Returns NULL (message on stderr, amgd_error()) on a communicator that
-   does not match comm, or when the setup runs out of HBM. */
+   every rank's entries are mapped to global ids on the host and uploaded; for np > 1
+   (library communicator amgd_comm_init_rccl / _host, rank = comm->id, size = comm->np):
+   * default, the partitioned setup: each rank's entries go to the
+     owners of their rows (duplicates -- dofs shared between ranks -- summed in rank
+     order), every rank keeps its row blocks of the hierarchy;
+   * after amgd_comm_set_partitioned(0), the round-2 replicated mode: the entries are
+     completed into one COO on every rank (allgatherv, rank order) and every rank keeps
+     the whole hierarchy, its heavy kernels row-sharded (amgd_comm.hip).
+   Global ids must be 1..N (row id-1 of the assembled matrix).  Returns NULL (message on
+   stderr, amgd_error()) on a communicator that does not match comm, or when the setup
+   runs out of HBM. */
 API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz, const amg_uint *Ai,
                                const amg_uint *Aj, const double *A, amg_uint null_space,
                                const struct comm *comm) {
@@ -1350,7 +1366,9 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
   /* entries of every rank: counts (above), then one allgatherv of (i, j, v) -- or, in
      partitioned mode, each rank hands its own entries to the partitioned setup, which
      routes them to the owners of their rows (the same rank order for duplicates) */
-  const int part = np > 1 && amgd_comm_partitioned();
+  const int part = np > 1 && amgd_comm_part_default();
+  const int part_was = amgd_comm_part_get();
+  if (part) amgd_comm_set_partitioned(1);
   for (int r = 0; r < np; r++) pre[r + 1] = pre[r] + (part && r != me ? 0 : cnt[r]);
   const uint64_t M = pre[np];
   uint32_t *di = (uint32_t *)amgd_alloc(M * 4 + 4), *dj = (uint32_t *)amgd_alloc(M * 4 + 4);
@@ -1371,7 +1389,12 @@ API struct crs_data *crs_setup(amg_uint n, const unsigned long *id, amg_uint nz,
     free(off);
   }
   free(cnt); free(pre);
+  /* np == 1: the whole matrix is this process's, the one-GPU setup */
+  const int susp = np <= 1 && amgd_comm_partitioned() && amgd_comm_procs() > 1;
+  if (susp) amgd_comm_suspend_partition(1);
   const int rc = amgd_setup_device(M, di, dj, dv, &d->h, 0);
+  if (susp) amgd_comm_suspend_partition(0);
+  if (part) amgd_comm_part_set(part_was);
   amgd_free(di); amgd_free(dj); amgd_free(dv);
   if (rc != 0) {
     fprintf(stderr, "omp_amg_amd: crs_setup failed: %s\n", amgd_last_error());

@@ -763,7 +763,7 @@ static int lane_rw(uint64_t n) {
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
-    amgd_route_hit(AMGD_R_SPMV_LANE);                                                         \
+    amgd_route_hit(AMGD_R_SPMV_PIPE);                                                         \
     amgd_route_hit(rw_ == 64 ? AMGD_R_MV_RW64 : rw_ == 16 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);   \
     const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
     if (rw_ == 64)                                                                            \
@@ -2401,7 +2401,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (kseq) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
   if (hc[1]) {
     if (kseq) {
-      amgd_route_hit(AMGD_R_SG_WSYM);
+      amgd_route_hit(AMGD_R_SG_WWIN_SYM);
       // bit-map windows of 32768 columns in 4 KB (round 4; the 4096-column byte maps
       // took 1239 against 909 ms per 256^3 setup, profiles/r04/ab_sym_ww)
       k_sg_wwin<32768, 2><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
@@ -2510,7 +2510,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 1024; }
   if (nt2 < 0) { const char *e = getenv("AMGD_SG_NT2"); nt2 = e ? atoi(e) : 512; }
   if (hn[0] || hn[1] || hn[2] || hn[3]) amgd_route_hit(kseq ? AMGD_R_SG_KSEQ : AMGD_R_SG_ROW);
-  if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WIN);
+  if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WWIN);
   if (hn[4]) amgd_route_hit(AMGD_R_SG_LONG);
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)

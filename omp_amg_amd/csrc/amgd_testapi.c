@@ -206,6 +206,26 @@ API void amgd_test_qf_reuse_stats(uint64_t *out) {
 /* cap on live device bytes (0: none): the out-of-HBM path without filling 288 GB */
 API void amgd_test_hbm_cap(uint64_t bytes) { amgd_set_hbm_cap((size_t)bytes); }
 API uint64_t amgd_test_pool_inuse(void) { return amgd_pool_bytes_in_use(); }
+/* one bare partitioned-mode collective (the collective guard's tests): kind 0 an allgatherv
+   of `bytes` per rank, 1 an alltoallv of `bytes` to every peer (expecting `expect` bytes
+   from each); returns 0 */
+API int amgd_test_comm(int kind, uint64_t bytes, uint64_t expect) {
+  const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  uint64_t *so = (uint64_t *)malloc(8 * ((size_t)N + 1)), *ro = (uint64_t *)malloc(8 * ((size_t)N + 1));
+  for (int p = 0; p <= N; p++) { so[p] = bytes * p; ro[p] = (kind ? expect : bytes) * p; }
+  char *sb = (char *)amgd_alloc(bytes * N + 16), *rb = (char *)amgd_alloc(ro[N] + 16);
+  amgd_memset(sb, me + 1, bytes * N);
+  if (kind == 0) {
+    void *b = sb;
+    amgd_allgatherv(1, &b, so);
+  } else {
+    amgd_pcomm_alltoallv(sb, so, rb, ro);
+  }
+  amgd_sync();
+  amgd_free(sb); amgd_free(rb);
+  free(so); free(ro);
+  return 0;
+}
 /* kernel-route counters since the last reset (out: AMGD_R_N entries) */
 API void amgd_test_route_stats(uint64_t *out, int reset) {
   for (int r = 0; r < AMGD_R_N; r++) out[r] = amgd_route_ctr[r];

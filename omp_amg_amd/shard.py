@@ -76,15 +76,28 @@ def init_host(rank: int, size: int, group=None) -> None:
 
 def init_rccl(rank: int, size: int, group=None) -> None:
     """RCCL communicator of the library (its own, on the library stream); the
-    unique id travels over the torch.distributed control group."""
-    import torch.distributed as dist
+    unique id travels over the torch.distributed control group (size 1: none needed)."""
     L = _lib()
     uid = C.create_string_buffer(128)
     if rank == 0 and L.amgd_comm_rccl_uid(uid) != 0:
         raise RuntimeError("amgd_comm_rccl_uid failed (librccl missing?)")
     box = [bytes(uid.raw)]
-    dist.broadcast_object_list(box, src=0, group=group)
-    rc = L.amgd_comm_init_rccl(rank, size, box[0])
+    if size > 1:
+        import torch.distributed as dist
+        dist.broadcast_object_list(box, src=0, group=group)
+    # RCCL prints its version banner on stdout at communicator creation: keep stdout for
+    # the caller's own output (bench.py's one JSON line) by sending fd 1 to stderr meanwhile
+    import os
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        rc = L.amgd_comm_init_rccl(rank, size, box[0])
+        C.CDLL(None).fflush(None)
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
     if rc != 0:
         raise RuntimeError(f"amgd_comm_init_rccl failed rc={rc}")
 

@@ -50,6 +50,9 @@ CASES = {
     "p7_64": ("oracle", {"kind": "poisson3d", "m": 64}),
     "p7_96": ("oracle", {"kind": "poisson3d", "m": 96}),
     "p7_128": ("oracle", {"kind": "poisson3d", "m": 128}),
+    # the smallest box measured to run the 64-rows-per-wavefront long-row SpMV by default
+    # (a >= 2^22-row long-row matrix: level 0's find_support R; tools/route_probe.py)
+    "p7_256x256x136": ("oracle", {"kind": "poisson3d", "m": 136, "mx": 256, "my": 256}),
     "aniso_20": ("oracle", {"kind": "poisson3d", "m": 20, "eps": 1e-3}),
     "aniso_24": ("oracle", {"kind": "poisson3d", "m": 24, "eps": 1e-3}),
     "aniso_32": ("oracle", {"kind": "poisson3d", "m": 32, "eps": 1e-3}),
@@ -67,7 +70,8 @@ CASES = {
 
 def generate(g: dict):
     if g["kind"] == "poisson3d":
-        return problems.poisson3d(g["m"], g.get("stencil", 7), eps=g.get("eps", 1.0))
+        return problems.poisson3d(g["m"], g.get("stencil", 7), eps=g.get("eps", 1.0), mx=g.get("mx"),
+                                  my=g.get("my"))
     if g["kind"] == "sem":
         e = g["e"]
         return problems.sem_laplacian(e, e, e, g["N"], seed=g["seed"], jitter=g["jitter"])

@@ -42,10 +42,69 @@ def main():
         digest = json.load(open(md.OUT))["cases"][case[7:]]
         Ai, Aj, Av = md.generate(digest["gen"])
     shard.init_host(rank, size)
-    oa.lib().amgd_comm_set_partitioned(1)
+    if not os.environ.get("PART_DEFAULT"):     # PART_DEFAULT: crs_setup's own default (partitioned)
+        oa.lib().amgd_comm_set_partitioned(1)
     shard.stats(reset=True)
     Ai64, Aj64, Av = np.asarray(Ai, np.int64), np.asarray(Aj, np.int64), np.asarray(Av)
-    if os.environ.get("PART_CRS"):
+    guard = os.environ.get("PART_GUARD")
+    if guard:
+        # the collective guard (AMGD_COMM_CHECK=1 in the env) must abort every rank on a
+        # kind / size disagreement: rank 1 enters a different collective (kind) or
+        # expects other byte counts (size) than rank 0 sends
+        L.amgd_test_comm.argtypes = [C.c_int, C.c_uint64, C.c_uint64]
+        L.amgd_test_comm(1, 64, 64)                         # agreeing alltoallv: passes
+        L.amgd_test_comm(0, 64, 0)                          # agreeing allgatherv: passes
+        if guard == "kind":
+            L.amgd_test_comm(0 if rank == 0 else 1, 64, 64)
+        else:
+            L.amgd_test_comm(1, 64, 64 if rank == 0 else 32)
+        print(json.dumps({"rank": rank, "unexpected": "no abort"}), flush=True)
+        sys.exit(0)
+    if os.environ.get("PART_OOM"):
+        # rank 1 runs out of HBM inside the partitioned setup; with the guard on, every
+        # rank's setup unwinds and returns -2 (none aborts), nothing stays allocated, and
+        # the next setup of the same ranks is the fixture
+        L.amgd_test_hbm_cap.argtypes = [C.c_uint64]
+        nz = len(Av)
+        k0, k1 = rank * nz // size, (rank + 1) * nz // size
+        ds = oa.DeviceSetup(Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+        held = L.amgd_test_pool_inuse()
+        ds.run()                                  # uncapped: this rank's peak
+        peak = int(oa.stats()["peak_bytes"])
+        ds.close()
+        ds = oa.DeviceSetup(Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+        held = L.amgd_test_pool_inuse()
+        if rank == 1:                             # a cap at PART_OOM of the way to the peak
+            L.amgd_test_hbm_cap(held + int((peak - held) * float(os.environ["PART_OOM"])))
+        failed = False
+        try:
+            ds.run()
+        except RuntimeError as e:
+            failed = True
+            out["error"] = str(e)[:200]
+        L.amgd_test_hbm_cap(0)
+        assert failed, "the capped setup did not fail on this rank"
+        assert L.amgd_test_pool_inuse() == held, (L.amgd_test_pool_inuse(), held)
+        ds.run()
+        h = ds.export()
+        ds.close()
+    elif os.environ.get("PART_AMG_SETUP"):
+        # amg_setup (amg_setup.h:5) takes the WHOLE matrix on every calling process, also
+        # with a partitioned multi-process communicator: no exchange, the one-GPU setup
+        h = abi.run_setup(oa.lib(), Ai64, Aj64, Av)
+        st = shard.stats()
+        assert st["calls"] == 0, st
+        shard.stats(reset=True)
+        # then the same ranks' partitioned setup still works (nothing left suspended)
+        nz = len(Av)
+        k0, k1 = rank * nz // size, (rank + 1) * nz // size
+        ds = oa.DeviceSetup(Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+        ds.run()
+        h2 = ds.export()
+        ds.close()
+        bad2 = parity.compare(h, h2, exact=True)
+        assert not bad2, bad2[:5]
+    elif os.environ.get("PART_CRS"):
         n = int(max(Ai64.max(), Aj64.max())) + 1
         lo, hi = rank * n // size, (rank + 1) * n // size
         sel = (Ai64 >= lo) & (Ai64 < hi)
@@ -55,9 +114,14 @@ def main():
         h = abi.crs_export(oa.lib(), hd)
         oa.lib().crs_free(hd)
     else:
+        # amgd_setup_device (omp_amg_amd.h): in partitioned mode its COO is this rank's
+        # share of the matrix (amg_setup keeps the reference's whole-matrix meaning)
         nz = len(Av)
         k0, k1 = rank * nz // size, (rank + 1) * nz // size
-        h = abi.run_setup(oa.lib(), Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+        ds = oa.DeviceSetup(Ai64[k0:k1], Aj64[k0:k1], Av[k0:k1])
+        ds.run()
+        h = ds.export()
+        ds.close()
     st = shard.stats()
     out["peak_bytes"] = int(oa.stats()["peak_bytes"])
     shard.free()

@@ -32,6 +32,7 @@ def main():
         Ai, Aj, Av = problems.poisson3d(m, 27 if case.startswith("p27") else 7)
         ref = abi.run_setup(oa.lib(), Ai, Aj, Av)            # one GPU, before sharding
     shard.init_host(rank, size)
+    oa.lib().amgd_comm_set_partitioned(0)      # the round-2 replicated mode (crs_setup's default is partitioned)
     shard.set_min_work(0.0)
     shard.stats(reset=True)
     if os.environ.get("SHARD_CRS"):

@@ -23,7 +23,7 @@ def declared_functions():
                 continue
             # only names in a declaration position: preceded by a type on the line
             line = src[src.rfind("\n", 0, m.start()) + 1:m.start()]
-            if re.search(r"(void|int|double|char|\*|struct\s+\w+\s*\*?)\s*$", line.strip() + " ") and \
+            if re.search(r"(void|int|double|char|u?int\d+_t|size_t|\*|struct\s+\w+\s*\*?)\s*$", line.strip() + " ") and \
                     not line.strip().startswith(("typedef", "#")):
                 names.add(name)
     return names

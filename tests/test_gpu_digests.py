@@ -9,8 +9,9 @@ for bit to the reference's own outputs.  Equal digests = bit-identical hierarchy
 
 The GPU run also records which kernel routes ran (omp_amg_amd.route_stats), so each
 case shows that the paths the small fixtures reach only by forcing -- incremental
-coarsening and find_support sweeps, lane SpMV, windowed / k-sequential SpGEMM --
-were the ones that produced the matching bits.
+coarsening and find_support sweeps, the pipelined long-row SpMV (k_spmv_pipe) with 4 / 16
+rows per wavefront, wave-private windowed / k-sequential SpGEMM, the 512- / 1024-point
+Q-factor tiers -- were the ones that produced the matching bits.
 """
 import json
 import os
@@ -35,20 +36,24 @@ def _mk():
     return make_digests
 
 
-# routes each case must have taken (kept to what its sizes guarantee by the defaults)
+# routes each case must take with the default routing (what its sizes guarantee; the
+# 64-rows-per-wavefront SpMV needs a >= 2^22-row long-row matrix, which no digest here has
+# -- test_gpu_matches_digest_rw64_forced covers its shape on p7_96 / p7_128)
 EXPECT_ROUTES = {
-    "p7_48": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
-    "p7_64": ("cs_inc", "fs_inc", "spmv_lane", "mv_long", "sg_tiny", "sg_win", "sg_wsym", "qf_reuse"),
-    "p7_96": ("cs_inc", "fs_inc", "spmv_lane", "mv_rw16", "mv_long", "sg_tiny", "sg_win", "sg_wsym",
+    "p7_48": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_long", "sg_tiny", "sg_wwin", "sg_wwin_sym",
               "qf_reuse"),
-    "p7_128": ("cs_inc", "fs_inc", "spmv_lane", "mv_rw16", "mv_long", "sg_tiny", "sg_win", "sg_wsym",
-               "qf_reuse"),
+    "p7_64": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_long", "sg_tiny", "sg_wwin", "sg_wwin_sym",
+              "qf_reuse"),
+    "p7_96": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "mv_long", "sg_tiny", "sg_wwin",
+              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024"),
+    "p7_128": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "mv_long", "sg_tiny", "sg_wwin",
+               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024"),
     "aniso_20": ("fs_inc", "mv_long"),
-    "aniso_32": ("fs_inc", "spmv_lane"),
-    "p27_20": ("fs_inc", "spmv_lane", "sg_win", "sg_wsym"),
-    "sem_e3_N7": ("spmv_lane", "sg_wsym"),
-    "sem_e4_N7": ("spmv_lane", "sg_kseq", "sg_wsym"),
-    "sem_e5_N7": ("spmv_lane", "sg_kseq"),
+    "aniso_32": ("fs_inc", "spmv_pipe"),
+    "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin", "sg_wwin_sym"),
+    "sem_e3_N7": ("spmv_pipe", "sg_wwin_sym"),
+    "sem_e4_N7": ("spmv_pipe", "sg_kseq", "sg_wwin_sym"),
+    "sem_e5_N7": ("spmv_pipe", "sg_kseq"),
 }
 
 
@@ -70,3 +75,27 @@ def test_gpu_matches_digest_default_routing(case):
     missing = [r for r in EXPECT_ROUTES.get(case, ()) if routes[r] == 0]
     assert not missing, f"default routes not taken: {missing} ({routes})"
     print(case, d["source"], d["summary"]["n"], routes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["p7_96", "p7_128"])
+def test_gpu_matches_digest_rw64_forced(case):
+    """the 64-rows-per-wavefront long-row SpMV (k_spmv_pipe<*,64,16>, by default only on
+    >= 2^22-row long-row matrices, amgd_sparse.hip lane_rw) forced on every long-row
+    product of the 0.9 M / 2.1 M-row digests: the whole hierarchy stays bit-identical"""
+    mk = _mk()
+    d = _db()["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    oa.route_stats(reset=True)
+    oa.spmv_rw(64)
+    try:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.spmv_rw(-1)
+    routes = oa.route_stats(reset=True)
+    got = mk.hierarchy_digest(h)
+    exp = d["arrays"]
+    bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    assert not bad, f"{len(bad)} arrays differ: {bad[:12]}"
+    assert routes["mv_rw64"] > 0 and routes["mv_rw16"] == 0 and routes["mv_rw4"] == 0, routes
+    print(case, routes)

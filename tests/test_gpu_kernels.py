@@ -187,9 +187,9 @@ def test_spgemm_wave_windows(case, win):
         oa.spgemm_win(-1)
     routes = oa.route_stats(reset=True)
     if win > 0:
-        assert routes["sg_win"] > 0
+        assert routes["sg_wwin"] > 0
     if win == 0:
-        assert routes["sg_win"] == 0
+        assert routes["sg_wwin"] == 0
     assert refops.same(X, R)
 
 
@@ -278,7 +278,7 @@ def test_spgemm_symbolic_windows(case):
     R = refops.spgemm(A, B)
     oa.route_stats(reset=True)
     X = oa.test_csr_op(0, A, B)
-    assert oa.route_stats(reset=True)["sg_wsym"] > 0
+    assert oa.route_stats(reset=True)["sg_wwin_sym"] > 0
     assert refops.same(X, R)
 
 
@@ -530,7 +530,7 @@ def test_spmv_long_rows_ragged(sl_min, rw, chunk):
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
 def test_spmv_rows_listed(sl_min, rw, mv_long, chunk):
     """listed-row products (amgd_spmv_rows): wave-per-row list kernel below the row
-    threshold, lane-per-row k_spmv_lane<true> with it forced to 0; unlisted rows untouched"""
+    threshold, lane-per-row k_spmv_pipe<true> with it forced to 0; unlisted rows untouched"""
     rng = np.random.default_rng(29)
     L = _ragged_long_rows(np.random.default_rng(23))
     x = rng.standard_normal(L.cn)

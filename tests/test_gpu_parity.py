@@ -284,7 +284,7 @@ def test_gpu_lane_spmv_forced_matches_default(gen, inc, monkeypatch):
     try:
         oa.route_stats(reset=True)
         h_f = abi.run_setup(oa.lib(), Ai, Aj, Av)
-        assert oa.route_stats(reset=True)["spmv_lane"] > 0
+        assert oa.route_stats(reset=True)["spmv_pipe"] > 0
     finally:
         oa.spmv_sl_min(-1)
     bad = parity.compare(h_d, h_f, exact=True)

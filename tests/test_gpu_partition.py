@@ -24,13 +24,19 @@ def _free_port():
     return p
 
 
-def _run(size, case, crs="", timeout=110, extra_env=None):
+def _spawn(size, case, crs="", extra_env=None):
     port = _free_port()
+    # every partitioned test runs with the collective-consistency guard on
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(size),
-               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8", **(extra_env or {}))
-    ps = [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "part_worker.py")],
-                           env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                           text=True) for r in range(size)]
+               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8", AMGD_COMM_CHECK="1",
+               **(extra_env or {}))
+    return [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "part_worker.py")],
+                             env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True) for r in range(size)]
+
+
+def _run(size, case, crs="", timeout=110, extra_env=None):
+    ps = _spawn(size, case, crs, extra_env)
     outs = []
     for p in ps:
         try:
@@ -88,6 +94,19 @@ def test_partitioned_crs_setup():
     _run(3, "gold:p7_12", crs="1")
 
 
+def test_crs_setup_defaults_to_partitioned():
+    """crs_setup(comm = {rank, 2}) with no mode chosen runs the partitioned setup (each
+    rank's rows stay on it; the matrix is never gathered): the reference fixture"""
+    _run(2, "gold:p7_12", crs="1", extra_env={"PART_DEFAULT": "1"})
+
+
+def test_amg_setup_under_partitioned_comm():
+    """amg_setup with a 2-process partitioned communicator: each process passes the whole
+    matrix (the reference's meaning) and gets the one-GPU hierarchy with no exchange;
+    then the partitioned setup of the same ranks matches it bit for bit"""
+    _run(2, "gold:amgdmp", extra_env={"PART_AMG_SETUP": "1"})
+
+
 @pytest.mark.parametrize("case", ["p7_48", "p27_20", "sem_e4_N7"])
 def test_partitioned_one_rank_rccl(case):
     """the partitioned driver with a one-rank RCCL communicator (every partitioned
@@ -114,3 +133,32 @@ def test_partitioned_one_rank_rccl(case):
     got = md.hierarchy_digest(h)
     bad = sorted(k for k in set(got) | set(d["arrays"]) if got.get(k) != d["arrays"].get(k))
     assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("what", ["kind", "size"])
+def test_collective_guard_aborts_every_rank(what):
+    """AMGD_COMM_CHECK=1: rank 1 enters an alltoallv where rank 0 enters an allgatherv
+    (a rank-local skip, round 4's r04e fault), or expects 32 bytes where rank 0 sends 64:
+    both ranks abort, naming the mismatch, instead of corrupting or hanging"""
+    ps = _spawn(2, "gold:p7_4", extra_env={"PART_GUARD": what})
+    outs = []
+    for p in ps:
+        try:
+            o, e = p.communicate(timeout=90)
+        except subprocess.TimeoutExpired:
+            for q in ps:
+                q.kill()
+            raise
+        outs.append((p.returncode, o, e))
+    for r, (rc, o, e) in enumerate(outs):
+        assert rc != 0, f"rank {r} did not abort: {o[-500:]}"
+        assert "COLLECTIVE MISMATCH" in e, f"rank {r}: {e[-1500:]}"
+        assert "no abort" not in o
+
+
+def test_out_of_hbm_on_one_rank_unwinds_all():
+    """rank 1 of 2 runs out of HBM mid-setup: with the guard every rank's setup returns
+    -2 (the failure travels in the guard record), no device bytes stay held, and the
+    ranks' next setup is the reference fixture bit for bit"""
+    res = _run(2, "gold:p7_12", extra_env={"PART_OOM": "0.5"})
+    assert all("out of HBM" in d.get("error", "") or "failed" in d.get("error", "") for d in res), res

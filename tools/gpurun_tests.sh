@@ -1,10 +1,21 @@
-# GPU tests (optionally a -k filter / file list), then optional config probes
+# one GPU call: a subset of the GPU suite (pytest -k / file args), then optional steps
+# usage: bash tools/gpurun_tests.sh <tag> <pytest args...>
+#   PHASES=1: afterwards one-GPU and partitioned-N=1 setups of 256^3 with AMGD_PHASES=1
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-export PYTHONPATH=$PWD
-TAG=${TAG:-r02}
-timeout -k 10 ${TLIM:-600} python3 -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 150 --timeout-method thread ${KSEL:+-k "$KSEL"} > gpurun_out/gputests_$TAG.log 2>&1
-rc=$?
-grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/gputests_$TAG.log | tail -40
-exit $rc
+TAG=${1:-tests}; shift
+D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+rm -rf $D; mkdir -p $D
+export PYTHONPATH=$GRAFT_REPO_ROOT
+if [ $# -gt 0 ]; then
+timeout -k 10 1000 python3 -u -m pytest "$@" -x -v --durations=20 --timeout 400 --timeout-method thread > $D/tests.log 2>&1 || { grep -E "PASS|FAIL|Error|error" $D/tests.log | tail -30; exit 1; }
+grep -E "passed|failed" $D/tests.log | tail -2
+grep -E "s call" $D/tests.log | head -12
+fi
+if [ -n "$PHASES" ]; then
+for mode in one part; do
+  extra=""; [ $mode = part ] && extra="--mode part"
+  AMGD_PHASES=1 timeout -k 10 400 python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline $extra > $D/bench_$mode.json 2> $D/phases_$mode.log || { tail -20 $D/phases_$mode.log; exit 1; }
+  tail -n 1 $D/bench_$mode.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$mode', round(d['ms_per_step']), d['phases_ms'])"
+done
+fi
