@@ -9,9 +9,11 @@
  *   they print a diagnostic and abort.
  *
  * `struct comm` is gslib's (comm.h:85-88) for a non-MPI build: {uint id, np; int c}.
- * np > 1: rank comm->id passes its local rows; the library's own communicator
- * (omp_amg_amd.h amgd_comm_init_rccl / _host, same rank and size) gathers the
- * assembled matrix and runs the row-sharded setup (DESIGN.md "Multi-GPU").
+ * np > 1: rank comm->id passes its local rows over the library's own communicator
+ * (omp_amg_amd.h amgd_comm_init_rccl / _host, same rank and size); by default the
+ * setup is row-partitioned -- each rank keeps its row blocks of the hierarchy and the
+ * matrix is never gathered; amgd_comm_set_partitioned(0) selects the
+ * replicated mode (matrix gathered to every rank, row-sharded kernels).
  * On failure (communicator mismatch, out of HBM) crs_setup returns NULL and
  * amgd_error() holds the reason; the reference exits the process instead.
  * amgd_crs_export (omp_amg_amd.h) copies the kept hierarchy out.

@@ -111,6 +111,7 @@ void amgd_shard_split(const uint64_t *prefix, uint32_t n, uint32_t *split_h);
    so every rank unwinds its setup together (amgd_comm_fail_agree). */
 void amgd_comm_site(const char *file, int line);
 int amgd_comm_fail_agree(void);    /* 1: every rank was told of this rank's failure */
+void amgd_comm_site_report(void);  /* AMGD_COMM_SITES=1: collectives per call site (stderr) */
 /* range s of buffer b = bytes [off[b*(N+1)+s], off[b*(N+1)+s+1]), completed on every rank */
 void amgd_allgatherv_(int nbuf, void *const *bufs, const uint64_t *off);
 #define amgd_allgatherv(...) (amgd_comm_site(__FILE__, __LINE__), amgd_allgatherv_(__VA_ARGS__))
@@ -133,6 +134,10 @@ void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m);  /* vals_h[N*m]: own m 
 /* rank sends send[soff[p]..soff[p+1]) to p, receives p's into recv[roff[p]..roff[p+1]) (bytes) */
 void amgd_pcomm_alltoallv_(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff);
 #define amgd_pcomm_alltoallv(...) (amgd_comm_site(__FILE__, __LINE__), amgd_pcomm_alltoallv_(__VA_ARGS__))
+/* nb such exchanges (buffers b = 0..nb-1) in one collective */
+void amgd_pcomm_alltoallv_n_(int nb, const void *const *send, const uint64_t *const *soff, void *const *recv,
+                             const uint64_t *const *roff);
+#define amgd_pcomm_alltoallv_n(...) (amgd_comm_site(__FILE__, __LINE__), amgd_pcomm_alltoallv_n_(__VA_ARGS__))
 
 /* ---------------- reductions (return host values, sync) ---------------- */
 void amgd_set_exact(int on);     /* 1: reference-order (sequential) dots -- default; 0: tree */
@@ -292,6 +297,7 @@ uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, do
                         uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
 /* the same over rows c0.. of R' (w, sumR at c0; sel_j global); perm NULL: R untouched;
    resum 0: rs / sumR not re-summed (partitioned mode) */
+void amgd_list_rowsum(const dcsr *M, const uint32_t *list, uint32_t n, double *out, int long_rows);
 uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
                            const double *w, double *sumR, double thr, uint32_t *sel_i,
                            uint32_t *sel_j, uint32_t *nremoved, uint32_t c0, int resum);

@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "amgd.h"
@@ -55,6 +56,7 @@ static uint64_t g_bytes = 0, g_calls = 0;
 // transposes, routed entries), [2] allgathers of a few u64 (counts, flags, maxima); calls, bytes
 static uint64_t g_kstat[3][2];
 static int g_kind_small = 0;
+static int g_inner = 0;        // host-transport alltoallv staging: its allgathervs are not counted
 static uint64_t g_seq = 0, g_guard_calls = 0;   // collective guard: records exchanged (below)
 static double g_ms = 0;
 
@@ -239,6 +241,34 @@ static int check_on(void) {
   return g_check;
 }
 extern "C" API uint64_t amgd_comm_guard_calls(void) { return g_guard_calls; }
+// AMGD_COMM_SITES=1: calls and bytes per call site and kind (the outermost caller's
+// file:line), printed by amgd_comm_site_report -- where a setup's collectives come from
+#include <map>
+#include <string>
+static int g_sites = -1;
+static std::map<std::string, std::pair<uint64_t, uint64_t>> g_site_stats;
+static void site_count(const char *kind, uint64_t bytes) {
+  if (g_sites < 0) { const char *e = getenv("AMGD_COMM_SITES"); g_sites = e && *e && atoi(e) ? 1 : 0; }
+  if (!g_sites) return;
+  char k[256];
+  const char *f = g_site_f ? strrchr(g_site_f, '/') : nullptr;
+  snprintf(k, sizeof k, "%s:%d %s", f ? f + 1 : g_site_f ? g_site_f : "?", g_site_l, kind);
+  auto &v = g_site_stats[k];
+  v.first++;
+  v.second += bytes;
+}
+void amgd_comm_site_report(void) {
+  if (g_sites <= 0 || g_site_stats.empty()) return;
+  std::vector<std::pair<uint64_t, std::string>> v;
+  uint64_t tot = 0;
+  for (auto &e : g_site_stats) { v.push_back({e.second.first, e.first}); tot += e.second.first; }
+  std::sort(v.rbegin(), v.rend());
+  fprintf(stderr, "rank %d collectives by call site: %lu in total\n", g_rank, (unsigned long)tot);
+  for (auto &e : v)
+    fprintf(stderr, "rank %d site %-40s %8lu calls %10.3f MB\n", g_rank, e.second.c_str(), (unsigned long)e.first,
+            g_site_stats[e.second].second / 1e6);
+  g_site_stats.clear();
+}
 static uint64_t fnv(const void *p, size_t n, uint64_t h = 1469598103934665603ull) {
   const unsigned char *c = (const unsigned char *)p;
   for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
@@ -353,10 +383,13 @@ void amgd_allgatherv_(int nbuf, void *const *bufs, const uint64_t *off) {
   double t0 = amgd_wtime();
   uint64_t nb = 0;
   for (int b = 0; b < nbuf; b++) nb += off[b * (N + 1) + N] - off[b * (N + 1)];
-  g_bytes += nb;
-  g_calls++;
-  g_kstat[g_kind_small ? 2 : 0][0]++;
-  g_kstat[g_kind_small ? 2 : 0][1] += nb;
+  if (!g_inner) {             // counted as the collective an RCCL run makes
+    g_bytes += nb;
+    g_calls++;
+    site_count(g_kind_small ? "u64" : "allgatherv", nb);
+    g_kstat[g_kind_small ? 2 : 0][0]++;
+    g_kstat[g_kind_small ? 2 : 0][1] += nb;
+  }
   if (g_kind == COMM_HOST) {
     amgd_sync();
     if (g_cb(g_user, nbuf, bufs, off, g_rank, N) != 0) {
@@ -476,78 +509,97 @@ void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m) {
 // both sides must agree: callers exchange counts first).  RCCL: one group of send/recv
 // pairs with every peer (each xGMI link carries its own pair).  Host transport: staged
 // through the allgatherv callback (every rank sees every send buffer; tests only).
-void amgd_pcomm_alltoallv_(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+// host transport (tests, several ranks on one GPU): N-1 rounds; in round k every rank
+// contributes its piece for rank (r + k) mod N to one allgatherv and takes the piece of
+// rank (r - k) mod N -- staging per round ~1/N of the data, not all of it
+static void a2a_host(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+  const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  g_inner = 1;
+  std::vector<uint64_t> so((size_t)N * (N + 1));
+  uint64_t *dt = (uint64_t *)amgd_alloc(8ull * N * (N + 1) + 8);
+  amgd_h2d(dt + (size_t)me * (N + 1), soff, 8ull * (N + 1));
+  {
+    std::vector<uint64_t> o(N + 1);
+    for (int q = 0; q <= N; q++) o[q] = 8ull * q * (N + 1);
+    void *b = dt;
+    amgd_allgatherv(1, &b, o.data());
+  }
+  amgd_d2h(so.data(), dt, 8ull * N * (N + 1));
+  amgd_free(dt);
+  for (int k = 1; k < N; k++) {
+    std::vector<uint64_t> base(N + 1, 0);
+    for (int r = 0; r < N; r++) {
+      const int d = (r + k) % N;
+      const uint64_t *sr = so.data() + (size_t)r * (N + 1);
+      base[r + 1] = base[r] + (sr[d + 1] - sr[d]);
+    }
+    if (base[N] == 0) continue;
+    char *stage = (char *)amgd_alloc(base[N] + 16);
+    const int dst = (me + k) % N, src = (me - k + N) % N;
+    const uint64_t mine = soff[dst + 1] - soff[dst];
+    if (mine) HIPCK(hipMemcpyAsync(stage + base[me], (const char *)send + soff[dst], mine,
+                                   hipMemcpyDeviceToDevice, amgd_s()));
+    {
+      std::vector<uint64_t> o(base.begin(), base.end());
+      void *b = stage;
+      amgd_allgatherv(1, &b, o.data());
+    }
+    const uint64_t len = base[src + 1] - base[src];
+    if (len != roff[src + 1] - roff[src]) {
+      fprintf(stderr, "omp_amg_amd: alltoallv: rank %d expects %lu bytes from %d, which sends %lu\n", me,
+              (unsigned long)(roff[src + 1] - roff[src]), src, (unsigned long)len);
+      abort();
+    }
+    if (len) HIPCK(hipMemcpyAsync((char *)recv + roff[src], stage + base[src], len, hipMemcpyDeviceToDevice,
+                                  amgd_s()));
+    g_bytes += len;
+    amgd_sync();
+    amgd_free(stage);
+  }
+  g_inner = 0;
+}
+
+// nb personalised exchanges in one collective (RCCL: one group of send/recv pairs)
+void amgd_pcomm_alltoallv_n_(int nb, const void *const *send, const uint64_t *const *soff, void *const *recv,
+                             const uint64_t *const *roff) {
   SiteScope site_;
   const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
-  if (N > 1 && check_on()) {
+  for (int b = 0; b < nb && N > 1 && check_on(); b++) {
     std::vector<uint64_t> sl(N), rl(N);
-    for (int p = 0; p < N; p++) { sl[p] = soff[p + 1] - soff[p]; rl[p] = roff[p + 1] - roff[p]; }
+    for (int p = 0; p < N; p++) { sl[p] = soff[b][p + 1] - soff[b][p]; rl[p] = roff[b][p + 1] - roff[b][p]; }
     guard(GK_A2A, 0, sl.data(), rl.data());
   }
-  const uint64_t own = soff[me + 1] - soff[me];
-  if (own) HIPCK(hipMemcpyAsync((char *)recv + roff[me], (const char *)send + soff[me], own,
-                                hipMemcpyDeviceToDevice, amgd_s()));
+  for (int b = 0; b < nb; b++) {
+    const uint64_t own = soff[b][me + 1] - soff[b][me];
+    if (own) HIPCK(hipMemcpyAsync((char *)recv[b] + roff[b][me], (const char *)send[b] + soff[b][me], own,
+                                  hipMemcpyDeviceToDevice, amgd_s()));
+  }
   if (N == 1) return;
   double t0 = amgd_wtime();
   g_calls++;
+  uint64_t rb = 0;
+  for (int b = 0; b < nb; b++)
+    for (int p = 0; p < N; p++) if (p != me) rb += roff[b][p + 1] - roff[b][p];
+  site_count("alltoallv", rb);
   g_kstat[1][0]++;
-  for (int p = 0; p < N; p++) if (p != me) g_kstat[1][1] += roff[p + 1] - roff[p];
+  g_kstat[1][1] += rb;
   if (g_kind == COMM_RCCL) {
     hipStream_t s = amgd_s();
     NCCK(R.GroupStart());
-    for (int p = 0; p < N; p++) {
-      if (p == me) continue;
-      const uint64_t sl = soff[p + 1] - soff[p], rl = roff[p + 1] - roff[p];
-      if (sl) NCCK(R.Send((const char *)send + soff[p], sl, ncclChar, p, g_nc, s));
-      if (rl) NCCK(R.Recv((char *)recv + roff[p], rl, ncclChar, p, g_nc, s));
-      g_bytes += rl;
-    }
+    for (int b = 0; b < nb; b++)
+      for (int p = 0; p < N; p++) {
+        if (p == me) continue;
+        const uint64_t sl = soff[b][p + 1] - soff[b][p], rl = roff[b][p + 1] - roff[b][p];
+        if (sl) NCCK(R.Send((const char *)send[b] + soff[b][p], sl, ncclChar, p, g_nc, s));
+        if (rl) NCCK(R.Recv((char *)recv[b] + roff[b][p], rl, ncclChar, p, g_nc, s));
+        g_bytes += rl;
+      }
     NCCK(R.GroupEnd());          // stream-ordered like amgd_allgatherv: no host sync
   } else {
-    // host transport (tests, several ranks on one GPU): N-1 rounds; in round k every rank
-    // contributes its piece for rank (r + k) mod N to one allgatherv and takes the piece
-    // of rank (r - k) mod N -- staging per round ~1/N of the data, not all of it
-    std::vector<uint64_t> so((size_t)N * (N + 1));
-    uint64_t *dt = (uint64_t *)amgd_alloc(8ull * N * (N + 1) + 8);
-    amgd_h2d(dt + (size_t)me * (N + 1), soff, 8ull * (N + 1));
-    {
-      std::vector<uint64_t> o(N + 1);
-      for (int q = 0; q <= N; q++) o[q] = 8ull * q * (N + 1);
-      void *b = dt;
-      amgd_allgatherv(1, &b, o.data());
-    }
-    amgd_d2h(so.data(), dt, 8ull * N * (N + 1));
-    amgd_free(dt);
-    for (int k = 1; k < N; k++) {
-      std::vector<uint64_t> base(N + 1, 0);
-      for (int r = 0; r < N; r++) {
-        const int d = (r + k) % N;
-        const uint64_t *sr = so.data() + (size_t)r * (N + 1);
-        base[r + 1] = base[r] + (sr[d + 1] - sr[d]);
-      }
-      if (base[N] == 0) continue;
-      char *stage = (char *)amgd_alloc(base[N] + 16);
-      const int dst = (me + k) % N, src = (me - k + N) % N;
-      const uint64_t mine = soff[dst + 1] - soff[dst];
-      if (mine) HIPCK(hipMemcpyAsync(stage + base[me], (const char *)send + soff[dst], mine,
-                                     hipMemcpyDeviceToDevice, amgd_s()));
-      {
-        std::vector<uint64_t> o(base.begin(), base.end());
-        void *b = stage;
-        amgd_allgatherv(1, &b, o.data());
-      }
-      const uint64_t len = base[src + 1] - base[src];
-      if (len != roff[src + 1] - roff[src]) {
-        fprintf(stderr, "omp_amg_amd: alltoallv: rank %d expects %lu bytes from %d, which sends %lu\n", me,
-                (unsigned long)(roff[src + 1] - roff[src]), src, (unsigned long)len);
-        abort();
-      }
-      if (len) HIPCK(hipMemcpyAsync((char *)recv + roff[src], stage + base[src], len, hipMemcpyDeviceToDevice,
-                                    amgd_s()));
-      g_bytes += len;
-      amgd_sync();
-      amgd_free(stage);
-    }
+    for (int b = 0; b < nb; b++) a2a_host(send[b], soff[b], recv[b], roff[b]);
   }
   g_ms += (amgd_wtime() - t0) * 1e3;
+}
+void amgd_pcomm_alltoallv_(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
+  amgd_pcomm_alltoallv_n_(1, &send, &soff, &recv, &roff);
 }

@@ -2428,6 +2428,17 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
   return h;
 }
 
+// ordered row sums (+0, left to right) of the listed rows of M into out[row]: one thread
+// per row for short rows, the long-row SpMV kernels (amgd_spmv_rows) for long ones.  M may
+// be a global-row view (other ranks' rows empty: their sums come out +0)
+extern "C" void amgd_list_rowsum(const dcsr *M, const uint32_t *list, uint32_t n, double *out, int long_rows) {
+  if (!n) return;
+  if (!long_rows)
+    k_list_rowsum_t<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, M->a, list, n, out);
+  else
+    amgd_spmv_rows(M, list, n, nullptr, out);
+  KCHECK();
+}
 // One selection sweep: select + remove, then bring rs (row sums of R) and sumR
 // (column sums) up to date for the rows / columns that lost an entry.
 extern "C" uint32_t amgd_fs_select(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
@@ -2480,16 +2491,8 @@ extern "C" uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint
   h[0] = h[2];                    // selections = bad columns (one per column)
   if (c0 && h[0]) k_add_u32<<<grid_for(h[0]), 256, 0, s>>>(sel_j, h[0], c0);
   if (h[1] && resum) {
-    const dcsr *M[2] = {Rl, Rt};
-    const uint32_t *L[2] = {sel_i, sel_j};
-    double *O[2] = {rs, sumR};
-    for (int q = 0; q < 2; q++) {
-      if (M[q]->nnz <= 32ull * M[q]->rn)
-        k_list_rowsum_t<<<grid_for(h[0]), 256, 0, s>>>(M[q]->ro, M[q]->a, L[q], h[0], O[q]);
-      else
-        amgd_spmv_rows(M[q], L[q], h[0], nullptr, O[q]);
-    }
-    KCHECK();
+    amgd_list_rowsum(Rl, sel_i, h[0], rs, Rl->nnz > 32ull * Rl->rn);
+    amgd_list_rowsum(Rt, sel_j, h[0], sumR, Rt->nnz > 32ull * Rt->rn);
   }
   amgd_free(list);
   amgd_free(cnt);

@@ -56,6 +56,17 @@ void pm_allgather_vec(void *v, size_t elem, const apart *P);
 /* z_i for listed rows i (the list may differ in order between ranks, not in content):
    each rank holds the values of the listed rows it owns; afterwards every rank holds all */
 void pm_list_sync(double *z, const uint32_t *list, uint32_t n, const apart *P);
+/* the same for nv vectors (each its list and partition) in one exchange */
+void pm_list_sync_n(int nv, double *const *z, const uint32_t *const *list, const uint32_t *n,
+                    const apart *const *P);
+/* every rank's `bytes` (device) and one u64 to every rank, concatenated in rank order (the
+   returned device buffer, amgd_free it): len[p] bytes of rank p, users[p] its value.  One
+   collective while the shares fit the call site's adaptive eager slot (a pm_eager kept by
+   the caller, zero-initialised; every rank adapts it alike). */
+typedef struct { uint64_t slot, gen; } pm_eager;
+void pm_eager_new_setup(void);   /* every partitioned setup starts from the default slots */
+char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes, uint64_t user, uint64_t *len,
+                       uint64_t *users, uint64_t *total);
 
 /* global-row view of A: row offsets for all rp->n rows (rows of other ranks empty),
    the same col / a arrays.  pm_gview_free releases the offsets only. */
@@ -111,6 +122,9 @@ uint32_t *pm_kpos(const pmat *Wskel, const dcsr *WtE);
 void pm_zero_entries(pmat *M, const uint32_t *ri, const uint32_t *cj, uint64_t n);
 /* out[i] = ordered sum of row i of M for the listed rows (whole list), completed everywhere */
 void pm_list_rowsum(const pmat *M, const uint32_t *list, uint32_t n, double *out);
+/* rows la of A into oa and rows lb of B into ob (n each), one exchange */
+void pm_list_rowsum2(const pmat *A, const uint32_t *la, double *oa, const pmat *B, const uint32_t *lb,
+                     double *ob, uint32_t n);
 /* the own rows of the whole COO (ri, cj, 1) as a partitioned CSR */
 pmat *pm_coo_ones(const uint32_t *ri, const uint32_t *cj, uint64_t n, const apart *rp, const apart *cp);
 

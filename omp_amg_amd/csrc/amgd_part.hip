@@ -112,36 +112,159 @@ __global__ void k_list_own(const uint32_t *list, uint32_t n, uint32_t lo, uint32
 __global__ void k_list_scatter(const uint32_t *oi, const double *ov, uint64_t n, double *z) {
   GRID_STRIDE(t, n) z[oi[t]] = ov[t];
 }
-extern "C" void pm_list_sync(double *z, const uint32_t *list, uint32_t n, const apart *P) {
-  const int N = P->N, me = amgd_pcomm_rank();
-  if (N == 1) return;
-  uint32_t *oi = (uint32_t *)amgd_alloc(4ull * n + 8);
-  double *ov = (double *)amgd_alloc(8ull * n + 8);
-  unsigned *cnt = (unsigned *)amgd_alloc(8);
-  amgd_memset(cnt, 0, 4);
-  if (n) k_list_own<<<grid_for(n), 256, 0, amgd_s()>>>(list, n, P->split[me], P->split[me + 1], z, oi, ov, cnt);
-  KCHECK();
-  unsigned h = 0;
-  amgd_d2h(&h, cnt, 4);
-  std::vector<uint64_t> c(N, 0);
-  c[me] = h;
-  amgd_pcomm_allgather_u64(c.data(), 1);
-  std::vector<uint64_t> pre(N + 1, 0);
-  for (int p = 0; p < N; p++) pre[p + 1] = pre[p] + c[p];
-  const uint64_t tot = pre[N];
-  uint32_t *ai = (uint32_t *)amgd_alloc(4 * tot + 8);
-  double *av = (double *)amgd_alloc(8 * tot + 8);
-  if (h) {
-    amgd_d2d(ai + pre[me], oi, 4ull * h);
-    amgd_d2d(av + pre[me], ov, 8ull * h);
+// listed rows per owner rank, counted on every rank alike (every rank holds the same list
+// content): the exchange needs no count round of its own
+__global__ void k_owner_hist(const uint32_t *list, uint32_t n, const uint32_t *split, int N,
+                             unsigned long long *cnt) {
+  GRID_STRIDE(r, n) {
+    const uint32_t i = list[r];
+    int lo = 0, hi = N;                       // owner: split[p] <= i < split[p+1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (split[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    atomicAdd(&cnt[lo], 1ull);
   }
-  std::vector<uint64_t> off(2 * (N + 1));
-  for (int p = 0; p <= N; p++) { off[p] = 4 * pre[p]; off[N + 1 + p] = 8 * pre[p]; }
-  void *bufs[2] = {ai, av};
-  amgd_allgatherv(2, bufs, off.data());
-  if (tot) k_list_scatter<<<grid_for(tot), 256, 0, amgd_s()>>>(ai, av, tot, z);
+}
+// Several lists at once (nv vectors, each with its list and partition): one allgatherv of
+// (row, value) pairs for all of them.  The counts come from k_owner_hist on every rank.
+extern "C" void pm_list_sync_n(int nv, double *const *z, const uint32_t *const *list, const uint32_t *n,
+                               const apart *const *P) {
+  const int N = P[0]->N, me = amgd_pcomm_rank();
+  if (N == 1) return;
+  hipStream_t s = amgd_s();
+  std::vector<uint64_t> cnt((size_t)nv * N);
+  {
+    unsigned long long *dc = (unsigned long long *)amgd_alloc(8ull * nv * N + 8);
+    uint32_t *dsp = (uint32_t *)amgd_alloc(4ull * nv * (N + 1) + 4);
+    amgd_memset(dc, 0, 8ull * nv * N);
+    for (int v = 0; v < nv; v++) {
+      amgd_h2d(dsp + (size_t)v * (N + 1), P[v]->split, 4ull * (N + 1));
+      if (n[v]) k_owner_hist<<<grid_for(n[v]), 256, 0, s>>>(list[v], n[v], dsp + (size_t)v * (N + 1), N,
+                                                           dc + (size_t)v * N);
+    }
+    KCHECK();
+    amgd_d2h(cnt.data(), dc, 8ull * nv * N);
+    amgd_free(dc);
+    amgd_free(dsp);
+  }
+  // buffers: per vector (ids, values); rank p's pairs of vector v at pre_v[p]
+  std::vector<void *> bufs(2 * nv);
+  std::vector<uint64_t> off((size_t)2 * nv * (N + 1));
+  std::vector<uint64_t> tot(nv);
+  std::vector<uint32_t *> oi(nv);
+  std::vector<double *> ov(nv);
+  unsigned *c = (unsigned *)amgd_alloc(8ull * nv + 8);
+  amgd_memset(c, 0, 8ull * nv);
+  for (int v = 0; v < nv; v++) {
+    uint64_t t = 0;
+    for (int p = 0; p < N; p++) {
+      off[(size_t)(2 * v) * (N + 1) + p] = 4 * t;
+      off[(size_t)(2 * v + 1) * (N + 1) + p] = 8 * t;
+      t += cnt[(size_t)v * N + p];
+    }
+    off[(size_t)(2 * v) * (N + 1) + N] = 4 * t;
+    off[(size_t)(2 * v + 1) * (N + 1) + N] = 8 * t;
+    tot[v] = t;
+    oi[v] = (uint32_t *)amgd_alloc(4 * t + 8);
+    ov[v] = (double *)amgd_alloc(8 * t + 8);
+    bufs[2 * v] = oi[v];
+    bufs[2 * v + 1] = ov[v];
+    const uint64_t at = off[(size_t)(2 * v) * (N + 1) + me] / 4;
+    if (n[v]) k_list_own<<<grid_for(n[v]), 256, 0, s>>>(list[v], n[v], P[v]->split[me], P[v]->split[me + 1], z[v],
+                                                       oi[v] + at, ov[v] + at, c + v);
+  }
   KCHECK();
-  amgd_free(oi); amgd_free(ov); amgd_free(cnt); amgd_free(ai); amgd_free(av);
+  amgd_allgatherv(2 * nv, bufs.data(), off.data());
+  for (int v = 0; v < nv; v++) {
+    if (tot[v]) k_list_scatter<<<grid_for(tot[v]), 256, 0, s>>>(oi[v], ov[v], tot[v], z[v]);
+    amgd_free(oi[v]);
+    amgd_free(ov[v]);
+  }
+  KCHECK();
+  amgd_free(c);
+}
+extern "C" void pm_list_sync(double *z, const uint32_t *list, uint32_t n, const apart *P) {
+  pm_list_sync_n(1, &z, &list, &n, &P);
+}
+
+// Every rank's `bytes` (device, at mine) and one u64 `user` value to every rank, in rank
+// order.  One collective when every rank's share fits the call site's eager slot: the
+// share travels with its length in a fixed-size record; past it a second, exact round
+// moves the rest, and the site's slot grows to 5/4 of the largest share seen -- the same
+// decision on every rank, since every rank sees every length.
+__global__ void k_eager_hdr(const uint64_t *rec, int N, uint64_t rs8, uint64_t *out) {
+  const int p = threadIdx.x;
+  if (p < N) { out[2 * p] = rec[p * rs8]; out[2 * p + 1] = rec[p * rs8 + 1]; }
+}
+static uint64_t g_eager_gen = 1;
+extern "C" void pm_eager_new_setup(void) { g_eager_gen++; }
+extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes, uint64_t user, uint64_t *len,
+                                  uint64_t *users, uint64_t *total) {
+  // slots adapt within one setup only: a rank's earlier setups must not change its record
+  // size in this one (all ranks start every partitioned setup from the same default)
+  if (e->gen != g_eager_gen) { e->gen = g_eager_gen; e->slot = 0; }
+  const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
+  hipStream_t s = amgd_s();
+  if (N == 1) {
+    char *out = (char *)amgd_alloc(bytes + 8);
+    if (bytes) HIPCK(hipMemcpyAsync(out, mine, bytes, hipMemcpyDeviceToDevice, s));
+    len[0] = bytes; users[0] = user; *total = bytes;
+    return out;
+  }
+  if (e->slot == 0) e->slot = 4096;
+  const uint64_t slot = (e->slot + 7) & ~7ull, rs = 16 + slot;       // record bytes
+  char *rec = (char *)amgd_alloc((uint64_t)N * rs + 8);
+  const uint64_t hdr[2] = {bytes, user};
+  amgd_h2d(rec + (uint64_t)me * rs, hdr, 16);
+  const uint64_t eb = bytes < slot ? bytes : slot;
+  if (eb) HIPCK(hipMemcpyAsync(rec + (uint64_t)me * rs + 16, mine, eb, hipMemcpyDeviceToDevice, s));
+  {
+    std::vector<uint64_t> off(N + 1);
+    for (int p = 0; p <= N; p++) off[p] = (uint64_t)p * rs;
+    void *b = rec;
+    amgd_allgatherv(1, &b, off.data());
+  }
+  std::vector<uint64_t> h(2 * N);
+  {
+    uint64_t *dh = (uint64_t *)amgd_alloc(16ull * N + 8);
+    k_eager_hdr<<<1, 64 * ((N + 63) / 64), 0, s>>>((const uint64_t *)rec, N, rs / 8, dh);
+    KCHECK();
+    amgd_d2h(h.data(), dh, 16ull * N);
+    amgd_free(dh);
+  }
+  std::vector<uint64_t> pre(N + 1, 0);
+  uint64_t mx = 0, over = 0;
+  for (int p = 0; p < N; p++) {
+    len[p] = h[2 * p];
+    users[p] = h[2 * p + 1];
+    pre[p + 1] = pre[p] + len[p];
+    mx = len[p] > mx ? len[p] : mx;
+    over += len[p] > slot ? len[p] - slot : 0;
+  }
+  *total = pre[N];
+  char *out = (char *)amgd_alloc(pre[N] + 8);
+  for (int p = 0; p < N; p++) {
+    const uint64_t c = len[p] < slot ? len[p] : slot;
+    if (c) HIPCK(hipMemcpyAsync(out + pre[p], rec + (uint64_t)p * rs + 16, c, hipMemcpyDeviceToDevice, s));
+  }
+  amgd_free(rec);
+  if (over) {                          // the rest of the long shares, exactly
+    std::vector<uint64_t> ro(N + 1, 0);
+    for (int p = 0; p < N; p++) ro[p + 1] = ro[p] + (len[p] > slot ? len[p] - slot : 0);
+    char *rem = (char *)amgd_alloc(ro[N] + 8);
+    if (bytes > slot)
+      HIPCK(hipMemcpyAsync(rem + ro[me], (const char *)mine + slot, bytes - slot, hipMemcpyDeviceToDevice, s));
+    void *b = rem;
+    amgd_allgatherv(1, &b, ro.data());
+    for (int p = 0; p < N; p++)
+      if (len[p] > slot)
+        HIPCK(hipMemcpyAsync(out + pre[p] + slot, rem + ro[p], len[p] - slot, hipMemcpyDeviceToDevice, s));
+    amgd_free(rem);
+    e->slot = mx + mx / 4;
+  }
+  return out;
 }
 
 // ---------------------------------------------------------------------------
@@ -319,8 +442,12 @@ extern "C" pmat *pm_transpose(const pmat *A) {
     s4[p] = 4 * tro[p]; s8[p] = 8 * tro[p];
     r4[p] = 4 * rpre[p]; r8[p] = 8 * rpre[p];
   }
-  amgd_pcomm_alltoallv(T->col, s4.data(), rcol, r4.data());
-  amgd_pcomm_alltoallv(T->a, s8.data(), ra, r8.data());
+  {                                       // columns and values in one exchange
+    const void *sb[2] = {T->col, T->a};
+    const uint64_t *so2[2] = {s4.data(), s8.data()}, *ro2[2] = {r4.data(), r8.data()};
+    void *rb[2] = {rcol, ra};
+    amgd_pcomm_alltoallv_n(2, sb, so2, rb, ro2);
+  }
   dcsr_free(&T);
   amgd_free(lens);
   // 3. assemble: row j = the pieces of ranks 0..N-1 in order
@@ -501,8 +628,12 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
     const uint64_t at = rb[p] + (p > me ? ownnz : 0);
     s4[p] = 4 * sb[p]; s8[p] = 8 * sb[p]; r4[p] = 4 * at; r8[p] = 8 * at;
   }
-  if (cols) amgd_pcomm_alltoallv(scol, s4.data(), E->col, r4.data());
-  amgd_pcomm_alltoallv(sa, s8.data(), E->a, r8.data());
+  {                                       // values (and columns) in one exchange
+    const void *sb[2] = {sa, scol};
+    const uint64_t *so2[2] = {s8.data(), s4.data()}, *ro2[2] = {r8.data(), r4.data()};
+    void *rb[2] = {E->a, E->col};
+    amgd_pcomm_alltoallv_n(cols ? 2 : 1, sb, so2, rb, ro2);
+  }
   amgd_free(req); amgd_free(rlen); amgd_free(roff); amgd_free(scol); amgd_free(sa);
   // the own rows: one contiguous block of B's arrays into one contiguous block of E's
   if (ownnz) {
@@ -634,36 +765,29 @@ extern "C" void pm_zero_entries(pmat *M, const uint32_t *ri, const uint32_t *cj,
 
 // ordered row sums (from +0, left to right -- amgd_spmv_rows' sums) of the listed rows this
 // rank owns, then every rank gets all of them
-__global__ __launch_bounds__(256) void k_own_rowsum(const uint64_t *ro, const double *a, uint32_t r0,
-                                                    uint32_t r1, const uint32_t *list, uint32_t n, double *out) {
-  __shared__ double buf[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (uint64_t r = (uint64_t)blockIdx.x * 4 + w; r < n; r += (uint64_t)gridDim.x * 4) {
-    const uint32_t gi = list[r];
-    if (gi < r0 || gi >= r1) continue;                      // wave-uniform
-    const uint64_t k0 = ro[gi - r0], k1 = ro[gi - r0 + 1];
-    double t = 0;
-    for (uint64_t c0 = k0; c0 < k1; c0 += 64) {
-      if (c0 + lane < k1) buf[w][lane] = a[c0 + lane];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (lane == 0) {
-        const int m = (int)min((uint64_t)64, k1 - c0);
-        for (int q = 0; q < m; q++) t += buf[w][q];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (lane == 0) out[gi] = t;
+// (the one-GPU kernels on the global-row view: rows of other ranks are empty there and sum
+// to +0, which pm_list_sync then overwrites with their owners' values)
+// rows si of Rl and rows sj of Rt (find_support's re-sums after a selection) in one exchange
+extern "C" void pm_list_rowsum2(const pmat *A, const uint32_t *la, double *oa, const pmat *B, const uint32_t *lb,
+                                double *ob, uint32_t n) {
+  const pmat *M[2] = {A, B};
+  const uint32_t *L[2] = {la, lb};
+  double *O[2] = {oa, ob};
+  for (int q = 0; q < 2 && n; q++) {
+    dcsr g = pm_gview(M[q]);
+    amgd_list_rowsum(&g, L[q], n, O[q], M[q]->m->nnz > 32ull * M[q]->m->rn);
+    pm_gview_free(&g);
   }
+  const uint32_t nn[2] = {n, n};
+  const apart *P[2] = {A->rp, B->rp};
+  pm_list_sync_n(2, O, L, nn, P);
 }
 extern "C" void pm_list_rowsum(const pmat *M, const uint32_t *list, uint32_t n, double *out) {
-  const uint32_t r0 = my_r0(M->rp);
-  if (n) k_own_rowsum<<<(int)std::min<uint64_t>(((uint64_t)n + 3) / 4, 65536), 256, 0, amgd_s()>>>(
-      M->m->ro, M->m->a, r0, r0 + M->m->rn, list, n, out);
-  KCHECK();
+  if (n) {
+    dcsr g = pm_gview(M);
+    amgd_list_rowsum(&g, list, n, out, M->m->nnz > 32ull * M->m->rn);
+    pm_gview_free(&g);
+  }
   pm_list_sync(out, list, n, M->rp);
 }
 

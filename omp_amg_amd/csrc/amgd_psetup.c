@@ -20,11 +20,12 @@
  * is bit-identical to the one-GPU one (tests/test_gpu_partition.py).
  *
  * Not partitioned (each rank computes the whole, identically): the per-sweep vector
- * arithmetic and reductions.  Paths taken in full on every rank instead: interp_lmop's
- * general walk (sp_add lands past the end of a row into the next rows,
- * amg_setup.c:1665-1677 -- gathered operator), the incremental coarsening / find_support
- * sweeps (full sweeps here: the same values, amgd_coarsen.hip), the transposed product
- * forms of the one-GPU driver (direct products here: the same sums).
+ * arithmetic and reductions.  The one-GPU driver's shortcuts run here too, on row blocks:
+ * the incremental coarsening / find_support sweeps (list mode across the ranks), the
+ * transposed product forms X = (B'A')' where A has long columns (p_spgemm_via_t, the
+ * same rule on the global mean rows) and the transposed R chain of the interpolation.
+ * interp_lmop's walks past the end of a row (amg_setup.c:1665-1677) are handled by the
+ * dirty prefix (p_lmop_prefix) and, as a counted fallback, on gathered data.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <math.h>
@@ -79,6 +80,38 @@ static uint64_t all_max(uint64_t v) {
   return s;
 }
 static uint64_t gnnz(const pmat *A) { return all_sum(A->m->nnz); }
+/* the global nnz of two matrices in one exchange */
+static void gnnz2(const pmat *A, const pmat *B, uint64_t *na, uint64_t *nb) {
+  uint64_t *a = (uint64_t *)calloc(2ull * g_N, 8);
+  a[2 * g_me] = A->m->nnz;
+  a[2 * g_me + 1] = B->m->nnz;
+  amgd_pcomm_allgather_u64(a, 2);
+  *na = *nb = 0;
+  for (int p = 0; p < g_N; p++) { *na += a[2 * p]; *nb += a[2 * p + 1]; }
+  free(a);
+}
+
+/* X = A*B, or as X = (B'*A')' where the one-GPU driver takes that form (amgd_setup.c
+   spgemm_via_t: A' has long rows -- mean >= 64 and >= twice B's -- so the transposed
+   product runs on the k-sequential kernels); the rule reads global means, so every rank
+   takes the same form.  Same products in the same k order either way: bit-identical.
+   tr != NULL: the transposed product is returned as it comes (*tr = 1). */
+static pmat *p_spgemm_via_t(const pmat *A, const pmat *At, const pmat *B, const pmat *Bt, int *tr) {
+  int t = 0;
+  if (At && Bt) {
+    uint64_t nat, nb;
+    gnnz2(At, B, &nat, &nb);
+    const uint64_t avg_at = At->rp->n ? nat / At->rp->n : 0, avg_b = B->rp->n ? nb / B->rp->n : 0;
+    t = !(avg_at < 64 || avg_at < 2 * avg_b);
+  }
+  if (tr) *tr = t;
+  if (!t) return pm_spgemm(A, B, 0);
+  pmat *Xt = pm_spgemm(Bt, At, 0);
+  if (tr) return Xt;
+  pmat *X = pm_transpose(Xt);
+  pm_free(&Xt);
+  return X;
+}
 
 /* ------------------------------------------------------------------------ */
 /* coarsen (amg_setup.c:2737): full sweeps, whole vectors                     */
@@ -102,9 +135,9 @@ static pmat *p_strength(const pmat *A) {
    decision everywhere: it reads the union's counts) */
 static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t *cnt_d, uint32_t *stamp,
                      uint32_t base8, uint32_t limit, uint32_t *cum) {
+  static pm_eager eg;                    /* one exchange per hop while the shares fit */
   uint32_t c[8];
-  uint64_t *cn = (uint64_t *)calloc((size_t)g_N, 8), *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
-  uint64_t *off = (uint64_t *)malloc(((size_t)g_N + 1) * 8);
+  uint64_t *len = (uint64_t *)calloc((size_t)g_N, 8), *usr = (uint64_t *)calloc((size_t)g_N, 8);
   int ok = 1;
   for (int r = 1; r <= 6 && ok; r++) {
     amgd_d2h(c, cnt_d, 32);
@@ -113,21 +146,14 @@ static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t 
     if (hi > limit) { ok = 0; break; }
     amgd_cs_hop1(gS, gSt, front, cnt_d, r, stamp, base8, limit);
     amgd_d2h(c, cnt_d, 32);
-    memset(cn, 0, 8ull * g_N);
-    cn[g_me] = c[r];
-    amgd_pcomm_allgather_u64(cn, 1);
-    for (int p = 0; p < g_N; p++) pre[p + 1] = pre[p] + cn[p];
-    if (pre[g_N] == 0) continue;          /* (a global condition: every rank takes part) */
-    uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
-    if (c[r]) amgd_d2d(ids + pre[g_me], front + hi, 4ull * c[r]);
-    for (int p = 0; p <= g_N; p++) off[p] = 4 * pre[p];
-    void *b = ids;
-    amgd_allgatherv(1, &b, off);
-    for (int p = 0; p < g_N; p++)
-      if (p != g_me && cn[p]) amgd_cs_claim_ext(ids + pre[p], cn[p], stamp, base8, r, front, hi, cnt_d + r);
+    uint64_t tot = 0;
+    char *ids = pm_allgather_dyn(&eg, front + hi, 4ull * c[r], c[r], len, usr, &tot);
+    for (int p = 0, at = 0; p < g_N; at += (int)len[p], p++)
+      if (p != g_me && len[p])
+        amgd_cs_claim_ext((const uint32_t *)(ids + at), len[p] / 4, stamp, base8, r, front, hi, cnt_d + r);
     amgd_free(ids);
   }
-  free(cn); free(pre); free(off);
+  free(len); free(usr);
   if (!ok) return 0;
   amgd_d2h(c, cnt_d, 32);
   uint32_t t = 0, cu[7];
@@ -141,10 +167,12 @@ static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t 
 }
 
 /* Incremental sweeps as on one GPU (amgd_coarsen.hip: after the first sweep only the rows
-   within 6 hops of the last sweep's new C points change), always in list mode: every
-   stage runs its list kernel on the global views (the other ranks' rows come out empty)
-   and the owners' values of the listed rows are exchanged (pm_list_sync) -- the same
-   values a full sweep gives, for a fraction of the rows.  AMGD_CS_INC=0: full sweeps. */
+   within 6 hops of the last sweep's new C points change).  Either mode of the one-GPU
+   driver, by its rule (AMGD_CS_LIST_NNZ, on the global nnz): list mode -- every stage runs
+   its list kernel on the global views (the other ranks' rows come out empty) -- or the
+   block filter -- the stage kernels on the own rows, recomputing the 256-row blocks that
+   hold a dirty row.  Then the owners' values of the dirty rows are exchanged
+   (pm_list_sync): the same values a full sweep gives.  AMGD_CS_INC=0: full sweeps. */
 static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
   const uint32_t n = A->rp->n, r0 = A->rp->split[g_me];
   pmat *S = p_strength(A);
@@ -160,7 +188,10 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
   }
   const char *e1 = getenv("AMGD_CS_INC"), *e2 = getenv("AMGD_CS_MIN_ROWS");
   const uint64_t min_rows = e2 && *e2 ? strtoull(e2, NULL, 10) : 65536;
-  const int inc = !(e1 && *e1 && atoi(e1) == 0) && n >= min_rows && gnnz(S) + gnnz(St) <= 64ull * n;
+  const uint64_t nnzS = gnnz(S);
+  const int inc = !(e1 && *e1 && atoi(e1) == 0) && n >= min_rows && nnzS + gnnz(St) <= 64ull * n;
+  const char *e3 = getenv("AMGD_CS_LIST_NNZ");
+  const int list_mode = nnzS <= (uint64_t)(e3 && *e3 ? atoi(e3) : 12) * n;
   const uint32_t limit = n / 4;
   dcsr gS, gSt;
   if (inc) { gS = pm_gview(S); gSt = pm_gview(St); }
@@ -172,18 +203,39 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
   int it = 0, cur = 0;
   for (;;) {
     it++;
-    amgd_csrows rows_, *rows = NULL;
+    amgd_csrows rows_, *rows = NULL, lrows;
     if (inc && it > 1 && p_cs_grow(&gS, &gSt, front[cur], cnt[cur], stamp, 8u * it, limit, rows_.cum)) {
-      rows_.list = front[cur];
+      rows_.list = list_mode ? front[cur] : NULL;
       rows_.fs = stamp;
       rows_.fb = 8u * it;
       rows = &rows_;
+      lrows = rows_;                       /* the block filter on the own rows */
+      lrows.fs = stamp + r0;
       amgd_route_hit(AMGD_R_CS_INC);
     }
-    const uint32_t *L = rows ? rows->list : NULL;
+    const uint32_t *L = front[cur];        /* the dirty rows by hop, in either mode */
 #define PSYNC(v, R) pm_list_sync((v), L, rows->cum[(R)], S->rp)
-    if (rows) {
-      amgd_cs_spmv(&gS, vfd, g, vf, rows, 1);  PSYNC(g, 1);
+    /* Amax (rows within 1 hop) depends on vf alone, fixed during the sweep: it is formed
+       beside g, and both travel in one exchange */
+#define PSYNC2(v1, v2, R)                                                            \
+  do {                                                                               \
+    double *zz_[2] = {(v1), (v2)};                                                   \
+    const uint32_t *ll_[2] = {L, L};                                                 \
+    const uint32_t nn_[2] = {rows->cum[(R)], rows->cum[(R)]};                        \
+    const apart *pp_[2] = {S->rp, S->rp};                                            \
+    pm_list_sync_n(2, zz_, ll_, nn_, pp_);                                           \
+  } while (0)
+    if (rows && !rows->list) {
+      amgd_cs_spmv(S->m, vfd, g + r0, vf + r0, &lrows, 1);
+      amgd_cs_amax(S->m, vf, 0.1, amax + r0, &lrows, 1);
+      PSYNC2(g, amax, 1);
+      amgd_cs_spmv(S->m, g, w1 + r0, vf + r0, &lrows, 2);   PSYNC(w1, 2);
+      amgd_cs_spmv(S->m, w1, w2a + r0, vf + r0, &lrows, 3); PSYNC(w2a, 3);
+      amgd_cs_spmv(S->m, w2a, w2 + r0, vf + r0, &lrows, 4); PSYNC(w2, 4);
+    } else if (rows) {
+      amgd_cs_spmv(&gS, vfd, g, vf, rows, 1);
+      amgd_cs_amax(&gS, vf, 0.1, amax, rows, 1);
+      PSYNC2(g, amax, 1);
       amgd_cs_spmv(&gS, g, w1, vf, rows, 2);   PSYNC(w1, 2);
       amgd_cs_spmv(&gS, w1, w2a, vf, rows, 3); PSYNC(w2a, 3);
       amgd_cs_spmv(&gS, w2a, w2, vf, rows, 4); PSYNC(w2, 4);
@@ -205,8 +257,11 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
       if (verbose()) printf("  coarsen: %d sweeps, norm bound = %f\n", it, b);
       break;
     }
-    if (rows) {
-      amgd_cs_amax(&gS, vf, 0.1, amax, rows, 1);              PSYNC(amax, 1);
+    if (rows && !rows->list) {
+      amgd_cs_gather(St->m, vf + r0, x1, amax, m1 + r0, &lrows, 5);  PSYNC(m1, 5);
+      amgd_cs_mask2(n, g, m1, ma, mb, x2, rows, 5);
+      amgd_cs_gather(St->m, vf + r0, x2, amax, m2 + r0, &lrows, 6);  PSYNC(m2, 6);
+    } else if (rows) {
       amgd_cs_gather(&gSt, vf, x1, amax, m1, rows, 5);        PSYNC(m1, 5);
       amgd_cs_mask2(n, g, m1, ma, mb, x2, rows, 5);
       amgd_cs_gather(&gSt, vf, x2, amax, m2, rows, 6);        PSYNC(m2, 6);
@@ -221,6 +276,7 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
       pm_allgather_vec(m2, 8, St->rp);
     }
 #undef PSYNC
+#undef PSYNC2
     const int nx = cur ^ 1;
     amgd_memset(cnt[nx], 0, 64);
     amgd_cs_mask3(n, m2, mb, vc, vf, vfd, anyvc, front[nx], cnt[nx], stamp, 8u * it + 8, rows, 6);
@@ -563,7 +619,7 @@ static pmat *p_qapply(const pfactor *f, const pmat *Amt, const double *au, const
   return Wt;
 }
 static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, pfactor *fac, const pmat *Amt,
-                             const double *alpha, const double *u, const double *v, double tol) {
+                             const double *alpha, const double *u, const double *v, double tol, pmat **Wt_out) {
   const uint32_t nf = W_skel->rp->n, nc = W_skel->cp->n;
   double *au = dalloc(nc), *zeros = dzeros(nf);
   amgd_vop(au, alpha, u, nc, AMGD_V_MUL);
@@ -576,7 +632,8 @@ static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, p
   p_solve_constraint(lam, W_skel, fac, *W0, alpha, u, v, tol);
   pmat *Wt = p_qapply(fac, Amt, au, lam);
   pmat *W = pm_transpose(Wt);
-  pm_free(&Wt);
+  if (Wt_out) *Wt_out = Wt;
+  else pm_free(&Wt);
   amgd_free(au); amgd_free(zeros);
   ph(PH_W);
   return W;
@@ -587,31 +644,32 @@ static pmat *p_solve_weights(const pmat **W0, double *lam, const pmat *W_skel, p
 typedef struct { const double *rs, *w, *tmp, *w2; } pfs_first;
 static uint32_t p_fs_select(pmat *Rl, pmat *Rt, double *rs, const double *w, double *sumR, double thr,
                             uint32_t *si, uint32_t *sj, uint32_t *nremoved) {
+  static pm_eager eg;
   const uint32_t c0 = Rt->rp->split[g_me], nl = Rt->m->rn;
-  uint32_t *li = (uint32_t *)amgd_alloc(4ull * nl + 8), *lj = (uint32_t *)amgd_alloc(4ull * nl + 8);
+  uint32_t *lb = (uint32_t *)amgd_alloc(12ull * nl + 16);
+  uint32_t *li = lb, *lj = lb + 2ull * nl + 2;         /* li has room for [rows | columns] */
   uint32_t rem = 0;
   const uint32_t h = amgd_fs_select_ex(Rl->m, Rt->m, NULL, rs, w + c0, sumR + c0, thr, li, lj, &rem, c0, 0);
-  uint64_t *cnt = (uint64_t *)calloc(2ull * g_N, 8);
-  cnt[2 * g_me] = h;
-  cnt[2 * g_me + 1] = rem;
-  amgd_pcomm_allgather_u64(cnt, 2);
-  uint64_t *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
-  uint64_t remall = 0;
-  for (int p = 0; p < g_N; p++) { pre[p + 1] = pre[p] + cnt[2 * p]; remall += cnt[2 * p + 1]; }
-  const uint64_t tot = pre[g_N];
-  if (h) { amgd_d2d(si + pre[g_me], li, 4ull * h); amgd_d2d(sj + pre[g_me], lj, 4ull * h); }
-  uint64_t *off = (uint64_t *)malloc(2 * ((size_t)g_N + 1) * 8);
-  for (int p = 0; p <= g_N; p++) { off[p] = 4 * pre[p]; off[g_N + 1 + p] = 4 * pre[p]; }
-  void *bufs[2] = {si, sj};
-  amgd_allgatherv(2, bufs, off);
-  free(off);
-  pm_zero_entries(Rl, si, sj, tot);
-  if (remall) {
-    pm_list_rowsum(Rl, si, (uint32_t)tot, rs);
-    pm_list_rowsum(Rt, sj, (uint32_t)tot, sumR);
+  if (h) amgd_d2d(li + h, lj, 4ull * h);                 /* [rows | columns] of the selections */
+  /* every rank's selections and its "removed" flag in one exchange */
+  uint64_t *len = (uint64_t *)calloc((size_t)g_N, 8), *usr = (uint64_t *)calloc((size_t)g_N, 8), tb = 0;
+  char *all = pm_allgather_dyn(&eg, li, 8ull * h, rem, len, usr, &tb);
+  uint64_t tot = 0, remall = 0, at = 0;
+  for (int p = 0; p < g_N; p++) {
+    const uint64_t hp = len[p] / 8;
+    if (hp) {
+      amgd_d2d(si + tot, all + at, 4 * hp);
+      amgd_d2d(sj + tot, all + at + 4 * hp, 4 * hp);
+    }
+    tot += hp;
+    at += len[p];
+    remall += usr[p];
   }
-  free(cnt); free(pre);
-  amgd_free(li); amgd_free(lj);
+  amgd_free(all);
+  free(len); free(usr);
+  pm_zero_entries(Rl, si, sj, tot);
+  if (remall) pm_list_rowsum2(Rl, si, rs, Rt, sj, sumR, (uint32_t)tot);
+  amgd_free(lb);
   *nremoved = (uint32_t)(remall ? 1 : 0);
   return (uint32_t)tot;
 }
@@ -619,27 +677,20 @@ static uint32_t p_fs_select(pmat *Rl, pmat *Rt, double *rs, const double *w, dou
    the union of the ranks' lists; > cap when any rank's list or the union overflowed */
 static uint32_t p_fs_expand(const dcsr *gM, const uint32_t *list, uint32_t n, uint32_t *stamp, uint32_t tag,
                             uint32_t *out, uint32_t cap) {
+  static pm_eager eg;
   const uint32_t h = amgd_fs_expand(gM, list, n, stamp, tag, out, cap);
-  uint64_t *cn = (uint64_t *)calloc((size_t)g_N, 8), *pre = (uint64_t *)calloc((size_t)g_N + 1, 8);
-  cn[g_me] = h;
-  amgd_pcomm_allgather_u64(cn, 1);
+  uint64_t *len = (uint64_t *)calloc((size_t)g_N, 8), *usr = (uint64_t *)calloc((size_t)g_N, 8), tb = 0;
+  /* an overflowed list (h > cap) is incomplete: only its count travels */
+  char *ids = pm_allgather_dyn(&eg, out, h > cap ? 0 : 4ull * h, h, len, usr, &tb);
   uint32_t res = h;
   int over = 0;
-  for (int p = 0; p < g_N; p++) { pre[p + 1] = pre[p] + cn[p]; if (cn[p] > cap) over = 1; }
+  for (int p = 0; p < g_N; p++) if (usr[p] > cap) over = 1;
   if (over) res = cap + 1;
-  else if (pre[g_N] > 0) {                      /* global condition: every rank takes part */
-    uint32_t *ids = (uint32_t *)amgd_alloc(4 * pre[g_N] + 8);
-    if (h) amgd_d2d(ids + pre[g_me], out, 4ull * h);
-    uint64_t *off = (uint64_t *)malloc(((size_t)g_N + 1) * 8);
-    for (int p = 0; p <= g_N; p++) off[p] = 4 * pre[p];
-    void *b = ids;
-    amgd_allgatherv(1, &b, off);
-    free(off);
-    for (int p = 0; p < g_N; p++)
-      if (p != g_me && cn[p]) res = amgd_fs_claim_ext(ids + pre[p], cn[p], stamp, tag, out, res, cap);
-    amgd_free(ids);
-  }
-  free(cn); free(pre);
+  else
+    for (int p = 0, at = 0; p < g_N; at += (int)len[p], p++)
+      if (p != g_me && len[p]) res = amgd_fs_claim_ext((const uint32_t *)(ids + at), len[p] / 4, stamp, tag, out, res, cap);
+  amgd_free(ids);
+  free(len); free(usr);
   return res;
 }
 
@@ -751,13 +802,22 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
 }
 
 typedef struct {
-  const pmat *Af, *W0, *Ar;
+  const pmat *Af, *AfT, *W0, *W0t, *Ar;
   const double *Dfsqrti, *Dcs;
 } pr0_ctx;
 static pmat *p_r0_rows(const pr0_ctx *c, const uint8_t *bad) {
   pmat *Afb = pm_rows_masked(c->Af, bad);
-  pmat *AfW0 = pm_spgemm(Afb, c->W0, 0);
+  /* (Af on the bad rows)' only where the transposed product will be taken (amgd_setup.c
+     r0_rows: mean row nnz(Afb) / cols(Af) >= 64 and >= twice W0's), by a column mask of Af' */
+  uint64_t nab, nw0;
+  gnnz2(Afb, c->W0, &nab, &nw0);
+  const uint64_t avg_at = c->Af->cp->n ? nab / c->Af->cp->n : 0, avg_b = c->W0->rp->n ? nw0 / c->W0->rp->n : 0;
+  pmat *AfbT = NULL;
+  if (avg_at >= 64 && avg_at >= 2 * avg_b)
+    AfbT = c->AfT ? pm_new(amgd_cols_masked(c->AfT->m, bad), c->AfT->rp, c->AfT->cp) : pm_transpose(Afb);
+  pmat *AfW0 = p_spgemm_via_t(Afb, AfbT, c->W0, c->W0t, NULL);
   pm_free(&Afb);
+  pm_free(&AfbT);
   pmat *Arb = pm_rows_masked(c->Ar, bad);
   pmat *Arhat0 = pm_mpm(1., AfW0, 1., Arb);
   pm_free(&AfW0); pm_free(&Arb);
@@ -806,7 +866,8 @@ static pmat *p_expand_support(const pmat *W_skel, const pmat *R, pmat *Rt, const
 }
 
 
-static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, double gamma2, double tol) {
+static pmat *p_interpolation(const pmat *Af, const pmat *AfT, const pmat *Ac, const pmat *Ar, const pmat *ArT,
+                             double gamma2, double tol) {
   const uint32_t rnf = Af->rp->n, cnc = Ac->rp->n;
   double *Df = dalloc(rnf), *Dfinv = dalloc(rnf);
   pm_diag(Af, Df);
@@ -853,24 +914,48 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
       prevQ = NULL; prevQoff = NULL;
     }
     const pmat *W0;
-    pmat *Wtmp = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol);
+    pmat *Wtmp_t = NULL;
+    pmat *Wtmp = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, tol, &Wtmp_t);
     pk_mark(g_pklvl, PK_WEIGHTS);
-    pmat *AfW = pm_spgemm(Af, Wtmp, 0);
-    pmat *Arhat = pm_mpm(1., AfW, 1., Ar);
-    pm_free(&AfW);
-    ph(PH_AFW);
-    pmat *Arr = pm_mpm(1.0, Arhat, 1.0, Ar);
-    pmat *ArW = pm_mxmpoint(Wtmp, Arr);
-    pm_free(&Arr);
-    pmat *ArWt = pm_transpose(ArW);
-    pm_colsum(ArWt, Dcs);
-    pm_free(&ArW); pm_free(&ArWt);
-    amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
-    amgd_vunary(Dcs, cnc, AMGD_V_INV);
-    amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
-    pmat *R = Arhat;                                     /* |Dfsqrti*Arhat|*Dcsqrti, in place */
-    pm_diag_op2(R, Dfsqrti, Dcs, AMGD_SCALE_ABS);
-    pmat *Rt = pm_transpose(R);
+    /* Arhat = Af*W + Ar, R = |Dfsqrti*Arhat|*Dcs and R' -- in transposed form when Af*W
+       runs as (W'*Af')' (the one-GPU chain, amgd_setup.c interpolation: entry-wise steps
+       on the transposes, only R transposed back) */
+    int trp = 0;
+    pmat *AfWx = p_spgemm_via_t(Af, AfT, Wtmp, Wtmp_t, &trp);
+    pmat *R, *Rt;
+    if (!trp) {
+      pmat *Arhat = pm_mpm(1., AfWx, 1., Ar);
+      pm_free(&AfWx);
+      pm_free(&Wtmp_t);
+      ph(PH_AFW);
+      pmat *Arr = pm_mpm(1.0, Arhat, 1.0, Ar);
+      pmat *ArW = pm_mxmpoint(Wtmp, Arr);
+      pm_free(&Arr);
+      pmat *ArWt = pm_transpose(ArW);
+      pm_colsum(ArWt, Dcs);
+      pm_free(&ArW); pm_free(&ArWt);
+      amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+      amgd_vunary(Dcs, cnc, AMGD_V_INV);
+      amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+      R = Arhat;                                         /* |Dfsqrti*Arhat|*Dcsqrti, in place */
+      pm_diag_op2(R, Dfsqrti, Dcs, AMGD_SCALE_ABS);
+      Rt = pm_transpose(R);
+    } else {
+      pmat *ArhatT = pm_mpm(1., AfWx, 1., ArT);          /* (Af*W + Ar)' */
+      pm_free(&AfWx);
+      ph(PH_AFW);
+      pmat *ArrT = pm_mpm(1.0, ArhatT, 1.0, ArT);
+      pmat *ArWT = pm_mxmpoint(Wtmp_t, ArrT);            /* (W.*Arr)' */
+      pm_free(&ArrT); pm_free(&Wtmp_t);
+      pm_colsum(ArWT, Dcs);                              /* sum(W.*(Arhat+Ar), 1) */
+      pm_free(&ArWT);
+      amgd_vop(Dcs, Dcs, Dc, cnc, AMGD_V_ADD);
+      amgd_vunary(Dcs, cnc, AMGD_V_INV);
+      amgd_vunary(Dcs, cnc, AMGD_V_SQRT);
+      Rt = ArhatT;                                       /* R' = |Dfsqrti*Arhat|*Dcsqrti, transposed */
+      pm_diag_op2(Rt, Dfsqrti, Dcs, AMGD_SCALE_ABS_T);
+      R = pm_transpose(Rt);
+    }
     pm_spmv(R, onesc, rs1, 0., NULL, 1., NULL);
     pm_spmvt(Rt, rs1, w1);
     pm_spmv(R, w1, tmp, 0., NULL, 1., NULL);
@@ -890,7 +975,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
     prev_nnz = wsk;
     if (n == 0 || w1m <= gamma2 || stalled) {
       pm_free(&Rt);
-      W = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16);
+      W = p_solve_weights(&W0, lam, W_skel, &fac, Amt, alpha, uc, v, 1e-16, NULL);
       double *wuc = dalloc(rnf);
       pm_spmv(W, uc, wuc, 0., NULL, 1., NULL);
       dcsr g = pm_gview(W);                              /* the diagonal match reads row ids */
@@ -904,7 +989,7 @@ static pmat *p_interpolation(const pmat *Af, const pmat *Ac, const pmat *Ar, dou
       break;
     }
     amgd_alpha_update(alpha, Dc, w2, cnc);
-    pr0_ctx r0c = {Af, W0, Ar, Dfsqrti, Dcs};
+    pr0_ctx r0c = {Af, AfT, W0, fac.W0t, Ar, Dfsqrti, Dcs};
     const pfs_first f1 = {rs1, w1, tmp, w2};
     pmat *nsk = p_expand_support(W_skel, R, Rt, &r0c, gamma2, &f1);
     pk_mark(g_pklvl, PK_EXPAND);
@@ -954,6 +1039,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
                                                            amgd_phier **out, amgd_stats *st) {
   g_me = amgd_pcomm_rank();
   g_N = amgd_pcomm_size();
+  pm_eager_new_setup();
   g_ub = 0;
   g_pst = st;
   g_plvl = 0;
@@ -1063,20 +1149,24 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
     L->idf = (unsigned long *)amgd_alloc((size_t)rnf * 8 + 8);
     amgd_compact_ids(level == 0 ? h->id : h->lv[level - 1].idc, vc, n, L->idc, L->idf);
     g_pklvl = level;
-    pmat *W = p_interpolation(Af, Ac, Afc, gamma2, itol);
+    /* Af' for the transposed products (where Af's rows are long enough to pay, the one-GPU
+       rule on the global counts) and A(C,F) = Afc' for the interpolation and the RAP */
+    pmat *AfT = Af->rp->n && gnnz(Af) >= 64ull * Af->rp->n ? pm_transpose(Af) : NULL;
+    pmat *Acf = pm_transpose(Afc);
+    pmat *W = p_interpolation(Af, AfT, Ac, Afc, Acf, gamma2, itol);
     L->W = W;
     add_time(&st->t_interp_ms, &t0);
     pk_mark(level, PK_INTERP);
     /* Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) (amg_setup.c:339-372) */
-    pmat *Acf = pm_transpose(Afc);
     amgd_spgemm_set_timer(0);
     pmat *Wt = pm_transpose(W);
-    pmat *AfW = pm_spgemm(Af, W, 0);
+    pmat *AfW = p_spgemm_via_t(Af, AfT, W, Wt, NULL);
     pmat *AfP = pm_mpm(1., AfW, 1., Afc);
     pm_free(&AfW);
     L->AfP = AfP;
     pmat *WtAfP = pm_spgemm(Wt, AfP, 0);
-    pmat *AcfW = pm_spgemm(Acf, W, 0);
+    pmat *AcfW = p_spgemm_via_t(Acf, Afc, W, Wt, NULL);      /* Acf' = Afc exactly */
+    pm_free(&AfT);
     amgd_spgemm_set_timer(-1);
     pmat *Atmp = pm_mpm(1., WtAfP, 1., AcfW);
     A = pm_mpm(1., Atmp, 1, Ac);
@@ -1095,6 +1185,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
   st->t_total_ms = (amgd_wtime() - t_start) * 1e3;
   pk_report(h->nlevels);
   if (g_me == 0) amgd_ph_report(h->nlevels);
+  amgd_comm_site_report();
   st->ub_events = (uint32_t)g_ub;
   st->nlevels = h->nlevels;
   if (verbose() && g_lmop_full)

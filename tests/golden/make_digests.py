@@ -52,7 +52,7 @@ CASES = {
     "p7_128": ("oracle", {"kind": "poisson3d", "m": 128}),
     # the smallest box measured to run the 64-rows-per-wavefront long-row SpMV by default
     # (a >= 2^22-row long-row matrix: level 0's find_support R; tools/route_probe.py)
-    "p7_256x256x136": ("oracle", {"kind": "poisson3d", "m": 136, "mx": 256, "my": 256}),
+    "p7_256x256x192": ("oracle", {"kind": "poisson3d", "m": 192, "mx": 256, "my": 256}),
     "aniso_20": ("oracle", {"kind": "poisson3d", "m": 20, "eps": 1e-3}),
     "aniso_24": ("oracle", {"kind": "poisson3d", "m": 24, "eps": 1e-3}),
     "aniso_32": ("oracle", {"kind": "poisson3d", "m": 32, "eps": 1e-3}),

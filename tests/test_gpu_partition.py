@@ -76,7 +76,7 @@ def test_partitioned_matches_digest(size, case, inc):
     """larger grids: the gathered partitioned hierarchy hashes to the stored oracle /
     reference digest (every array of every level); incremental coarsening / find_support
     sweeps across the ranks (default) and full sweeps"""
-    _run(size, case, timeout=240, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
+    _run(size, case, timeout=170, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
 
 
 @pytest.mark.parametrize("case", ["gold:amgdmp", "gold:p27_8", "digest:p7_48"],

@@ -19,3 +19,13 @@ for mode in one part; do
   tail -n 1 $D/bench_$mode.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$mode', round(d['ms_per_step']), d['phases_ms'])"
 done
 fi
+if [ -n "$SITES" ]; then
+  # collectives per call site of a partitioned setup over the host transport (N ranks, one GPU)
+  AMGD_COMM_SITES=1 AMGD_PHASES=1 timeout -k 10 600 python3 -u tools/part_peak.py $SITES $D/part_peak.json > $D/part_peak.log 2>&1 || { tail -20 $D/part_peak.log; exit 1; }
+  python3 -c "
+import json; d=json.load(open('$D/part_peak.json'))
+print('bit_identical', d['bit_identical'], 'peak ratio', round(d['max_rank_peak_over_one_gpu'],3), 'secs', [round(r['secs'],1) for r in d['partitioned']], 'calls', [r['comm_calls'] for r in d['partitioned']])
+for l in d['partitioned'][0]['phase_peaks']:
+    if 'site' in l or 'collectives' in l or 'exchanges' in l: print(l)
+"
+fi
