@@ -2246,9 +2246,29 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     if (tro[c + 1] - tro[c] > maxlen) continue;      // k_fs_select_long
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
-    for (uint64_t q = tro[c] + sub; q < tro[c + 1]; q += G) {
-      double x = ta[q] * rs[trow[q]];
-      if (x > mx) { mx = x; best = q; }
+    // U entries per lane per step: their (row, value) loads, then their rs gathers, are in
+    // flight together (round 4 walked one dependent row -> rs chain at a time); a position
+    // past the column's end loads the last entry and is left out of the compare.  The
+    // lane's positions are compared in ascending order, so the first maximum still wins.
+    constexpr int U = 8;
+    const uint64_t qb = tro[c], qe = tro[c + 1];
+    for (uint64_t q0 = qb + sub; q0 < qe; q0 += (uint64_t)G * U) {
+      uint32_t tr[U];
+      double tv[U], rv[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = min(q0 + (uint64_t)u * G, qe - 1);
+        tr[u] = trow[q];
+        tv[u] = ta[q];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) rv[u] = rs[tr[u]];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = q0 + (uint64_t)u * G;
+        const double x = tv[u] * rv[u];
+        if (q < qe && x > mx) { mx = x; best = q; }
+      }
     }
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) {

@@ -482,7 +482,13 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
     return 0;
   } else if (dend > 0) {              // dirty prefix [0, dend): opens every sum it touches
     g_lmop_stats[2]++;
-    amgd_lmop_general(S, Wt, Q, qoff, u, 0, dend);
+    // the walk on the supports of [0, dend) only: a row-prefix view of Wt, so the general
+    // walk's per-support set-up (offsets, row of entry, host copies) is O(dend), not O(nc)
+    // -- the partitioned driver's form (p_lmop_prefix), 0.3-0.4 s faster at 256^3
+    dcsr wv = *Wt;
+    wv.rn = dend;
+    amgd_d2h(&wv.nnz, Wt->ro + dend, 8);
+    amgd_lmop_general(S, &wv, Q, qoff, u, 0, dend);
   }
   // S rows binned by length: thread / wave with a 1024-wide window / 256 threads with
   // 4096-wide windows.  Multi-GPU: S rows are independent, so each rank pulls the rows of

@@ -192,8 +192,9 @@ extern "C" void pm_list_sync(double *z, const uint32_t *list, uint32_t n, const 
 // Every rank's `bytes` (device, at mine) and one u64 `user` value to every rank, in rank
 // order.  One collective when every rank's share fits the call site's eager slot: the
 // share travels with its length in a fixed-size record; past it a second, exact round
-// moves the rest, and the site's slot grows to 5/4 of the largest share seen -- the same
-// decision on every rank, since every rank sees every length.
+// moves the rest.  After every call the site's slot is set to 5/4 of that call's largest
+// share, within [4 KB, 64 KB] -- the same decision on every rank, since every rank sees
+// every length; the cap keeps a record exchange latency-sized (N x 64 KB at most).
 __global__ void k_eager_hdr(const uint64_t *rec, int N, uint64_t rs8, uint64_t *out) {
   const int p = threadIdx.x;
   if (p < N) { out[2 * p] = rec[p * rs8]; out[2 * p + 1] = rec[p * rs8 + 1]; }
@@ -262,7 +263,10 @@ extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes,
       if (len[p] > slot)
         HIPCK(hipMemcpyAsync(out + pre[p] + slot, rem + ro[p], len[p] - slot, hipMemcpyDeviceToDevice, s));
     amgd_free(rem);
-    e->slot = mx + mx / 4;
+  }
+  {
+    uint64_t ns = mx + mx / 4;
+    e->slot = ns < 4096 ? 4096 : ns > 65536 ? 65536 : ns;
   }
   return out;
 }

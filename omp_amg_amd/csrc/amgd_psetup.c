@@ -240,7 +240,17 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
       amgd_cs_spmv(&gS, w1, w2a, vf, rows, 3); PSYNC(w2a, 3);
       amgd_cs_spmv(&gS, w2a, w2, vf, rows, 4); PSYNC(w2, 4);
     } else {
-      pm_spmv(S, vfd, g, 0.0, NULL, 1.0, vf);           /* g   = vf.*(S*vf)  */
+      /* g = vf.*(S*vf) and Amax (vf alone: formed here, used after the bound test) in one
+         exchange of their row segments */
+      amgd_spmv(S->m, vfd, g + r0, 0.0, NULL, 1.0, vf + r0);
+      amgd_mat_amax(S->m, vf, 0.1, amax + r0);
+      {
+        void *b2[2] = {g, amax};
+        uint64_t *o2 = (uint64_t *)malloc(2 * ((size_t)g_N + 1) * 8);
+        for (int p = 0; p <= g_N; p++) o2[p] = o2[g_N + 1 + p] = 8ull * S->rp->split[p];
+        if (g_N > 1) amgd_allgatherv(2, b2, o2);
+        free(o2);
+      }
       pm_spmv(S, g, w1, 0.0, NULL, 1.0, vf);            /* w1  = vf.*(S*g)   */
       pm_spmv(S, w1, w2a, 0.0, NULL, 1.0, vf);          /* w2a = vf.*(S*w1)  */
       pm_spmv(S, w2a, w2, 0.0, NULL, 1.0, vf);          /* w2  = vf.*(S*w2a) */
@@ -266,9 +276,7 @@ static void p_coarsen(const pmat *A, uint8_t *vc, double ctol) {
       amgd_cs_mask2(n, g, m1, ma, mb, x2, rows, 5);
       amgd_cs_gather(&gSt, vf, x2, amax, m2, rows, 6);        PSYNC(m2, 6);
     } else {
-      /* Amax rows: local, then whole (the gather reads Amax of any row of S) */
-      amgd_mat_amax(S->m, vf, 0.1, amax + r0);
-      pm_allgather_vec(amax, 8, S->rp);
+      /* (Amax: whole since the first exchange of the sweep) */
       amgd_mat_max_gather(St->m, vf + r0, x1, amax, m1 + r0);
       pm_allgather_vec(m1, 8, St->rp);
       amgd_cs_mask2(n, g, m1, ma, mb, x2, NULL, 5);

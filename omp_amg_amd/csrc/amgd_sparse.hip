@@ -643,7 +643,17 @@ extern "C" void amgd_spmv_set_sl_min(int64_t n) { g_sl_forced = n < 0 ? -1 : n; 
 // loads of round r+2 are in flight.  Every row is summed left to right from +0: the
 // reference's row sum.  LIST: the rows are list[0..n) instead of 0..n (rows longer
 // than maxlen are left to k_rows_exact).
-template <bool LIST, int RW, int PER = 16>
+//
+// Round 5: every load is unconditional and straight-line.  Round 4's loads sat behind
+// per-lane bounds branches and a uniform "last round" branch, so the load counts between
+// the waits were not static and the compiler waited for ALL outstanding loads
+// (s_waitcnt vmcnt(0)) before the products of every round -- the two rounds meant to be
+// in flight drained to one.  Now a lane past its row's end loads a valid dummy entry
+// (index 0: the kernel only runs on matrices with entries) and its product is dropped by
+// a per-round bit mask applied when the product is formed, after the data arrived; the
+// same entries enter the same ordered sums.  HASX: products with x (x == nullptr:
+// ordered row sums) as a template parameter, so no load sits behind a runtime branch.
+template <bool LIST, int RW, int PER = 16, bool HASX = true>
 __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, uint32_t n,
                                                    const uint32_t *list, const double *x,
@@ -651,6 +661,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
                                                    double beta, const uint8_t *f,
                                                    uint32_t maxlen = 0xffffffffu) {
   constexpr int SEG = 64 * PER / RW;
+  static_assert(PER <= 32, "k_spmv_pipe: the round mask holds PER bits");
   __shared__ double buf[4][RW][SEG + 1];
   __shared__ uint64_t rk0[4][RW];
   __shared__ uint32_t rlen[4][RW];
@@ -673,46 +684,48 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (value, column) of round `off`: lane L's q-th entry is flat entry q*64 + L
-    auto ld = [&](uint32_t off, double *av, uint32_t *cv) {
+    // (value, column) of round `off`: lane L's q-th entry is flat entry q*64 + L; a lane
+    // past its row's end loads entry 0 and clears its bit of the round mask
+    auto ld = [&](uint32_t off, double *av, uint32_t *cv) -> uint32_t {
+      uint32_t m = 0;
 #pragma unroll
       for (int q = 0; q < PER; q++) {
         const int fl = q * 64 + lane, rr = fl / SEG, sub = fl % SEG;
         const uint32_t en = off + sub;
-        av[q] = 0.0;
-        cv[q] = 0;
-        if (en < rlen[w][rr]) {
-          const uint64_t k = rk0[w][rr] + en;
-          av[q] = a[k];
-          if (x) cv[q] = col[k];
-        }
+        const bool ok = en < rlen[w][rr];
+        const uint64_t k = ok ? rk0[w][rr] + en : 0;
+        m |= ok ? 1u << q : 0u;
+        av[q] = a[k];
+        if (HASX) cv[q] = col[k];
       }
+      return m;
     };
     double a0[PER], g0[PER], a1[PER];
     uint32_t c0[PER], c1[PER];
-    ld(0, a0, c0);
+    const uint32_t m0i = ld(0, a0, c0);
+    if (HASX) {
 #pragma unroll
-    for (int q = 0; q < PER; q++) g0[q] = x ? x[c0[q]] : 0.0;
-    ld(SEG, a1, c1);
+      for (int q = 0; q < PER; q++) g0[q] = x[c0[q]];
+    }
+    uint32_t m0 = m0i, m1 = ld(SEG, a1, c1);
     double t = 0;
     for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
       for (int q = 0; q < PER; q++) {
         const int fl = q * 64 + lane;
-        buf[w][fl / SEG][fl % SEG] = x ? a0[q] * g0[q] : a0[q];
+        const double pr = HASX ? a0[q] * g0[q] : a0[q];
+        buf[w][fl / SEG][fl % SEG] = (m0 >> q) & 1u ? pr : 0.0;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       double g1[PER], a2[PER];
       uint32_t c2[PER];
+      if (HASX) {
 #pragma unroll
-      for (int q = 0; q < PER; q++) g1[q] = x ? x[c1[q]] : 0.0;   // round off + SEG
-      if (off + 2 * SEG < mx) ld(off + 2 * SEG, a2, c2);           // round off + 2 SEG
-      else {
-#pragma unroll
-        for (int q = 0; q < PER; q++) { a2[q] = 0.0; c2[q] = 0; }
+        for (int q = 0; q < PER; q++) g1[q] = x[c1[q]];              // round off + SEG
       }
+      const uint32_t m2 = ld(off + 2 * SEG, a2, c2);                 // round off + 2 SEG
       if (lane < RW && off < len) {
         const uint32_t m = min((uint32_t)SEG, len - off);
         if (m == SEG) {
@@ -733,7 +746,12 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-      for (int q = 0; q < PER; q++) { a0[q] = a1[q]; g0[q] = g1[q]; a1[q] = a2[q]; c1[q] = c2[q]; }
+      for (int q = 0; q < PER; q++) {
+        a0[q] = a1[q]; a1[q] = a2[q];
+        if (HASX) { g0[q] = g1[q]; c1[q] = c2[q]; }
+      }
+      m0 = m1;
+      m1 = m2;
     }
     if (own && (!LIST || ro[i + 1] - ro[i] <= maxlen)) {
       double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
@@ -766,15 +784,27 @@ static int lane_rw(uint64_t n) {
     amgd_route_hit(AMGD_R_SPMV_PIPE);                                                         \
     amgd_route_hit(rw_ == 64 ? AMGD_R_MV_RW64 : rw_ == 16 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);   \
     const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
-    if (rw_ == 64)                                                                            \
-      k_spmv_pipe<LIST, 64><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,     \
-                                                       z_, al, y_, be, f_, ml_);              \
-    else if (rw_ == 16)                                                                       \
-      k_spmv_pipe<LIST, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,     \
-                                                       z_, al, y_, be, f_, ml_);              \
-    else                                                                                      \
-      k_spmv_pipe<LIST, 4, 8><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,   \
-                                                         z_, al, y_, be, f_, ml_);            \
+    if ((x_) != nullptr) {                                                                    \
+      if (rw_ == 64)                                                                          \
+        k_spmv_pipe<LIST, 64, 16, true><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,     \
+                                                 list_, x_, z_, al, y_, be, f_, ml_);           \
+      else if (rw_ == 16)                                                                     \
+        k_spmv_pipe<LIST, 16, 16, true><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,     \
+                                                 list_, x_, z_, al, y_, be, f_, ml_);           \
+      else                                                                                    \
+        k_spmv_pipe<LIST, 4, 8, true><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,       \
+                                                list_, x_, z_, al, y_, be, f_, ml_);            \
+    } else {                                                                                  \
+      if (rw_ == 64)                                                                          \
+        k_spmv_pipe<LIST, 64, 16, false><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,    \
+                                                  list_, x_, z_, al, y_, be, f_, ml_);          \
+      else if (rw_ == 16)                                                                     \
+        k_spmv_pipe<LIST, 16, 16, false><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,    \
+                                                  list_, x_, z_, al, y_, be, f_, ml_);          \
+      else                                                                                    \
+        k_spmv_pipe<LIST, 4, 8, false><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,      \
+                                                 list_, x_, z_, al, y_, be, f_, ml_);           \
+    }                                                                                         \
   } while (0)
 // ordered sums (x == nullptr) or products of the listed rows only (rows longer than
 // maxlen are skipped: k_rows_exact does them)

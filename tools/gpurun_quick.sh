@@ -1,13 +1,16 @@
-# one GPU call: the GPU suite (optionally a -k filter) + a short bench line on the same tree
-# usage: bash tools/gpurun_quick.sh <tag>   (KSEL=... pytest -k filter; NOBENCH=1)
+# one GPU call: a pytest subset, then a short 256^3 bench (one-GPU driver) with its line
+# usage: bash tools/gpurun_quick.sh <tag> <steps> <pytest args...>
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-TAG=${1:-r04}
+TAG=${1:-quick}; STEPS=${2:-3}; shift 2
 D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 rm -rf $D; mkdir -p $D
 export PYTHONPATH=$GRAFT_REPO_ROOT
-timeout -k 10 ${TLIM:-900} python3 -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 150 --timeout-method thread ${KSEL:+-k "$KSEL"} > $D/gputests.log 2>&1 || { tail -40 $D/gputests.log; exit 1; }
-tail -3 $D/gputests.log
-[ -n "$NOBENCH" ] && exit 0
-timeout -k 10 300 python3 bench.py --gpus 1 --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline > $D/bench.json 2> $D/bench.err || { echo bench failed; tail -20 $D/bench.err; exit 1; }
-cat $D/bench.json
+if [ $# -gt 0 ]; then
+timeout -k 10 900 python3 -u -m pytest "$@" -x -q --timeout 300 --timeout-method thread > $D/tests.log 2>&1 || { grep -E "PASS|FAIL|Error|error|assert" $D/tests.log | tail -30; exit 1; }
+tail -1 $D/tests.log
+fi
+timeout -k 10 600 python3 bench.py --steps $STEPS --warmup 1 --no-cpu-baseline > $D/bench.json 2> $D/bench.err || { tail -20 $D/bench.err; exit 1; }
+tail -n 1 $D/bench.json | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']
+print('ms', round(d['ms_per_step']), 'frac', round(r['frac'],3), 'mv_ms', round(r['kernel_ms_per_setup']), {k: (round(v['ms_per_setup']), round(v['achieved_gbs'] or 0)) for k, v in r['by_shape'].items()}, 'rap_ms', round(d['rap_roofline']['kernel_ms_per_setup']), d['phases_ms'])"
