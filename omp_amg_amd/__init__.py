@@ -115,7 +115,6 @@ def lib() -> C.CDLL:
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
-        L.amgd_test_sg_hash.argtypes = [C.c_int, C.c_int]
         L.amgd_comm_rccl_uid.argtypes = [C.c_char_p]
         L.amgd_comm_rccl_uid.restype = C.c_int
         L.amgd_comm_init_rccl.argtypes = [C.c_int, C.c_int, C.c_char_p]
@@ -424,17 +423,6 @@ def lmop_small(n: int) -> None:
     """interp_lmop row pull: S rows of <= 32 entries one thread each (n > 0) or on the
     wavefront kernel (0); -1: back to the env (AMGD_LMOP_SMALL)"""
     lib().amgd_test_lmop_small(int(n))
-
-
-def sg_hash(mode: int) -> None:
-    """LDS hash slots of the SpGEMM row kernels: 0 multiplicative hash (default), 1 bank-aware
-    (low bits kept per 32-column block), -1 environment (AMGD_SG_HASH).  Same sums."""
-    lib().amgd_test_sg_hash(int(mode), -1)
-
-
-def ww_swizzle(on: int) -> None:
-    """windowed SpGEMM accumulator swizzle: 1 on (default), 0 off, -1 environment (AMGD_WW_SWZ)"""
-    lib().amgd_test_sg_hash(-1, int(on))
 
 
 def spgemm_flat(on: bool) -> None:

@@ -1547,38 +1547,7 @@ __global__ void k_bin_rows(const uint64_t *v, uint32_t rn, SgBins b, int nb, int
   }
 }
 
-// Slot of column j in a 2^lg-slot LDS hash.  Mode 0: multiplicative (Knuth) hash of j.
-// Mode 1 (AMGD_SG_HASH=1, an A/B switch): the slot's low 5 bits are j's low 5 bits XOR
-// bits 5-9 and 10-14, the rest a multiplicative hash of j >> 5 -- the 16 / 32 lanes of
-// one chunk (consecutive sorted columns of one B row: runs plus grid strides) then land on
-// distinct LDS banks instead of on random ones.  Any slot map gives the same sums (each
-// column's additions stay in layer order), so the mode is a performance choice only.
-__constant__ int c_sg_hash_mode = 0;
-__device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) {
-  if (c_sg_hash_mode && lg >= 6) {
-    const uint32_t lo = (j ^ (j >> 5) ^ (j >> 10)) & 31u;
-    const uint32_t hi = ((j >> 5) * 2654435761u) >> (32 - (lg - 5));
-    return (hi << 5) | lo;
-  }
-  return (j * 2654435761u) >> (32 - lg);
-}
-__constant__ int c_ww_swz = 1;       // k_sg_wwin window swizzle (AMGD_WW_SWZ=0: off, A/B)
-static int g_sg_hash_set = 0;
-static void sg_hash_mode_init() {
-  if (g_sg_hash_set) return;
-  g_sg_hash_set = 1;
-  const char *e = getenv("AMGD_SG_HASH"), *e2 = getenv("AMGD_WW_SWZ");
-  const int m = e && *e ? atoi(e) : 0, w = e2 && *e2 ? atoi(e2) : 1;
-  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(c_sg_hash_mode), &m, sizeof m));
-  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(c_ww_swz), &w, sizeof w));
-}
-// tests / A/B: hash mode and window swizzle (-1: back to the environment)
-extern "C" void amgd_spgemm_set_hash(int hash, int swz) {
-  g_sg_hash_set = 0;
-  sg_hash_mode_init();
-  if (hash >= 0) HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(c_sg_hash_mode), &hash, sizeof hash));
-  if (swz >= 0) HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(c_ww_swz), &swz, sizeof swz));
-}
+__device__ __forceinline__ uint32_t sg_hash(uint32_t j, int lg) { return (j * 2654435761u) >> (32 - lg); }
 
 // Emit a finished row from the LDS hash: occupied nonzero slots are compacted to
 // the front (order kept), bitonic-sorted by column and written at xro[i].
@@ -2181,13 +2150,6 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 __device__ __forceinline__ double rld(double v, int l) {
   return __longlong_as_double((long long)rl64((uint64_t)__double_as_longlong(v), l));
 }
-// Window slot of window index x: the low 4 bits XORed with bits 4-7 and 8-11.  A layer's
-// 16 / 32 lanes (ds_write_b64 / ds_read_b64 bank groups, double slot x on bank pair x mod 16
-// / 32) hold consecutive B-row columns: runs of neighbours separated by the grid's line and
-// plane strides, which on the power-of-two coarse grids are multiples of 16 -- unswizzled,
-// every such stride lands on the same bank (round 4: 44 % of the window kernel's LDS cycles
-// were bank conflicts).  A bijection on [0, W): emission reads slots in window order.
-__device__ __forceinline__ uint32_t ww_swz(uint32_t x) { return c_ww_swz ? x ^ (((x >> 4) ^ (x >> 8)) & 15u) : x; }
 template <int W, int MODE, int RAP = 0>
 __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t nrows,
                                                  const uint64_t *aro, const uint32_t *acol,
@@ -2293,13 +2255,13 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
           uint32_t cu = rl32(lcur, e);
           for (;;) {
             const bool in = col <= we;                 // a prefix of the lanes (sorted row)
-            if (in) {
-              if (NUM) {
-                double *p = acc + ww_swz(col - wb);
+            if (NUM) {
+              if (in) {
+                double *p = acc + (col - wb);
                 *p = *p + val * av;
-              } else {
-                atomicOr(&mp32[(col - wb) >> 5], 1u << ((col - wb) & 31));
               }
+            } else if (in) {
+              atomicOr(&mp32[(col - wb) >> 5], 1u << ((col - wb) & 31));
             }
             const uint32_t n = (uint32_t)__popcll(__ballot(in));
             if (n < 64) {
@@ -2325,7 +2287,7 @@ __global__ __launch_bounds__(256) void k_sg_wwin(const uint32_t *rows, uint32_t 
       }
       if (NUM) {                                      // emit in column order
         for (int q = 0; q < W; q += 64) {
-          const double v = acc[ww_swz((uint32_t)(q + lane))];
+          const double v = acc[q + lane];
           const bool nz = v != 0.0;
           const uint64_t bm = __ballot(nz);
           if (nz) {
@@ -2416,7 +2378,6 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     abort();
   }
   hipStream_t s = amgd_s();
-  sg_hash_mode_init();
   static int sglog = -1;
   if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
   double t_start = 0;

@@ -206,10 +206,7 @@ API void amgd_test_qf_reuse_stats(uint64_t *out) {
 /* cap on live device bytes (0: none): the out-of-HBM path without filling 288 GB */
 API void amgd_test_hbm_cap(uint64_t bytes) { amgd_set_hbm_cap((size_t)bytes); }
 API uint64_t amgd_test_pool_inuse(void) { return amgd_pool_bytes_in_use(); }
-/* SpGEMM LDS layout: hash mode (0 multiplicative, 1 bank-aware) and the windowed kernel's
-   swizzle (0 / 1); -1 leaves one as the environment sets it.  Same sums either way. */
-void amgd_spgemm_set_hash(int hash, int swz);
-API void amgd_test_sg_hash(int hash, int swz) { amgd_spgemm_set_hash(hash, swz); }
+
 /* one bare partitioned-mode collective (the collective guard's tests): kind 0 an allgatherv
    of `bytes` per rank, 1 an alltoallv of `bytes` to every peer (expecting `expect` bytes
    from each); returns 0 */

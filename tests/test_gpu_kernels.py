@@ -193,42 +193,6 @@ def test_spgemm_wave_windows(case, win):
     assert refops.same(X, R)
 
 
-@pytest.mark.parametrize("hash_mode,swz", [(1, 1), (0, 0), (1, 0)])
-@pytest.mark.parametrize("win", [0, 1024])
-@pytest.mark.parametrize("case", ["banded", "dups_cancel", "strided"])
-def test_spgemm_lds_layouts(case, win, hash_mode, swz):
-    """the LDS layouts of the SpGEMM row kernels are performance choices only: the
-    bank-aware hash (slot low bits = column low bits mixed with bits 5-14) and the
-    windowed kernel's XOR swizzle, on and off, give mxm's sums bit for bit -- in the hash
-    kernels (win 0) and the wave-private windows (win 1024); 'strided' B rows hold
-    power-of-two column strides (the coarse grids' line / plane strides)"""
-    rng = np.random.default_rng({"banded": 81, "dups_cancel": 82, "strided": 83}[case])
-    if case == "banded":
-        A, B = _banded(rng, 211, 400, 6000, 60, 0.7, 150, 3000, ints=False)
-    elif case == "dups_cancel":
-        A, B = _banded(rng, 157, 300, 5000, 50, 0.8, 160, 2500, dups=True)
-    else:
-        kn, cn = 300, 8192
-        ro, cols, vals = [0], [], []
-        for k in range(kn):
-            base = int(rng.integers(0, 4096))
-            c = sorted({(base + dx + 32 * dy + 256 * dz) % cn for dx in (-1, 0, 1) for dy in range(-3, 4)
-                        for dz in range(-4, 5)})
-            cols += c; vals += rng.integers(-3, 4, size=len(c)).astype(float).tolist(); ro.append(len(cols))
-        B = refops.Csr(kn, cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
-        A = refops.rand_csr(rng, 150, kn, 0.1, ints=True)
-    R = refops.spgemm(A, B)
-    oa.spgemm_flat(False)
-    oa.spgemm_win(win)
-    oa.lib().amgd_test_sg_hash(hash_mode, swz)
-    try:
-        X = oa.test_csr_op(0, A, B)
-    finally:
-        oa.spgemm_win(-1)
-        oa.lib().amgd_test_sg_hash(-1, -1)
-    assert refops.same(X, R)
-
-
 @pytest.mark.parametrize("case", ["short", "long_b", "wide", "tiny", "nonpositive"])
 def test_spgemm_pattern(case):
     """amgd_spgemm_pattern (the constraint operator's pattern W_skel * W_skel'): operands
