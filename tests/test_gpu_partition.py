@@ -79,12 +79,14 @@ def test_partitioned_matches_digest(size, case, inc):
     _run(size, case, timeout=170, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
 
 
-@pytest.mark.parametrize("case", ["gold:amgdmp", "gold:p27_8", "digest:p7_48"],
+@pytest.mark.parametrize("case", ["gold:amgdmp", "gold:p27_8", "digest:p7_48", "digest:p27_20"],
                          ids=lambda v: v.split(":")[1])
 def test_partitioned_eight_ranks(case):
     """8 ranks -- the north_star's GPU count -- on small fixtures (coarse levels leave
-    ranks with no rows: empty blocks, empty halos, empty segments in every exchange) and
-    on the 7-point 48^3 digest (110 k rows, 13.8 k per rank)"""
+    ranks with no rows: empty blocks, empty halos, empty segments in every exchange), on
+    the 7-point 48^3 digest (110 k rows, 13.8 k per rank) and on the 27-point 20^3 digest
+    (configs[3]'s stencil: the densified levels, interp_lmop's dirty points past clean
+    ones -- the reference-checked hierarchy)"""
     _run(8, case, timeout=240)
 
 
