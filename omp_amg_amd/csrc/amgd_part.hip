@@ -193,8 +193,10 @@ extern "C" void pm_list_sync(double *z, const uint32_t *list, uint32_t n, const 
 // order.  One collective when every rank's share fits the call site's eager slot: the
 // share travels with its length in a fixed-size record; past it a second, exact round
 // moves the rest.  After every call the site's slot is set to 5/4 of that call's largest
-// share, within [4 KB, 64 KB] -- the same decision on every rank, since every rank sees
-// every length; the cap keeps a record exchange latency-sized (N x 64 KB at most).
+// share, within [4 KB, 1 MB] -- the same decision on every rank, since every rank sees
+// every length; callers keep one state per recurring exchange (a BFS hop, an expansion
+// step), whose share is like the previous sweep's.  N x 1 MB at most per record exchange
+// (~20 us over xGMI at N = 8: comparable to the latency of the round it saves).
 __global__ void k_eager_hdr(const uint64_t *rec, int N, uint64_t rs8, uint64_t *out) {
   const int p = threadIdx.x;
   if (p < N) { out[2 * p] = rec[p * rs8]; out[2 * p + 1] = rec[p * rs8 + 1]; }
@@ -266,7 +268,7 @@ extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes,
   }
   {
     uint64_t ns = mx + mx / 4;
-    e->slot = ns < 4096 ? 4096 : ns > 65536 ? 65536 : ns;
+    e->slot = ns < 4096 ? 4096 : ns > (1u << 20) ? (1u << 20) : ns;
   }
   return out;
 }

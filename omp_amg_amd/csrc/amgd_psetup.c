@@ -135,7 +135,9 @@ static pmat *p_strength(const pmat *A) {
    decision everywhere: it reads the union's counts) */
 static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t *cnt_d, uint32_t *stamp,
                      uint32_t base8, uint32_t limit, uint32_t *cum) {
-  static pm_eager eg;                    /* one exchange per hop while the shares fit */
+  /* one exchange per hop while the shares fit; one slot state per hop, since a hop's share
+     is like the same hop's of the previous sweep (the front grows hop by hop within one) */
+  static pm_eager eg[7];
   uint32_t c[8];
   uint64_t *len = (uint64_t *)calloc((size_t)g_N, 8), *usr = (uint64_t *)calloc((size_t)g_N, 8);
   int ok = 1;
@@ -147,7 +149,7 @@ static int p_cs_grow(const dcsr *gS, const dcsr *gSt, uint32_t *front, uint32_t 
     amgd_cs_hop1(gS, gSt, front, cnt_d, r, stamp, base8, limit);
     amgd_d2h(c, cnt_d, 32);
     uint64_t tot = 0;
-    char *ids = pm_allgather_dyn(&eg, front + hi, 4ull * c[r], c[r], len, usr, &tot);
+    char *ids = pm_allgather_dyn(&eg[r], front + hi, 4ull * c[r], c[r], len, usr, &tot);
     for (int p = 0, at = 0; p < g_N; at += (int)len[p], p++)
       if (p != g_me && len[p])
         amgd_cs_claim_ext((const uint32_t *)(ids + at), len[p] / 4, stamp, base8, r, front, hi, cnt_d + r);
@@ -684,12 +686,11 @@ static uint32_t p_fs_select(pmat *Rl, pmat *Rt, double *rs, const double *w, dou
 /* amgd_fs_expand across the ranks: the own listed rows' neighbours (global view), then
    the union of the ranks' lists; > cap when any rank's list or the union overflowed */
 static uint32_t p_fs_expand(const dcsr *gM, const uint32_t *list, uint32_t n, uint32_t *stamp, uint32_t tag,
-                            uint32_t *out, uint32_t cap) {
-  static pm_eager eg;
+                            uint32_t *out, uint32_t cap, pm_eager *eg) {
   const uint32_t h = amgd_fs_expand(gM, list, n, stamp, tag, out, cap);
   uint64_t *len = (uint64_t *)calloc((size_t)g_N, 8), *usr = (uint64_t *)calloc((size_t)g_N, 8), tb = 0;
   /* an overflowed list (h > cap) is incomplete: only its count travels */
-  char *ids = pm_allgather_dyn(&eg, out, h > cap ? 0 : 4ull * h, h, len, usr, &tb);
+  char *ids = pm_allgather_dyn(eg, out, h > cap ? 0 : 4ull * h, h, len, usr, &tb);
   uint32_t res = h;
   int over = 0;
   for (int p = 0; p < g_N; p++) if (usr[p] > cap) over = 1;
@@ -744,11 +745,12 @@ static pmat *p_find_support(const pmat *R, pmat *Rt, double goal, const pfs_firs
     it++;
     int done = 0;
     if (fs_inc && it > 1 && prev_nsel <= cap_c) {
-      const uint32_t n1 = p_fs_expand(&gRl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c);
+      static pm_eager egx[3];          /* the three expansions' own slot states */
+      const uint32_t n1 = p_fs_expand(&gRl, si + prev_off, prev_nsel, st_c, ++tag, L1, cap_c, &egx[0]);
       if (n1 <= cap_c) {
-        const uint32_t n2 = p_fs_expand(&gRt, L1, n1, st_r, ++tag, L2, cap_r);
+        const uint32_t n2 = p_fs_expand(&gRt, L1, n1, st_r, ++tag, L2, cap_r, &egx[1]);
         if (n2 <= cap_r) {
-          const uint32_t n3 = p_fs_expand(&gRl, L2, n2, st_c, ++tag, L3, cap_c);
+          const uint32_t n3 = p_fs_expand(&gRl, L2, n2, st_c, ++tag, L3, cap_c, &egx[2]);
           if (n3 <= cap_c) {
             amgd_spmv_rows(&gRt, L1, n1, rs, w);           /* w  on C1 */
             pm_list_sync(w, L1, n1, Rt->rp);
