@@ -112,6 +112,7 @@ def lib() -> C.CDLL:
         L.amgd_test_mv_long.argtypes = [C.c_int64]
         L.amgd_test_fs_long.argtypes = [C.c_int64]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
+        L.amgd_test_spmv_pair.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -290,6 +291,12 @@ def spmv_rw(rw: int) -> None:
     lib().amgd_test_spmv_rw(int(rw))
 
 
+def spmv_pair(on: int) -> None:
+    """products with x through the paired-load lane kernel k_spmv_pair (1), the
+    single-load k_spmv_pipe (0), or as AMGD_MV_PAIR says (-1).  Same sums either way."""
+    lib().amgd_test_spmv_pair(int(on))
+
+
 def test_build(Ai, Aj, Av) -> abi.Csr:
     init()
     Ai = np.ascontiguousarray(Ai, dtype=np.uint32)
@@ -367,7 +374,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024")
+          "qf_t512", "qf_t1024", "mv_pair")
 
 
 def route_stats(reset: bool = True) -> dict:

@@ -760,6 +760,192 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
     }
   }
 }
+// k_spmv_pipe with paired loads (products with x only): lane L's p-th load covers the two
+// consecutive entries 2 (p 64 + L) and 2 (p 64 + L) + 1 of the round, one 16 B value load
+// and one 8 B column load for both -- two thirds of the memory instructions of k_spmv_pipe
+// per entry.  For the pairs to be aligned a row is walked from the even offset k0 & ~1:
+// when its first entry sits at an odd offset, the leading slot holds a masked product
+// (+0) that enters the row's sum before its first product, which leaves the reference's
+// ordered sum unchanged ((+0) + p == p for every p, -0 included).  A slot past a row's
+// end, or the masked leading slot, gathers x[0] (its column may be another row's or the
+// allocation's padding).  Needs a 16 B aligned value array and an 8 B aligned column
+// array (the launcher checks: arena blocks are 256 B aligned; views fall back).
+// Depths (rounds ahead of the round whose products are formed): CA for the columns, GA
+// for the x gathers (issued when a round's columns have arrived, CA - GA rounds after
+// them), VA for the values (VA == CA: loaded with the columns; else on their own, the
+// pair index recomputed).  Default CA 2, GA 1, VA 2.
+template <bool LIST, int RW, int PER, int CA, int GA, int VA>
+__device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_t *col,
+                                               const double *a, uint32_t n,
+                                               const uint32_t *list, const double *x,
+                                               double *z, double alpha, const double *y,
+                                               double beta, const uint8_t *f, uint32_t maxlen) {
+  constexpr int SEG = 64 * PER / RW, PH = PER / 2, NC = CA - GA;
+  static_assert(PER <= 32 && PER % 2 == 0 && SEG % 2 == 0, "k_spmv_pair: round shape");
+  static_assert(GA >= 1 && NC >= 1 && VA >= 1 && VA <= CA, "k_spmv_pair: depths");
+  __shared__ double buf[4][RW][SEG + 1];
+  __shared__ uint64_t rk0[4][RW];
+  __shared__ uint32_t rlen[4][RW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double2 *a2p = reinterpret_cast<const double2 *>(a);
+  const uint2 *c2p = reinterpret_cast<const uint2 *>(col);
+  for (uint64_t rb = ((uint64_t)blockIdx.x * 4 + w) * RW; rb < n;
+       rb += (uint64_t)gridDim.x * 4 * RW) {
+    const uint64_t r = rb + lane;
+    const bool own = lane < RW && r < n;
+    const uint32_t i = own ? (LIST ? list[r] : (uint32_t)r) : 0u;
+    uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    if (LIST && k1 - k0 > maxlen) k1 = k0;
+    const uint32_t lead = k1 > k0 ? (uint32_t)(k0 & 1) : 0u;
+    const uint32_t vlen = (uint32_t)(k1 - k0) + lead;     // slots from the even start
+    if (lane < RW) {
+      rk0[w][lane] = (k0 - lead) >> 1;                    // in pairs
+      rlen[w][lane] = vlen | lead << 31;
+    }
+    uint32_t mx = vlen;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // pair index of lane's p-th pair of round `off` (0 past the row's end) and its two
+    // mask bits (first slot: a real entry, not the masked leading slot; second: in the row)
+    auto pk = [&](uint32_t off, int p, uint32_t &m) -> uint64_t {
+      const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+      const uint32_t en = off + sub, info = rlen[w][rr], vl = info & 0x7fffffffu;
+      const bool any = en < vl;
+      m |= (any && en >= (info >> 31) ? 1u : 0u) << (2 * p);
+      m |= (en + 1 < vl ? 1u : 0u) << (2 * p + 1);
+      return any ? rk0[w][rr] + (en >> 1) : 0;
+    };
+    // columns (and, VA == CA, values) of round `off`; its mask
+    auto ldc = [&](uint32_t off, double *av, uint32_t *cv) -> uint32_t {
+      uint32_t m = 0;
+#pragma unroll
+      for (int p = 0; p < PH; p++) {
+        const uint64_t k = pk(off, p, m);
+        if (VA == CA) {
+          const double2 v = a2p[k];
+          av[2 * p] = v.x; av[2 * p + 1] = v.y;
+        }
+        const uint2 c = c2p[k];
+        cv[2 * p] = c.x; cv[2 * p + 1] = c.y;
+      }
+      return m;
+    };
+    auto lda = [&](uint32_t off, double *av) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int p = 0; p < PH; p++) {
+        const double2 v = a2p[pk(off, p, m)];
+        av[2 * p] = v.x; av[2 * p + 1] = v.y;
+      }
+    };
+    auto gat = [&](const uint32_t *cv, uint32_t m, double *gv) {
+#pragma unroll
+      for (int q = 0; q < PER; q++) gv[q] = x[(m >> q) & 1u ? cv[q] : 0u];
+    };
+    // ring state at the top of round r: va[j] values of round r + j (j < VA), gv[j] gathers
+    // of round r + j (j < GA), cq[j] columns of round r + GA + j (j < NC), ms[j] the mask of
+    // round r + j (j < CA)
+    double va[VA][PER], gv[GA][PER];
+    uint32_t cq[NC][PER], ms[CA];
+    {
+      double vt[PER];
+      uint32_t ct[PER];
+#pragma unroll
+      for (int j = 0; j < CA; j++) {
+        if (j < GA) {
+          ms[j] = ldc(j * SEG, j < VA ? va[j] : vt, ct);
+          gat(ct, ms[j], gv[j]);
+        } else {
+          ms[j] = ldc(j * SEG, j < VA ? va[j] : vt, cq[j - GA]);
+        }
+        if (VA < CA && j < VA) lda(j * SEG, va[j]);
+      }
+    }
+    double t = 0;
+    for (uint32_t off = 0; off < mx; off += SEG) {
+#pragma unroll
+      for (int p = 0; p < PH; p++) {
+        const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+        buf[w][rr][sub] = (ms[0] >> (2 * p)) & 1u ? va[0][2 * p] * gv[0][2 * p] : 0.0;
+        buf[w][rr][sub + 1] = (ms[0] >> (2 * p + 1)) & 1u ? va[0][2 * p + 1] * gv[0][2 * p + 1] : 0.0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // shift the rings down one round, then fill the new last slots
+#pragma unroll
+      for (int j = 0; j + 1 < VA; j++)
+#pragma unroll
+        for (int q = 0; q < PER; q++) va[j][q] = va[j + 1][q];
+#pragma unroll
+      for (int j = 0; j + 1 < GA; j++)
+#pragma unroll
+        for (int q = 0; q < PER; q++) gv[j][q] = gv[j + 1][q];
+#pragma unroll
+      for (int j = 0; j + 1 < CA; j++) ms[j] = ms[j + 1];
+      gat(cq[0], ms[GA - 1], gv[GA - 1]);                     // round off + GA SEG
+#pragma unroll
+      for (int j = 0; j + 1 < NC; j++)
+#pragma unroll
+        for (int q = 0; q < PER; q++) cq[j][q] = cq[j + 1][q];
+      if (VA < CA) lda(off + VA * SEG, va[VA - 1]);           // round off + VA SEG
+      ms[CA - 1] = ldc(off + CA * SEG, va[VA - 1], cq[NC - 1]);   // round off + CA SEG
+      if (lane < RW && off < vlen) {
+        const uint32_t m = min((uint32_t)SEG, vlen - off);
+        if (m == SEG) {
+          constexpr int U = SEG < (VA < CA ? 8 : 16) ? SEG : (VA < CA ? 8 : 16);
+#pragma unroll
+          for (int e0 = 0; e0 < SEG; e0 += U) {
+            double u[U];
+#pragma unroll
+            for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
+#pragma unroll
+            for (int e = 0; e < U; e++) t += u[e];
+          }
+        } else {
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (own && (!LIST || ro[i + 1] - ro[i] <= maxlen)) {
+      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) v = v * (f[i] ? 1.0 : 0.0);
+      z[i] = v;
+    }
+  }
+}
+template <bool LIST, int RW, int PER, int CA = 2, int GA = 1, int VA = 2>
+__global__ __launch_bounds__(256) void k_spmv_pair(const uint64_t *ro, const uint32_t *col,
+                                                   const double *a, uint32_t n,
+                                                   const uint32_t *list, const double *x,
+                                                   double *z, double alpha, const double *y,
+                                                   double beta, const uint8_t *f,
+                                                   uint32_t maxlen = 0xffffffffu) {
+  spmv_pair_body<LIST, RW, PER, CA, GA, VA>(ro, col, a, n, list, x, z, alpha, y, beta, f, maxlen);
+}
+// (A/B) the same at >= 3 wavefronts per SIMD
+template <bool LIST, int RW, int PER, int CA, int GA, int VA>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void k_spmv_pair_w3(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t n,
+                    const uint32_t *list, const double *x, double *z, double alpha,
+                    const double *y, double beta, const uint8_t *f, uint32_t maxlen = 0xffffffffu) {
+  spmv_pair_body<LIST, RW, PER, CA, GA, VA>(ro, col, a, n, list, x, z, alpha, y, beta, f, maxlen);
+}
+// Products with x take k_spmv_pair by default (round 5: long-row SpMV 5.02 -> 4.88 s per
+// 256^3 setup, profiles/r05/pair_*); AMGD_MV_PAIR / amgd_spmv_set_pair (tests, A/B): 0
+// k_spmv_pipe, 2..4 other depths
+static int g_mv_pair = -1;
+extern "C" void amgd_spmv_set_pair(int on) { g_mv_pair = on < 0 ? -1 : on; }
+static bool mv_pair(const dcsr *M) {
+  if (g_mv_pair == -1) g_mv_pair = (int)sl_env("AMGD_MV_PAIR", 1);
+  return g_mv_pair > 0 && ((uintptr_t)M->a & 15) == 0 && ((uintptr_t)M->col & 7) == 0;
+}
 // rows per wavefront of the lane kernel for n rows (>= ~2048 wavefronts in flight)
 static int64_t g_rw_forced = -2;     // AMGD_SL_RW / amgd_spmv_set_rw (tests): 4, 16 or 64
 extern "C" void amgd_spmv_set_rw(int rw) { g_rw_forced = rw < 0 ? -2 : rw; }
@@ -778,13 +964,33 @@ static int lane_rw(uint64_t n) {
 // everywhere RW=4 measured slower, profiles/r04/ab_spmv_per).  The round-2
 // lane kernel, the contiguous-chunk kernel, nontemporal loads and the fused selection /
 // column-sum variants measured slower and were removed in round 4.
+#define PAIR_LAUNCH(K, LIST, CA, GA, VA, n_, list_, x_, z_, al, y_, be, f_, ml_)                \
+  do {                                                                                        \
+    if (rw_ == 64)                                                                            \
+      K<LIST, 64, 16, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,    \
+                                                       x_, z_, al, y_, be, f_, ml_);          \
+    else if (rw_ == 16)                                                                       \
+      K<LIST, 16, 16, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,    \
+                                                       x_, z_, al, y_, be, f_, ml_);          \
+    else                                                                                      \
+      K<LIST, 4, 8, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,      \
+                                                     x_, z_, al, y_, be, f_, ml_);            \
+  } while (0)
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     const int rw_ = lane_rw(n_);                                                              \
     amgd_route_hit(AMGD_R_SPMV_PIPE);                                                         \
     amgd_route_hit(rw_ == 64 ? AMGD_R_MV_RW64 : rw_ == 16 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);   \
     const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
-    if ((x_) != nullptr) {                                                                    \
+    if ((x_) != nullptr && mv_pair(M)) {                                                      \
+      amgd_route_hit(AMGD_R_MV_PAIR);                                                         \
+      switch (g_mv_pair) {                                                                    \
+        case 2: PAIR_LAUNCH(k_spmv_pair_w3, LIST, 2, 1, 1, n_, list_, x_, z_, al, y_, be, f_, ml_); break; \
+        case 3: PAIR_LAUNCH(k_spmv_pair, LIST, 3, 2, 1, n_, list_, x_, z_, al, y_, be, f_, ml_); break;    \
+        case 4: PAIR_LAUNCH(k_spmv_pair, LIST, 3, 2, 2, n_, list_, x_, z_, al, y_, be, f_, ml_); break;    \
+        default: PAIR_LAUNCH(k_spmv_pair, LIST, 2, 1, 2, n_, list_, x_, z_, al, y_, be, f_, ml_); break;   \
+      }                                                                                       \
+    } else if ((x_) != nullptr) {                                                             \
       if (rw_ == 64)                                                                          \
         k_spmv_pipe<LIST, 64, 16, true><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,     \
                                                  list_, x_, z_, al, y_, be, f_, ml_);           \

@@ -239,6 +239,8 @@ extern void amgd_qapply_set_huge(int n);
 API void amgd_test_qa_huge(int n) { amgd_qapply_set_huge(n); }
 extern void amgd_spmv_set_rw(int rw);
 API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
+extern void amgd_spmv_set_pair(int on);
+API void amgd_test_spmv_pair(int on) { amgd_spmv_set_pair(on); }
 extern void amgd_qfactor_set_coop_lds(int m);
 API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }
 /* huge supports factored per connected component (1, default) or whole (0); -1: env */
