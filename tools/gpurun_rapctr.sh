@@ -10,7 +10,7 @@ D=$GRAFT_REPO_ROOT/gpurun_out/rapctr_$TAG
 rm -rf $D; mkdir -p $D
 export PYTHONPATH=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-RX=${RX:-'k_sg_(row|kseq)<[0-9]+, [0-9]+, 1, 1>|k_sg_wwin<|k_spgemm_long<1, 1>|k_spmv_pipe<false'}
+RX=${RX:-'k_sg_(row|kseq)<[0-9]+, [0-9]+, 1, 1>|k_sg_wwin<|k_spgemm_long<1, 1>|k_spmv_(pipe|pair)<false'}
 i=0
 for G in "TCC_HIT_sum TCC_MISS_sum" \
          "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES" \

@@ -29,7 +29,7 @@ fk, fn = counter(f"{d0}/calib_FETCH_SIZE", "FETCH_SIZE")
 wk, wn = counter(f"{d0}/calib_WRITE_SIZE", "WRITE_SIZE")
 f_fetch = cal["read_bytes_per_product"] / (fk * 1024 / fn)
 f_write = cal["write_bytes_per_product"] / (wk * 1024 / wn)
-names = {"spmv": "k_spmv_pipe<false,RW,PER> (roofline kernel)",
+names = {"spmv": "k_spmv_pair<false,RW,PER,...> + k_spmv_pipe<false,RW,PER,false> (roofline kernels)",
          "rap": "RAP SpGEMM numeric kernels (rap_roofline)"}
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per pass (tools/gpurun_pmc.sh), "
                  f"one 256^3 setup (tools/probe_scale.py 256), tree of {tag}",
