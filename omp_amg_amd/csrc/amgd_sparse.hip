@@ -773,7 +773,7 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
 // Depths (rounds ahead of the round whose products are formed): CA for the columns, GA
 // for the x gathers (issued when a round's columns have arrived, CA - GA rounds after
 // them), VA for the values (VA == CA: loaded with the columns; else on their own, the
-// pair index recomputed).  Default CA 2, GA 1, VA 2.
+// pair index recomputed).  CA 2, GA 1, VA 2 (other depths measured slower).
 template <bool LIST, int RW, int PER, int CA, int GA, int VA>
 __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_t *col,
                                                const double *a, uint32_t n,
@@ -808,10 +808,17 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // row and slot of lane's p-th pair in a round: 64 consecutive pairs per load (a row's
+    // segment, 128 B and more per row)
+    auto slot = [&](int p, int &rr, int &sub) {
+      const int fl = 2 * (p * 64 + lane);
+      rr = fl / SEG; sub = fl % SEG;
+    };
     // pair index of lane's p-th pair of round `off` (0 past the row's end) and its two
     // mask bits (first slot: a real entry, not the masked leading slot; second: in the row)
     auto pk = [&](uint32_t off, int p, uint32_t &m) -> uint64_t {
-      const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+      int rr, sub;
+      slot(p, rr, sub);
       const uint32_t en = off + sub, info = rlen[w][rr], vl = info & 0x7fffffffu;
       const bool any = en < vl;
       m |= (any && en >= (info >> 31) ? 1u : 0u) << (2 * p);
@@ -868,7 +875,8 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
     for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
       for (int p = 0; p < PH; p++) {
-        const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+        int rr, sub;
+        slot(p, rr, sub);
         buf[w][rr][sub] = (ms[0] >> (2 * p)) & 1u ? va[0][2 * p] * gv[0][2 * p] : 0.0;
         buf[w][rr][sub + 1] = (ms[0] >> (2 * p + 1)) & 1u ? va[0][2 * p + 1] * gv[0][2 * p + 1] : 0.0;
       }
@@ -929,17 +937,14 @@ __global__ __launch_bounds__(256) void k_spmv_pair(const uint64_t *ro, const uin
                                                    uint32_t maxlen = 0xffffffffu) {
   spmv_pair_body<LIST, RW, PER, CA, GA, VA>(ro, col, a, n, list, x, z, alpha, y, beta, f, maxlen);
 }
-// (A/B) the same at >= 3 wavefronts per SIMD
-template <bool LIST, int RW, int PER, int CA, int GA, int VA>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-void k_spmv_pair_w3(const uint64_t *ro, const uint32_t *col, const double *a, uint32_t n,
-                    const uint32_t *list, const double *x, double *z, double alpha,
-                    const double *y, double beta, const uint8_t *f, uint32_t maxlen = 0xffffffffu) {
-  spmv_pair_body<LIST, RW, PER, CA, GA, VA>(ro, col, a, n, list, x, z, alpha, y, beta, f, maxlen);
-}
 // Products with x take k_spmv_pair by default (round 5: long-row SpMV 5.02 -> 4.88 s per
-// 256^3 setup, profiles/r05/pair_*); AMGD_MV_PAIR / amgd_spmv_set_pair (tests, A/B): 0
-// k_spmv_pipe, 2..4 other depths
+// 256^3 setup, profiles/r05/pair/); AMGD_MV_PAIR=0 / amgd_spmv_set_pair(0) (tests, A/B):
+// k_spmv_pipe.  Measured and dropped (profiles/r05/pair/): values one round ahead at 3
+// wavefronts per SIMD (4.94 s), gathers two rounds ahead (5.01 / 5.08 s), 8 / 16 rows
+// side by side in each load instead of one row's segment (5.51 / 5.98 s).  The lane
+// kernels are bound by texture-address work: TA busy 87-96 % of the kernel's cycles, one
+// TA cycle per distinct cache line, ~53 distinct lines per 64-lane x gather
+// (profiles/r05/mvctr/)
 static int g_mv_pair = -1;
 extern "C" void amgd_spmv_set_pair(int on) { g_mv_pair = on < 0 ? -1 : on; }
 static bool mv_pair(const dcsr *M) {
@@ -964,17 +969,17 @@ static int lane_rw(uint64_t n) {
 // everywhere RW=4 measured slower, profiles/r04/ab_spmv_per).  The round-2
 // lane kernel, the contiguous-chunk kernel, nontemporal loads and the fused selection /
 // column-sum variants measured slower and were removed in round 4.
-#define PAIR_LAUNCH(K, LIST, CA, GA, VA, n_, list_, x_, z_, al, y_, be, f_, ml_)                \
+#define PAIR_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
     if (rw_ == 64)                                                                            \
-      K<LIST, 64, 16, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,    \
-                                                       x_, z_, al, y_, be, f_, ml_);          \
+      k_spmv_pair<LIST, 64, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
+                                                    z_, al, y_, be, f_, ml_);                 \
     else if (rw_ == 16)                                                                       \
-      K<LIST, 16, 16, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,    \
-                                                       x_, z_, al, y_, be, f_, ml_);          \
+      k_spmv_pair<LIST, 16, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,  \
+                                                    z_, al, y_, be, f_, ml_);                 \
     else                                                                                      \
-      K<LIST, 4, 8, CA, GA, VA><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_,      \
-                                                     x_, z_, al, y_, be, f_, ml_);            \
+      k_spmv_pair<LIST, 4, 8><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_, list_, x_,    \
+                                                  z_, al, y_, be, f_, ml_);                   \
   } while (0)
 #define LANE_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_)                             \
   do {                                                                                        \
@@ -984,12 +989,7 @@ static int lane_rw(uint64_t n) {
     const int gp_ = (int)std::min<uint64_t>(((uint64_t)(n_) + 4 * rw_ - 1) / (4 * rw_), 65536); \
     if ((x_) != nullptr && mv_pair(M)) {                                                      \
       amgd_route_hit(AMGD_R_MV_PAIR);                                                         \
-      switch (g_mv_pair) {                                                                    \
-        case 2: PAIR_LAUNCH(k_spmv_pair_w3, LIST, 2, 1, 1, n_, list_, x_, z_, al, y_, be, f_, ml_); break; \
-        case 3: PAIR_LAUNCH(k_spmv_pair, LIST, 3, 2, 1, n_, list_, x_, z_, al, y_, be, f_, ml_); break;    \
-        case 4: PAIR_LAUNCH(k_spmv_pair, LIST, 3, 2, 2, n_, list_, x_, z_, al, y_, be, f_, ml_); break;    \
-        default: PAIR_LAUNCH(k_spmv_pair, LIST, 2, 1, 2, n_, list_, x_, z_, al, y_, be, f_, ml_); break;   \
-      }                                                                                       \
+      PAIR_LAUNCH(LIST, n_, list_, x_, z_, al, y_, be, f_, ml_);                               \
     } else if ((x_) != nullptr) {                                                             \
       if (rw_ == 64)                                                                          \
         k_spmv_pipe<LIST, 64, 16, true><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, n_,     \

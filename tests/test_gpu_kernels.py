@@ -380,13 +380,11 @@ def rw(request):
     oa.spmv_rw(-1)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["pipe", "pair", "pair_w3", "pair_g2v1", "pair_g2v2"])
+@pytest.fixture(params=[0, 1], ids=["pipe", "pair"])
 def chunk(request):
     """whole-matrix long-row products: per-row segments with the gather one round ahead
     (k_spmv_pipe, whole-matrix and listed rows); "pair": products with x through
-    k_spmv_pair (two entries per 16 B load, rows walked from an even offset); 2..4: its
-    other depths (values one round ahead at 3 wavefronts per SIMD; gathers two rounds
-    ahead, values one / two)"""
+    k_spmv_pair (two entries per 16 B load, rows walked from an even offset)"""
     oa.spmv_pair(request.param)
     yield request.param
     oa.spmv_pair(-1)
