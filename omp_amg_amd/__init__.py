@@ -113,6 +113,7 @@ def lib() -> C.CDLL:
         L.amgd_test_fs_long.argtypes = [C.c_int64]
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_spmv_pair.argtypes = [C.c_int]
+        L.amgd_test_spmv_rw_bounds.argtypes = [C.c_int, C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -289,6 +290,13 @@ def spmv_rw(rw: int) -> None:
     """rows per wavefront of the lane-per-row SpMV kernel: 4, 16 or 64 (-1: by row count).
     Same sums either way."""
     lib().amgd_test_spmv_rw(int(rw))
+
+
+def spmv_rw_bounds(code: int) -> None:
+    """row-count bounds of the lane SpMV's 16 / 64-row shapes as lo * 100 + hi (log2 of
+    the row counts, e.g. 1622 = 2^16 / 2^22, the default; -1: default).  A/B only."""
+    code = int(code)
+    lib().amgd_test_spmv_rw_bounds(code // 100 if code > 0 else 0, code % 100 if code > 0 else 0)
 
 
 def spmv_pair(on: int) -> None:

@@ -954,10 +954,16 @@ static bool mv_pair(const dcsr *M) {
 // rows per wavefront of the lane kernel for n rows (>= ~2048 wavefronts in flight)
 static int64_t g_rw_forced = -2;     // AMGD_SL_RW / amgd_spmv_set_rw (tests): 4, 16 or 64
 extern "C" void amgd_spmv_set_rw(int rw) { g_rw_forced = rw < 0 ? -2 : rw; }
+// row-count bounds of the 16 / 64-row shapes (log2; amgd_spmv_set_rw_bounds: A/B)
+static int g_rw_lo = 16, g_rw_hi = 22;
+extern "C" void amgd_spmv_set_rw_bounds(int lo, int hi) {
+  g_rw_lo = lo > 0 ? lo : 16;
+  g_rw_hi = hi > 0 ? hi : 22;
+}
 static int lane_rw(uint64_t n) {
   if (g_rw_forced == -2) g_rw_forced = sl_env("AMGD_SL_RW", 0);
   if (g_rw_forced == 4 || g_rw_forced == 16 || g_rw_forced == 64) return (int)g_rw_forced;
-  return n >= (1u << 22) ? 64 : n >= (1u << 16) ? 16 : 4;
+  return n >= (1ull << g_rw_hi) ? 64 : n >= (1ull << g_rw_lo) ? 16 : 4;
 }
 // Long-row products: k_spmv_pipe, 16 entries per lane per round (round 3: 256^3 SpMV
 // 6.26 -> 5.46 s against the round-2 lane kernel; 8 per lane 5.64 s, 4: 6.98 s, 12:

@@ -240,6 +240,8 @@ API void amgd_test_qa_huge(int n) { amgd_qapply_set_huge(n); }
 extern void amgd_spmv_set_rw(int rw);
 API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_spmv_set_pair(int on);
+extern void amgd_spmv_set_rw_bounds(int lo, int hi);
+API void amgd_test_spmv_rw_bounds(int lo, int hi) { amgd_spmv_set_rw_bounds(lo, hi); }
 API void amgd_test_spmv_pair(int on) { amgd_spmv_set_pair(on); }
 extern void amgd_qfactor_set_coop_lds(int m);
 API void amgd_test_qf_coop_lds(int m) { amgd_qfactor_set_coop_lds(m); }

@@ -7,5 +7,5 @@ TAG=$1; shift
 D=gpurun_out/ab_$TAG
 mkdir -p $D
 export PYTHONPATH=$PWD
-timeout -k 10 900 python3 tools/ab_setup.py 256 --no-digest "$@" > $D/ab256.txt 2> $D/ab256.err || { tail -5 $D/ab256.err; cat $D/ab256.txt; exit 1; }
+timeout -k 10 1000 python3 tools/ab_setup.py 256 --no-digest "$@" > $D/ab256.txt 2> $D/ab256.err || { tail -5 $D/ab256.err; cat $D/ab256.txt; exit 1; }
 cat $D/ab256.txt
