@@ -114,6 +114,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spmv_rw.argtypes = [C.c_int]
         L.amgd_test_spmv_pair.argtypes = [C.c_int]
         L.amgd_test_spmv_rw_bounds.argtypes = [C.c_int, C.c_int]
+        L.amgd_test_d2h_poll.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -297,6 +298,12 @@ def spmv_rw_bounds(code: int) -> None:
     the row counts, e.g. 1622 = 2^16 / 2^22, the default; -1: default).  A/B only."""
     code = int(code)
     lib().amgd_test_spmv_rw_bounds(code // 100 if code > 0 else 0, code % 100 if code > 0 else 0)
+
+
+def d2h_poll(on: int) -> None:
+    """small readbacks polled from host-coherent memory (1, default) or blocking copies
+    (0); -1 back to the default.  A/B only: same results."""
+    lib().amgd_test_d2h_poll(int(on))
 
 
 def spmv_pair(on: int) -> None:

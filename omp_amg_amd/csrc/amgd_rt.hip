@@ -268,7 +268,69 @@ extern "C" void amgd_h2d(void *d, const void *h, size_t n) {
   if (n) HIPCK(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, amgd_s()));
   HIPCK(hipStreamSynchronize(g_stream));
 }
+// Small readbacks (counts, scalars, flags: ~15 k per 256^3 setup) skip the runtime's
+// copy + stream synchronisation: a one-wavefront kernel, ordered after all earlier work
+// on the stream, stores the bytes and then a sequence number into host-coherent memory,
+// and the host polls the sequence number.  A blocking hipMemcpyAsync + hipStreamSynchronize
+// left the GPU idle ~28 us per readback (the copy's own launch, the completion signal,
+// the host's wake-up); a polled store cuts that gap.  After ~0.5 s of polling the host
+// falls back to hipStreamSynchronize, which reports a device fault as before.
+// AMGD_D2H_POLL=0: the blocking copy for every readback.
+#define PUB_MAX 256
+static uint8_t *g_pub = nullptr;                 // [0, 8): sequence; [64, 64 + PUB_MAX): data
+static uint64_t g_pub_seq = 0;
+static int g_pub_on = -1;
+__global__ void k_publish(const uint8_t *src, uint32_t n, uint8_t *dst, unsigned long long *flag,
+                          unsigned long long seq) {
+  for (uint32_t i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+  __threadfence_system();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static bool pub_ready() {
+  if (g_pub_on < 0) {
+    const char *e = getenv("AMGD_D2H_POLL");
+    g_pub_on = !(e && *e == '0');
+    if (g_pub_on) {
+      void *p = nullptr;
+      if (hipHostMalloc(&p, 64 + PUB_MAX, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        g_pub_on = 0;
+      } else {
+        g_pub = (uint8_t *)p;
+        memset(g_pub, 0, 64 + PUB_MAX);
+      }
+    }
+  }
+  return g_pub_on > 0;
+}
+// (A/B, tests) 0: blocking copies, 1: polled, -1: as AMGD_D2H_POLL says
+extern "C" void amgd_set_d2h_poll(int on) {
+  if (on == 0) { if (g_pub_on < 0) pub_ready(); if (g_pub_on > 0) g_pub_on = 2; return; }
+  if (g_pub_on == 2) g_pub_on = 1;
+  (void)on;
+}
 extern "C" void amgd_d2h(void *h, const void *d, size_t n) {
+  if (n && n <= PUB_MAX && pub_ready() && g_pub_on == 1) {
+    const unsigned long long seq = ++g_pub_seq;
+    k_publish<<<1, 64, 0, amgd_s()>>>((const uint8_t *)d, (uint32_t)n, g_pub + 64,
+                                      (unsigned long long *)g_pub, seq);
+    HIPCK(hipGetLastError());
+    const volatile unsigned long long *flag = (const volatile unsigned long long *)g_pub;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1; __atomic_load_n((const unsigned long long *)flag, __ATOMIC_ACQUIRE) != seq; it++) {
+      __builtin_ia32_pause();
+      if ((it & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+        HIPCK(hipStreamSynchronize(g_stream));   // a long wait: block (reports faults)
+        if (__atomic_load_n((const unsigned long long *)flag, __ATOMIC_ACQUIRE) != seq) {
+          fprintf(stderr, "omp_amg_amd: readback flag not set after the stream drained\n");
+          abort();
+        }
+        break;
+      }
+    }
+    memcpy(h, g_pub + 64, n);
+    return;
+  }
   if (n) HIPCK(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, amgd_s()));
   HIPCK(hipStreamSynchronize(g_stream));
 }
@@ -375,8 +437,7 @@ static T scan_impl(T *counts, uint64_t n) {
                                 rocprim::plus<T>(), s));
   HIPCK(hipMemcpyAsync(counts, tmpout, (n + 1) * sizeof(T), hipMemcpyDeviceToDevice, s));
   T total;
-  HIPCK(hipMemcpyAsync(&total, tmpout + n, sizeof(T), hipMemcpyDeviceToHost, s));
-  HIPCK(hipStreamSynchronize(s));
+  amgd_d2h(&total, tmpout + n, sizeof(T));
   amgd_free(tmp);
   amgd_free(tmpout);
   return total;
@@ -461,8 +522,7 @@ static int red_grid(uint64_t n) {
 static double sum_finish(int nb) {
   double *p = red_buf();
   k_sum_final<<<1, RED_THREADS, 0, amgd_s()>>>(p, nb, p + 2 * RED_BLOCKS);
-  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 8, hipMemcpyDeviceToHost, amgd_s()));
-  HIPCK(hipStreamSynchronize(amgd_s()));
+  amgd_d2h(g_red_h, p + 2 * RED_BLOCKS, 8);
   return g_red_h[0];
 }
 // Reference-order ("exact") dot products.  The reference sums left to right
@@ -1129,8 +1189,7 @@ extern "C" int amgd_get_exact(void) {
 }
 static double seq_finish() {
   double *p = red_buf();
-  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 8, hipMemcpyDeviceToHost, amgd_s()));
-  HIPCK(hipStreamSynchronize(amgd_s()));
+  amgd_d2h(g_red_h, p + 2 * RED_BLOCKS, 8);
   return g_red_h[0];
 }
 extern "C" double amgd_dot(const double *a, const double *b, uint64_t n) {
@@ -1199,8 +1258,7 @@ extern "C" double amgd_max_first(const double *a, uint64_t n, uint64_t *idx) {
   k_argmax_partial<<<nb, RED_THREADS, 0, amgd_s()>>>(a, nullptr, n, p, pi);
   k_argmax_partial<<<1, RED_THREADS, 0, amgd_s()>>>(p, pi, nb, p + 2 * RED_BLOCKS,
                                                     (uint64_t *)(p + 2 * RED_BLOCKS + 1));
-  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 16, hipMemcpyDeviceToHost, amgd_s()));
-  HIPCK(hipStreamSynchronize(amgd_s()));
+  amgd_d2h(g_red_h, p + 2 * RED_BLOCKS, 16);
   uint64_t gi;
   memcpy(&gi, &g_red_h[1], 8);
   if (idx) *idx = gi;
@@ -1219,8 +1277,7 @@ extern "C" double amgd_max_first2(const double *a, const double *b, uint64_t n, 
     k_argmax_partial<<<1, RED_THREADS, 0, amgd_s()>>>(p, pi, nb, p + 2 * RED_BLOCKS + 2 * q,
                                                       (uint64_t *)(p + 2 * RED_BLOCKS + 2 * q + 1));
   }
-  HIPCK(hipMemcpyAsync(g_red_h, p + 2 * RED_BLOCKS, 32, hipMemcpyDeviceToHost, amgd_s()));
-  HIPCK(hipStreamSynchronize(amgd_s()));
+  amgd_d2h(g_red_h, p + 2 * RED_BLOCKS, 32);
   uint64_t gi;
   memcpy(&gi, &g_red_h[1], 8);
   if (idx) *idx = gi;

@@ -241,6 +241,8 @@ extern void amgd_spmv_set_rw(int rw);
 API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_spmv_set_pair(int on);
 extern void amgd_spmv_set_rw_bounds(int lo, int hi);
+extern void amgd_set_d2h_poll(int on);
+API void amgd_test_d2h_poll(int on) { amgd_set_d2h_poll(on); }
 API void amgd_test_spmv_rw_bounds(int lo, int hi) { amgd_spmv_set_rw_bounds(lo, hi); }
 API void amgd_test_spmv_pair(int on) { amgd_spmv_set_pair(on); }
 extern void amgd_qfactor_set_coop_lds(int m);
