@@ -46,6 +46,9 @@ void amgd_reset_call_state(void);
 void amgd_sparse_reset_state(void);
 void amgd_interp_reset_state(void);
 void amgd_free(void *p);
+uint32_t amgd_max_row_len(const dcsr *M);   /* longest row of a pinned matrix, else UINT32_MAX */
+void amgd_rowmax_pin(const dcsr *M);           /* pattern fixed until unpinned / freed */
+void amgd_rowmax_unpin(const dcsr *M);
 void amgd_spmv_split_forget(const void *ro);   /* drop cached SpMV shard splits of a freed buffer */
 void amgd_rt_shutdown(void);             /* free everything; pointers become invalid */
 void amgd_pool_release(void);            /* return every cached block to the driver */
@@ -65,6 +68,8 @@ void amgd_set_stream(void *stream);
 /* event timers on the library stream, for kernel-level throughput */
 void amgd_timer_start(int slot);
 void amgd_timer_stop(int slot);
+void amgd_timer_start2(int slot, int slot2);   /* two slots timing the same interval */
+void amgd_timer_stop2(int slot, int slot2);
 double amgd_timer_ms(int slot);          /* accumulated, syncs */
 void amgd_timer_reset(void);
 void amgd_spgemm_set_timer(int slot);     /* SpGEMM numeric kernels timed on slot (-1: off) */

@@ -2433,8 +2433,10 @@ extern "C" uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t
   if (M->rn && M->nnz >= 16ull * M->rn) {
     uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 4);
     const uint32_t ml = fs_long(M);
-    k_pick_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, nullptr, ml, 0, ll, cnt + 1);
-    k_fs_expand_long<<<512, 256, 0, amgd_s()>>>(M->ro, M->col, ll, cnt + 1, stamp, tag, out, cnt, cap);
+    if (amgd_max_row_len(M) > ml) {                   // outlier rows present
+      k_pick_long<<<grid_for(n), 256, 0, amgd_s()>>>(M->ro, list, n, nullptr, ml, 0, ll, cnt + 1);
+      k_fs_expand_long<<<512, 256, 0, amgd_s()>>>(M->ro, M->col, ll, cnt + 1, stamp, tag, out, cnt, cap);
+    }
     k_fs_expand_wave<<<grid_for((uint64_t)n * 64, 256, 16384), 256, 0, amgd_s()>>>(
         M->ro, M->col, list, n, stamp, tag, out, cnt, cap, ml);
     amgd_free(ll);
@@ -2485,10 +2487,12 @@ extern "C" uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint
     k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
     llist = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
     const uint32_t ml = fs_long(Rt);
-    k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, ml, 1,
-                                                       llist, cnt + 3);
-    k_fs_select_long<<<64, 1024, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, llist,
-                                         cnt + 3, sel_i, sel_j, cnt + 1);
+    if (amgd_max_row_len(Rt) > ml) {                  // outlier columns present
+      k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, ml, 1,
+                                                         llist, cnt + 3);
+      k_fs_select_long<<<64, 1024, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, llist,
+                                           cnt + 3, sel_i, sel_j, cnt + 1);
+    }
     uint64_t avg = (Rt->nnz + nc - 1) / nc;
     int G = 4;
     while (G < 64 && (uint64_t)G * 2 <= avg) G <<= 1;

@@ -375,6 +375,30 @@ extern "C" void amgd_timer_stop(int s) {
   HIPCK(hipEventRecord(b, amgd_s()));
   g_pend[s].push_back({g_t0[s], b});
 }
+// Two slots over the same interval (the long-row SpMV: all shapes + its own shape) share
+// one event per end -- each timing event on the stream costs a few microseconds of GPU
+// idle between kernels.  A shared event returns to the pool when both slots have read it.
+static std::unordered_map<hipEvent_t, int> g_evshare;
+extern "C" void amgd_timer_start2(int s, int s2) {
+  amgd_timer_start(s);
+  g_t0[s2] = g_t0[s];
+}
+extern "C" void amgd_timer_stop2(int s, int s2) {
+  hipEvent_t b = ev_get();
+  HIPCK(hipEventRecord(b, amgd_s()));
+  g_pend[s].push_back({g_t0[s], b});
+  g_pend[s2].push_back({g_t0[s2], b});
+  g_evshare[g_t0[s]] += 2;
+  g_evshare[b] += 2;
+}
+static void ev_put(hipEvent_t e) {
+  auto it = g_evshare.find(e);
+  if (it != g_evshare.end()) {
+    if (--it->second > 0) return;
+    g_evshare.erase(it);
+  }
+  g_evpool.push_back(e);
+}
 extern "C" double amgd_timer_ms(int s) {
   tinit();
   for (auto &pr : g_pend[s]) {
@@ -382,8 +406,8 @@ extern "C" double amgd_timer_ms(int s) {
     float ms = 0;
     HIPCK(hipEventElapsedTime(&ms, pr.first, pr.second));
     g_acc[s] += ms;
-    g_evpool.push_back(pr.first);
-    g_evpool.push_back(pr.second);
+    ev_put(pr.first);
+    ev_put(pr.second);
   }
   g_pend[s].clear();
   return g_acc[s];
@@ -1352,13 +1376,18 @@ extern "C" void amgd_rt_shutdown(void) {
   g_inuse = 0;
   if (g_red) { (void)hipFree(g_red); g_red = nullptr; }
   if (g_red_h) { (void)hipHostFree(g_red_h); g_red_h = nullptr; }
+  if (g_pub) { (void)hipHostFree(g_pub); g_pub = nullptr; g_pub_on = -1; }
   if (g_tinit) {
+    std::vector<hipEvent_t> all(g_evpool);
     for (int i = 0; i < NTIMERS; i++) {
-      for (auto &pr : g_pend[i]) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+      for (auto &pr : g_pend[i]) { all.push_back(pr.first); all.push_back(pr.second); }
       g_pend[i].clear();
     }
-    for (hipEvent_t e : g_evpool) (void)hipEventDestroy(e);
+    std::sort(all.begin(), all.end());
+    all.erase(std::unique(all.begin(), all.end()), all.end());   // shared events once
+    for (hipEvent_t e : all) (void)hipEventDestroy(e);
     g_evpool.clear();
+    g_evshare.clear();
     g_tinit = false;
   }
   (void)hipStreamDestroy(g_stream);

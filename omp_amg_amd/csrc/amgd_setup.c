@@ -494,6 +494,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
   uint64_t prev_off = 0;
   uint32_t prev_nsel = 0;
   const int fslog = getenv("AMGD_FSLOG") != NULL;
+  amgd_rowmax_pin(Rl);                 /* the sweeps zero values, never move entries */
+  amgd_rowmax_pin(Rt);
   ph(PH_FS);
   for (;;) {
     it++;
@@ -560,6 +562,8 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
   if (fs_inc) {
     amgd_free(st_r); amgd_free(st_c); amgd_free(L1); amgd_free(L2); amgd_free(L3);
   }
+  amgd_rowmax_unpin(Rl);
+  amgd_rowmax_unpin(Rt);
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);

@@ -1066,7 +1066,7 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
                                double *z) {
   if (!n) return;
   const uint32_t ml = mv_long(M);
-  if (ml != 0xffffffffu && M->nnz > ml) {
+  if (ml != 0xffffffffu && M->nnz > ml && amgd_max_row_len(M) > ml) {
     uint32_t *ll = (uint32_t *)amgd_alloc((size_t)n * 4 + 16);
     unsigned *cnt = (unsigned *)(ll + n);
     amgd_memset(cnt, 0, 4);
@@ -1135,13 +1135,53 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
 #define MV_SHARD_MIN (1ull << 24)
 struct MvSplit { const uint64_t *ro; uint32_t rn; uint64_t nnz; std::vector<uint32_t> split; std::vector<uint64_t> pre; };
 static std::vector<MvSplit> g_mv_split;
+// Longest row of a matrix whose pattern a caller holds fixed over a loop (find_support's
+// R and R': hundreds of sweeps change values only): amgd_rowmax_pin computes it once,
+// amgd_rowmax_unpin drops it (and so does freeing the row-offset buffer).  The long-row
+// (outlier) paths -- a pick kernel plus the grid-wide scan, up to five launches per call
+// -- are skipped when no row of a pinned matrix is long.  An unpinned matrix reports
+// UINT32_MAX: the long-row paths run as before.
+struct RowMax { const uint64_t *ro; uint32_t rn; uint64_t nnz; uint32_t mx; };
+static std::vector<RowMax> g_rowmax;
+__global__ void k_row_max(const uint64_t *ro, uint32_t rn, unsigned *mx) {
+  unsigned m = 0;
+  GRID_STRIDE(i, rn) m = max(m, (unsigned)(ro[i + 1] - ro[i]));
+  for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+extern "C" void amgd_rowmax_pin(const dcsr *M) {
+  for (const RowMax &e : g_rowmax)
+    if (e.ro == M->ro && e.rn == M->rn && e.nnz == M->nnz) return;
+  unsigned h = 0;
+  if (M->rn) {
+    unsigned *d = (unsigned *)amgd_alloc(4);
+    amgd_memset(d, 0, 4);
+    k_row_max<<<grid_for(M->rn), 256, 0, amgd_s()>>>(M->ro, M->rn, d);
+    amgd_d2h(&h, d, 4);
+    amgd_free(d);
+  }
+  g_rowmax.push_back({M->ro, M->rn, M->nnz, h});
+}
+extern "C" void amgd_rowmax_unpin(const dcsr *M) {
+  for (size_t q = 0; q < g_rowmax.size();)
+    if (g_rowmax[q].ro == M->ro) g_rowmax.erase(g_rowmax.begin() + q);
+    else q++;
+}
+extern "C" uint32_t amgd_max_row_len(const dcsr *M) {
+  for (const RowMax &e : g_rowmax)
+    if (e.ro == M->ro && e.rn == M->rn && e.nnz == M->nnz) return e.mx;
+  return 0xffffffffu;
+}
 void amgd_spmv_split_forget(const void *ro) {
+  for (size_t q = 0; q < g_rowmax.size();)
+    if ((const void *)g_rowmax[q].ro == ro) g_rowmax.erase(g_rowmax.begin() + q);
+    else q++;
   if (g_mv_split.empty()) return;
   for (size_t q = 0; q < g_mv_split.size();)
     if ((const void *)g_mv_split[q].ro == ro) g_mv_split.erase(g_mv_split.begin() + q);
     else q++;
 }
-void amgd_spmv_split_clear(void) { g_mv_split.clear(); }
+void amgd_spmv_split_clear(void) { g_mv_split.clear(); g_rowmax.clear(); }
 static uint64_t g_mv_shard_calls = 0;
 extern "C" uint64_t amgd_spmv_shard_calls(void) { return g_mv_shard_calls; }   // (test API)
 static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alpha, const double *y,
@@ -1199,11 +1239,9 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     const int rwi = lane_rw(M->rn) == 64 ? 2 : lane_rw(M->rn) == 16 ? 1 : 0;
-    amgd_timer_start(1);                       // roofline: whole-matrix long-row products
-    amgd_timer_start(2 + rwi);                 // ... and per shape (RW 4 / 16 / 64)
+    amgd_timer_start2(1, 2 + rwi);             // roofline: whole-matrix long-row products,
     LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
-    amgd_timer_stop(2 + rwi);
-    amgd_timer_stop(1);
+    amgd_timer_stop2(1, 2 + rwi);              // all shapes and per shape (RW 4 / 16 / 64)
     const uint64_t rest = 16ull * M->rn + 8 + (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
     g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;
     g_mv_bytes_strict += 12 * M->nnz + (x ? 8ull * M->cn : 0) + rest;
