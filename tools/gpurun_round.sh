@@ -8,9 +8,10 @@ D=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 rm -rf $D; mkdir -p $D
 export PYTHONPATH=$GRAFT_REPO_ROOT
 if [ -z "$SKIP_TESTS" ]; then
-timeout -k 10 1080 python3 -u -m pytest tests -m gpu -x -q --durations=15 --timeout 300 --timeout-method thread > $D/gputests.log 2>&1 || { tail -30 $D/gputests.log; exit 1; }
+timeout -k 10 1140 python3 -u -m pytest tests -m gpu -x -q --durations=15 --timeout 300 --timeout-method thread > $D/gputests.log 2>&1 || { tail -30 $D/gputests.log; exit 1; }
 tail -2 $D/gputests.log
 fi
+[ -n "$TESTS_ONLY" ] && exit 0
 t0=$(date +%s)
 timeout -k 10 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench.json 2> $D/bench.err || { echo bench failed; tail -20 $D/bench.err; exit 1; }
 echo "bench wall $(( $(date +%s) - t0 )) s"
