@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spmv_pair.argtypes = [C.c_int]
         L.amgd_test_spmv_rw_bounds.argtypes = [C.c_int, C.c_int]
         L.amgd_test_d2h_poll.argtypes = [C.c_int]
+        L.amgd_test_qa_tile.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
         L.amgd_test_route_stats.argtypes = [C.POINTER(C.c_uint64), C.c_int]
@@ -298,6 +299,12 @@ def spmv_rw_bounds(code: int) -> None:
     the row counts, e.g. 1622 = 2^16 / 2^22, the default; -1: default).  A/B only."""
     code = int(code)
     lib().amgd_test_spmv_rw_bounds(code // 100 if code > 0 else 0, code % 100 if code > 0 else 0)
+
+
+def qa_tile(t: int) -> None:
+    """Q application of 33..512-point supports: U staged through LDS in 64 x t tiles
+    (16 / 32) or the row-per-lane kernel (0); -1 back to the default.  Same sums."""
+    lib().amgd_test_qa_tile(int(t))
 
 
 def d2h_poll(on: int) -> None:

@@ -1398,6 +1398,68 @@ __global__ __launch_bounds__(NT) void k_qapply(const uint32_t *rows, uint32_t nr
     __syncthreads();
   }
 }
+// k_qapply's first triangular product with U staged through LDS in tiles of 64 rows x T
+// columns (round 5).  Lane i walks row i of U left to right: in k_qapply every lane reads
+// its own row, so one load instruction touches 64 cache lines (texture-address work per
+// line, as in the long-row SpMV); a tile load covers 64 / T rows x T consecutive entries.
+// Each lane then continues its chain over the tile in order: the same products, the
+// same left-to-right sums.  The second product (lanes across i at fixed j) is coalesced
+// already and unchanged.
+template <int T>
+__global__ __launch_bounds__(64) void k_qapply_t(const uint32_t *rows, uint32_t nrows,
+                                                 const uint64_t *wro, const uint32_t *wcol,
+                                                 const double *Q, const uint64_t *qoff,
+                                                 const uint64_t *bro, const uint32_t *bcol,
+                                                 const double *ba, const double *u,
+                                                 const double *lambda, double *out) {
+  __shared__ double sq1[QF_LDS_NZ], sq2[QF_LDS_NZ];
+  __shared__ double tile[64][T + 1];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint32_t c = rows[r];
+    const uint64_t w0 = wro[c];
+    const uint32_t nz = (uint32_t)(wro[c + 1] - w0);
+    const uint32_t *Qj = wcol + w0;
+    const double *Qc = Q + qoff[c];
+    const uint64_t b0 = bro[c], b1 = bro[c + 1];
+    const double uc = u[c];
+    for (uint32_t m = lane; m < nz; m += 64) {
+      const double v = row_lookup(bcol, ba, b0, b1, Qj[m]);
+      sq1[m] = v + uc * lambda[Qj[m]];
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < nz; i0 += 64) {
+      const uint32_t i = i0 + lane, nr = min(64u, nz - i0), jend = i0 + nr;
+      double v = 0;
+      for (uint32_t j0 = 0; j0 < jend; j0 += T) {
+#pragma unroll
+        for (int q = 0; q < T; q++) {
+          const uint32_t fl = (uint32_t)q * 64 + lane, rr = fl / T, jj = fl % T;
+          const uint32_t ii = i0 + rr, j = j0 + jj;
+          tile[rr][jj] = rr < nr && j <= ii ? Qc[tri(ii) + j] : 0.0;
+        }
+        __syncthreads();
+        if (i < nz && i >= j0) {
+          const uint32_t jn = min((uint32_t)T, i + 1 - j0);
+          for (uint32_t jj = 0; jj < jn; jj++) v += tile[lane][jj] * sq1[j0 + jj];
+        }
+        __syncthreads();
+      }
+      if (i < nz) sq2[i] = v;
+    }
+    __syncthreads();
+    for (uint32_t i = lane; i < nz; i += 64) {
+      double y = 0;
+      for (uint32_t j = i; j < nz; j++) y += Qc[tri(j) + i] * sq2[j];
+      out[w0 + i] = y;
+    }
+    __syncthreads();
+  }
+}
+// AMGD_QA_TILE / amgd_qa_set_tile (tests, A/B): 16 (default: 256^3 24.94 -> 24.84 s,
+// profiles/r05/abq_qapply_tiles.txt), 32 (25.08 s), 0 the row-per-lane k_qapply<64>
+static int g_qa_tile = -1;
+extern "C" void amgd_qa_set_tile(int t) { g_qa_tile = t; }
 // Small supports (nz <= SEG: most coarse points of the fine levels) take SEG lanes each,
 // 256 / SEG supports per work-group, synchronised per wavefront: a 64-lane group per
 // support left most lanes idle and paid three block barriers per support.  Same sums in
@@ -1555,8 +1617,19 @@ static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, 
   }
   if (rs.ns) {
     int g = (int)std::min<unsigned>(rs.ns, 65536u);
-    k_qapply<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
-                                         Bt->a, u, lambda, out, nullptr, 0);
+    if (g_qa_tile == -1) {
+      const char *e = getenv("AMGD_QA_TILE");
+      g_qa_tile = e && *e ? atoi(e) : 16;
+    }
+    if (g_qa_tile == 16)
+      k_qapply_t<16><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
+                                      Bt->a, u, lambda, out);
+    else if (g_qa_tile == 32)
+      k_qapply_t<32><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
+                                      Bt->a, u, lambda, out);
+    else
+      k_qapply<64, false><<<g, 64, 0, s>>>(rs.sl, rs.ns, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
+                                           Bt->a, u, lambda, out, nullptr, 0);
   }
   if (rs.nb) {
     int g = (int)std::min<unsigned>(rs.nb, 1024u);

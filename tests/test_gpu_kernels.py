@@ -836,6 +836,22 @@ def test_qapply_huge_grid_path(structure):
     assert np.array_equal(X1.a.view(np.uint64), X2.a.view(np.uint64))
 
 
+@pytest.mark.parametrize("tile", [16, 32])
+def test_qapply_lds_tiles(tile):
+    """Q application of 33..512-point supports with U staged through LDS in 64 x tile
+    tiles equals the row-per-lane kernel bit for bit (every tier size, a partial last
+    row group, an empty support)"""
+    W, A = _qfactor_case("tiers")
+    oa.qa_tile(0)
+    try:
+        X1 = oa.test_csr_op(7, W, A)
+        oa.qa_tile(tile)
+        X2 = oa.test_csr_op(7, W, A)
+    finally:
+        oa.qa_tile(-1)
+    assert np.array_equal(X1.a.view(np.uint64), X2.a.view(np.uint64))
+
+
 @pytest.mark.parametrize("case", ["short", "long", "ties", "over_lds"])
 def test_expand_pick(case):
     """expand_support's per-row pick: short rows (rank-count kernel), long rows (LDS
