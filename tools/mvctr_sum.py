@@ -1,5 +1,5 @@
 """Sum tools/gpurun_mvctr.sh's per-dispatch counters per kernel and print the ratios:
-TA busy share (TA_TA_BUSY over 256 CUs x GRBM_GUI_ACTIVE), TA address / data stalls on
+TA busy share (TA_TA_BUSY over 256 CUs x the kernel's cycles, GRBM_GUI_ACTIVE / 8 XCDs), TA address / data stalls on
 the cache, L1 cache-line accesses and L2 requests per load wavefront, UTCL1 misses.
 usage: python tools/mvctr_sum.py <dir>"""
 import collections
@@ -20,6 +20,7 @@ for f in glob.glob(os.path.join(d, "pass*", "**", "*counter_collection.csv"), re
             c = f"GRBM_GUI_ACTIVE@{p}"
         tot[name][c] += float(r["Counter_Value"])
 CU = 256
+XCD = 8      # GRBM_GUI_ACTIVE comes summed over the 8 XCDs: per-dispatch cycles x 8
 
 
 def q(t, a, b, s=1.0):
@@ -30,7 +31,7 @@ print(f"{'kernel':64s} {'TAbusy':>6s} {'TAaddrSt':>8s} {'TAdataSt':>8s} {'lines/
       f"{'TLBmiss':>7s} {'pendSt':>7s}")
 for k in sorted(tot, key=lambda k: -tot[k].get("GRBM_GUI_ACTIVE@1", 0)):
     t = tot[k]
-    g1, g2 = t.get("GRBM_GUI_ACTIVE@1", 0), t.get("GRBM_GUI_ACTIVE@2", 0)
+    g1, g2 = t.get("GRBM_GUI_ACTIVE@1", 0) / XCD, t.get("GRBM_GUI_ACTIVE@2", 0) / XCD
     ta = t.get("TA_TA_BUSY_sum", 0) / (CU * g1) if g1 else float("nan")
     sa = t.get("TA_ADDR_STALLED_BY_TC_CYCLES_sum", 0) / (CU * g2) if g2 else float("nan")
     sd = t.get("TA_DATA_STALLED_BY_TC_CYCLES_sum", 0) / (CU * g2) if g2 else float("nan")
