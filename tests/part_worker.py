@@ -26,7 +26,10 @@ from omp_amg_amd import abi, parity, shard  # noqa: E402
 def main():
     rank, size = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=size)
-    oa.init(0)
+    # PART_TRANSPORT=rccl (>= size GPUs): one GPU per rank, the library's RCCL communicator
+    # over xGMI -- the send/recv groups of the halo fetches, transposes and routes
+    rccl = os.environ.get("PART_TRANSPORT") == "rccl"
+    oa.init(rank if rccl else 0)
     L = oa.lib()
     L.amgd_test_pool_inuse.restype = C.c_uint64
     before = L.amgd_test_pool_inuse()
@@ -41,7 +44,10 @@ def main():
         import make_digests as md
         digest = json.load(open(md.OUT))["cases"][case[7:]]
         Ai, Aj, Av = md.generate(digest["gen"])
-    shard.init_host(rank, size)
+    if rccl:
+        shard.init_rccl(rank, size)
+    else:
+        shard.init_host(rank, size)
     if not os.environ.get("PART_DEFAULT"):     # PART_DEFAULT: crs_setup's own default (partitioned)
         oa.lib().amgd_comm_set_partitioned(1)
     shard.stats(reset=True)

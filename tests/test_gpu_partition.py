@@ -102,6 +102,21 @@ def test_crs_setup_defaults_to_partitioned():
     _run(2, "gold:p7_12", crs="1", extra_env={"PART_DEFAULT": "1"})
 
 
+def _gpus():
+    import torch
+    return torch.cuda.device_count()          # counts devices without initialising one
+
+
+@pytest.mark.skipif(_gpus() < 2, reason="needs >= 2 GPUs (one rank per GPU over RCCL)")
+@pytest.mark.parametrize("case", ["digest:p7_48", "gold:aniso_12"])
+def test_partitioned_two_ranks_rccl(case):
+    """the partitioned driver over the library's RCCL communicator with two ranks on two
+    GPUs (xGMI send/recv groups for every halo fetch, transpose and route; the host
+    transport of the other tests stages them through gloo): bit-identical to the
+    one-GPU digest / reference fixture, with the collective guard on"""
+    _run(2, case, timeout=170, extra_env={"PART_TRANSPORT": "rccl"})
+
+
 def test_amg_setup_under_partitioned_comm():
     """amg_setup with a 2-process partitioned communicator: each process passes the whole
     matrix (the reference's meaning) and gets the one-GPU hierarchy with no exchange;
