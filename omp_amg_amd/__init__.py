@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         L.amgd_test_spmv_pair.argtypes = [C.c_int]
         L.amgd_test_spmv_rw_bounds.argtypes = [C.c_int, C.c_int]
         L.amgd_test_d2h_poll.argtypes = [C.c_int]
+        L.amgd_test_fs_amx.argtypes = [C.c_int]
         L.amgd_test_qa_tile.argtypes = [C.c_int]
         L.amgd_test_qa_huge.argtypes = [C.c_int]
         L.amgd_test_spmv_shard_calls.restype = C.c_uint64
@@ -305,6 +306,13 @@ def qa_tile(t: int) -> None:
     """Q application of 33..512-point supports: U staged through LDS in 64 x t tiles
     (16 / 32) or the row-per-lane kernel (0); -1 back to the default.  Same sums."""
     lib().amgd_test_qa_tile(int(t))
+
+
+def fs_amx(on: int) -> None:
+    """find_support's selection after a full sweep: from the fused first maxima of the
+    w = R' rs product (1, default) or by its own pass over the bad columns (0); -1 back to
+    the default.  Same selections."""
+    lib().amgd_test_fs_amx(int(on))
 
 
 def d2h_poll(on: int) -> None:

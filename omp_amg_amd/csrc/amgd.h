@@ -308,6 +308,10 @@ uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
                            uint32_t *sel_j, uint32_t *nremoved, uint32_t c0, int resum);
 /* incremental sweeps: distinct columns of the listed rows of M (stamp/tag dedupe);
    returns the count, > cap when the list overflowed */
+int amgd_spmv_amax(const dcsr *M, const double *x, double *z, uint64_t *amx);
+uint32_t amgd_fs_select_amx(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm, double *rs,
+                            const double *w, double *sumR, double thr, const uint64_t *amx,
+                            uint32_t *sel_i, uint32_t *sel_j, uint32_t *nremoved);
 uint32_t amgd_fs_expand(const dcsr *M, const uint32_t *list, uint32_t n, uint32_t *stamp,
                         uint32_t tag, uint32_t *out, uint32_t cap);
 /* partitioned mode: ids of another rank's expansion claimed into out (have: entries so far) */

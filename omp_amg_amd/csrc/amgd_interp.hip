@@ -2598,6 +2598,50 @@ extern "C" uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint
   return h[0];
 }
 
+// The selection when the sweep's w = R' rs product also produced each column's first
+// largest product (amgd_spmv_amax on R'): the same (value, first position) maximum as
+// k_fs_select's, taken from the product instead of a second pass over the bad columns.
+__global__ void k_fs_pick_amx(const uint32_t *list, const unsigned *nlist, const uint64_t *amx,
+                              const uint32_t *trow, const uint64_t *perm, double *ta, double *a,
+                              uint32_t *si, uint32_t *sj, unsigned *removed) {
+  const unsigned n = *nlist;
+  for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = list[r];
+    const uint64_t best = amx[c];
+    si[r] = best != ~0ull ? trow[best] : 0u;
+    sj[r] = c;
+    if (best != ~0ull) { ta[best] = 0.0; if (perm) a[perm[best]] = 0.0; *removed = 1u; }
+  }
+}
+extern "C" uint32_t amgd_fs_select_amx(const dcsr *Rl, const dcsr *Rt, const uint64_t *perm,
+                                       double *rs, const double *w, double *sumR, double thr,
+                                       const uint64_t *amx, uint32_t *sel_i, uint32_t *sel_j,
+                                       uint32_t *nremoved) {
+  hipStream_t s = amgd_s();
+  const uint32_t nc = Rt->rn;
+  uint32_t *list = (uint32_t *)amgd_alloc(((size_t)nc + 1) * 4);
+  unsigned *cnt = (unsigned *)amgd_alloc(16);
+  amgd_memset(cnt, 0, 16);
+  if (nc) {
+    k_fs_badlist<<<grid_for(nc), 256, 0, s>>>(w, sumR, thr, nc, list, cnt + 2);
+    k_fs_pick_amx<<<grid_for(nc), 256, 0, s>>>(list, cnt + 2, amx, Rt->col, perm, Rt->a, Rl->a,
+                                                sel_i, sel_j, cnt + 1);
+  }
+  KCHECK();
+  unsigned h[4];
+  amgd_d2h(h, cnt, 12);
+  h[0] = h[2];
+  if (h[1]) {
+    amgd_list_rowsum(Rl, sel_i, h[0], rs, Rl->nnz > 32ull * Rl->rn);
+    amgd_list_rowsum(Rt, sel_j, h[0], sumR, Rt->nnz > 32ull * Rt->rn);
+  }
+  amgd_free(list);
+  amgd_free(cnt);
+  *nremoved = h[1];
+  return h[0];
+}
+
 // ---------------------------------------------------------------------------
 // expand_support pieces (amg_setup.c:907)
 // ---------------------------------------------------------------------------

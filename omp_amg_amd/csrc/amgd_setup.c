@@ -451,6 +451,17 @@ static void solve_weights(dcsr **W, dcsr **Wt_out, const dcsr **W0, double *lam,
 
 
 
+/* AMGD_FS_AMX=0 / amgd_fs_set_amx(0) (tests, A/B): find_support selects by its own pass
+   over the bad columns (k_fs_select) even after a full sweep's fused product */
+static int g_fs_amx = -1;
+void amgd_fs_set_amx(int on) { g_fs_amx = on; }
+static int fs_amx_on(void) {
+  if (g_fs_amx < 0) {
+    const char *e = getenv("AMGD_FS_AMX");
+    return !(e && *e == '0');
+  }
+  return g_fs_amx;
+}
 /* the first sweep's products when the caller already formed them from the same R
    (interpolation's w1 / w2 test, amg_setup.c:870-880: rs = R*1, w = R'rs, tmp = R w,
    w2 = R' tmp -- the same ordered sums), else NULL */
@@ -496,6 +507,9 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
   const int fslog = getenv("AMGD_FSLOG") != NULL;
   amgd_rowmax_pin(Rl);                 /* the sweeps zero values, never move entries */
   amgd_rowmax_pin(Rt);
+  /* full sweeps: the selection's per-column first maximum comes out of w = R' rs */
+  uint64_t *amx = fs_amx_on() ? (uint64_t *)amgd_alloc((size_t)nc * 8 + 8) : NULL;
+  int amx_ok = 0;
   ph(PH_FS);
   for (;;) {
     it++;
@@ -526,8 +540,10 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
       amgd_d2d(w2, f1->w2, (size_t)nc * 8);
       done = 1;
     }
+    amx_ok = 0;
     if (!done) {
-      amgd_spmvt(Rt, rs, w);                              /* w = R'*rs (row order) */
+      if (amx) amx_ok = amgd_spmv_amax(Rt, rs, w, amx);  /* w = R'*rs (row order) */
+      else amgd_spmvt(Rt, rs, w);
       amgd_spmv(Rl, w, tmp, 0., NULL, 1., NULL);
       amgd_spmvt(Rt, tmp, w2);                            /* w2 = R'*(R*w) */
     }
@@ -540,7 +556,9 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
     if (theta == 0) { UB(1); break; }                   /* reference spins forever */
     if (nf <= 1) { UB(2); break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
-    uint32_t nsel = amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
+    uint32_t nsel = amx_ok ? amgd_fs_select_amx(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, amx, si + ns,
+                                                sj + ns, &nrem)
+                           : amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);
     prev_off = ns;
     prev_nsel = nsel;
     ns += nsel;
@@ -564,6 +582,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
   }
   amgd_rowmax_unpin(Rl);
   amgd_rowmax_unpin(Rt);
+  if (amx) amgd_free(amx);
   dcsr_free(&Rl); dcsr_free(&Rt); amgd_free(perm);
   amgd_free(onec); amgd_free(rs); amgd_free(w); amgd_free(w2); amgd_free(tmp); amgd_free(vv);
   amgd_free(sumR); amgd_free(si); amgd_free(sj);

@@ -774,12 +774,16 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
 // for the x gathers (issued when a round's columns have arrived, CA - GA rounds after
 // them), VA for the values (VA == CA: loaded with the columns; else on their own, the
 // pair index recomputed).  CA 2, GA 1, VA 2 (other depths measured slower).
-template <bool LIST, int RW, int PER, int CA, int GA, int VA>
+// AMX (whole-matrix products only): per row also the position of its first largest
+// product (strict >, from -DBL_MAX: find_support's selection rule, k_fs_select) as the
+// global entry index into amx[row] (~0 when no product beats -DBL_MAX).
+template <bool LIST, int RW, int PER, int CA, int GA, int VA, bool AMX = false>
 __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_t *col,
                                                const double *a, uint32_t n,
                                                const uint32_t *list, const double *x,
                                                double *z, double alpha, const double *y,
-                                               double beta, const uint8_t *f, uint32_t maxlen) {
+                                               double beta, const uint8_t *f, uint32_t maxlen,
+                                               uint64_t *amx = nullptr) {
   constexpr int SEG = 64 * PER / RW, PH = PER / 2, NC = CA - GA;
   static_assert(PER <= 32 && PER % 2 == 0 && SEG % 2 == 0, "k_spmv_pair: round shape");
   static_assert(GA >= 1 && NC >= 1 && VA >= 1 && VA <= CA, "k_spmv_pair: depths");
@@ -871,7 +875,8 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
         if (VA < CA && j < VA) lda(j * SEG, va[j]);
       }
     }
-    double t = 0;
+    double t = 0, mxv = -DBL_MAX;
+    uint32_t mxp = 0xffffffffu;
     for (uint32_t off = 0; off < mx; off += SEG) {
 #pragma unroll
       for (int p = 0; p < PH; p++) {
@@ -911,10 +916,20 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
 #pragma unroll
             for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
 #pragma unroll
-            for (int e = 0; e < U; e++) t += u[e];
+            for (int e = 0; e < U; e++) {
+              t += u[e];
+              if (AMX) {
+                const uint32_t pos = off + (uint32_t)(e0 + e);
+                if (pos >= lead && u[e] > mxv) { mxv = u[e]; mxp = pos; }
+              }
+            }
           }
         } else {
-          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+          for (uint32_t e = 0; e < m; e++) {
+            const double pv = buf[w][lane][e];
+            t += pv;
+            if (AMX && off + e >= lead && pv > mxv) { mxv = pv; mxp = off + e; }
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -926,6 +941,7 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
       if (f) v = v * (f[i] ? 1.0 : 0.0);
       z[i] = v;
     }
+    if (AMX && own) amx[i] = mxp == 0xffffffffu ? ~0ull : k0 - lead + mxp;
   }
 }
 template <bool LIST, int RW, int PER, int CA = 2, int GA = 1, int VA = 2>
@@ -936,6 +952,13 @@ __global__ __launch_bounds__(256) void k_spmv_pair(const uint64_t *ro, const uin
                                                    double beta, const uint8_t *f,
                                                    uint32_t maxlen = 0xffffffffu) {
   spmv_pair_body<LIST, RW, PER, CA, GA, VA>(ro, col, a, n, list, x, z, alpha, y, beta, f, maxlen);
+}
+template <int RW, int PER>
+__global__ __launch_bounds__(256) void k_spmv_pair_amx(const uint64_t *ro, const uint32_t *col,
+                                                       const double *a, uint32_t n, const double *x,
+                                                       double *z, uint64_t *amx) {
+  spmv_pair_body<false, RW, PER, 2, 1, 2, true>(ro, col, a, n, nullptr, x, z, 0.0, nullptr, 1.0, nullptr,
+                                                0xffffffffu, amx);
 }
 // Products with x take k_spmv_pair by default (round 5: long-row SpMV 5.02 -> 4.88 s per
 // 256^3 setup, profiles/r05/pair/); AMGD_MV_PAIR=0 / amgd_spmv_set_pair(0) (tests, A/B):
@@ -1085,8 +1108,22 @@ extern "C" void amgd_spmv_rows(const dcsr *M, const uint32_t *list, uint32_t n, 
   LANE_LAUNCH(true, n, list, x, z, 0.0, nullptr, 1.0, nullptr, ml);
   KCHECK();
 }
+// amgd_spmv_amax: z = M x plus, per row, the global entry index of its first largest product
+// (find_support's selection, fused into the w = R' rs product of a full sweep).  Returns 1
+// when the lane kernel produced them, 0 when the product took another kernel (short rows,
+// few rows, a sharded product, an unaligned view): the caller selects the old way then.
+static uint64_t *g_amx = nullptr;
+static int g_amx_done = 0;
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                       double beta, const uint8_t *f);
+extern "C" int amgd_spmv_amax(const dcsr *M, const double *x, double *z, uint64_t *amx) {
+  g_amx = amx;
+  g_amx_done = 0;
+  amgd_spmv(M, x, z, 0.0, nullptr, 1.0, nullptr);
+  g_amx = nullptr;
+  KCHECK();
+  return g_amx_done;
+}
 // algorithmic bytes of the event-timed (timer slot 1) lane-kernel products: each entry's
 // column + value once, x gathered once per entry, row offsets, z (and y, f) once per row
 // g_mv_bytes_strict: the same with x read once (8 B per column), the minimum any
@@ -1240,7 +1277,22 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     const int rwi = lane_rw(M->rn) == 64 ? 2 : lane_rw(M->rn) == 16 ? 1 : 0;
     amgd_timer_start2(1, 2 + rwi);             // roofline: whole-matrix long-row products,
-    LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
+    if (g_amx && x && alpha == 0.0 && beta == 1.0 && !f && mv_pair(M)) {
+      const int rw_ = lane_rw(M->rn);          // + each row's first largest product
+      const int gp_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
+      amgd_route_hit(AMGD_R_SPMV_PIPE);
+      amgd_route_hit(AMGD_R_MV_PAIR);
+      amgd_route_hit(rw_ == 64 ? AMGD_R_MV_RW64 : rw_ == 16 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);
+      if (rw_ == 64)
+        k_spmv_pair_amx<64, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, g_amx);
+      else if (rw_ == 16)
+        k_spmv_pair_amx<16, 16><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, g_amx);
+      else
+        k_spmv_pair_amx<4, 8><<<gp_, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, g_amx);
+      g_amx_done = 1;
+    } else {
+      LANE_LAUNCH(false, M->rn, (const uint32_t *)nullptr, x, z, alpha, y, beta, f, 0xffffffffu);
+    }
     amgd_timer_stop2(1, 2 + rwi);              // all shapes and per shape (RW 4 / 16 / 64)
     const uint64_t rest = 16ull * M->rn + 8 + (y && alpha != 0.0 ? 8ull * M->rn : 0) + (f ? (uint64_t)M->rn : 0);
     g_mv_bytes += 12 * M->nnz + (x ? 8 * M->nnz : 0) + rest;

@@ -242,6 +242,8 @@ API void amgd_test_spmv_rw(int rw) { amgd_spmv_set_rw(rw); }
 extern void amgd_spmv_set_pair(int on);
 extern void amgd_spmv_set_rw_bounds(int lo, int hi);
 extern void amgd_set_d2h_poll(int on);
+extern void amgd_fs_set_amx(int on);
+API void amgd_test_fs_amx(int on) { amgd_fs_set_amx(on); }
 extern void amgd_qa_set_tile(int t);
 API void amgd_test_qa_tile(int t) { amgd_qa_set_tile(t); }
 API void amgd_test_d2h_poll(int on) { amgd_set_d2h_poll(on); }
