@@ -776,7 +776,9 @@ __global__ __launch_bounds__(256) void k_spmv_pipe(const uint64_t *ro, const uin
 // pair index recomputed).  CA 2, GA 1, VA 2 (other depths measured slower).
 // AMX (whole-matrix products only): per row also the position of its first largest
 // product (strict >, from -DBL_MAX: find_support's selection rule, k_fs_select) as the
-// global entry index into amx[row] (~0 when no product beats -DBL_MAX).
+// global entry index into amx[row] (~0 when no product beats -DBL_MAX).  Every round's
+// maximum is found by all 64 lanes (the adds use only RW of them); tracking it in the adding
+// lane alone measured 0.1 s slower per 256^3 setup (profiles/r05/ab256_r05aj_parallel_max.txt).
 template <bool LIST, int RW, int PER, int CA, int GA, int VA, bool AMX = false>
 __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_t *col,
                                                const double *a, uint32_t n,
@@ -888,6 +890,32 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (AMX) {
+        // the round's first largest product of every row, by all 64 lanes: 64 / RW lanes
+        // per row scan SEG / (64 / RW) consecutive slots each in order, then combine --
+        // larger value, or equal value at the smaller position -- which is the sequential
+        // "first x > max" (NaN, -inf and -DBL_MAX never enter); earlier rounds keep ties
+        constexpr int LPR = 64 / RW, EPL = SEG / LPR;
+        const int rr = lane / LPR, part = lane % LPR;
+        const uint32_t info = rlen[w][rr], vl = info & 0x7fffffffu, ld0 = info >> 31;
+        double bv = -DBL_MAX;
+        uint32_t bp = 0xffffffffu;
+#pragma unroll
+        for (int e = 0; e < EPL; e++) {
+          const uint32_t sub = (uint32_t)(part * EPL + e), pos = off + sub;
+          const double v = buf[w][rr][sub];
+          if (pos < vl && pos >= ld0 && v > bv) { bv = v; bp = pos; }
+        }
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) {
+          const double ov = __shfl_xor(bv, o, 64);
+          const uint32_t op = (uint32_t)__shfl_xor((int)bp, o, 64);
+          if (ov > bv || (ov == bv && op < bp)) { bv = ov; bp = op; }
+        }
+        const double sv = __shfl(bv, (lane % RW) * LPR, 64);
+        const uint32_t sp = (uint32_t)__shfl((int)bp, (lane % RW) * LPR, 64);
+        if (lane < RW && sv > mxv) { mxv = sv; mxp = sp; }
+      }
       // shift the rings down one round, then fill the new last slots
 #pragma unroll
       for (int j = 0; j + 1 < VA; j++)
@@ -916,20 +944,10 @@ __device__ __forceinline__ void spmv_pair_body(const uint64_t *ro, const uint32_
 #pragma unroll
             for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
 #pragma unroll
-            for (int e = 0; e < U; e++) {
-              t += u[e];
-              if (AMX) {
-                const uint32_t pos = off + (uint32_t)(e0 + e);
-                if (pos >= lead && u[e] > mxv) { mxv = u[e]; mxp = pos; }
-              }
-            }
+            for (int e = 0; e < U; e++) t += u[e];
           }
         } else {
-          for (uint32_t e = 0; e < m; e++) {
-            const double pv = buf[w][lane][e];
-            t += pv;
-            if (AMX && off + e >= lead && pv > mxv) { mxv = pv; mxp = off + e; }
-          }
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
