@@ -82,6 +82,26 @@ def test_gpu_matches_digest_default_routing(case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["p7_64", "p7_96"])
+def test_gpu_matches_digest_unfused_selection(case):
+    """find_support's selection by its own pass over the bad columns (k_fs_select) instead
+    of the maxima fused into the full sweeps' w = R' rs product (the default since round
+    5): the same stored digest either way"""
+    mk = _mk()
+    d = _db()["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    oa.fs_amx(0)
+    try:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.fs_amx(-1)
+    got = mk.hierarchy_digest(h)
+    exp = d["arrays"]
+    bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    assert not bad, f"{len(bad)} arrays differ from the {d['source']}: {bad[:12]}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("case", ["p7_96", "p7_128"])
 def test_gpu_matches_digest_rw64_forced(case):
     """the 64-rows-per-wavefront long-row SpMV (k_spmv_pipe<*,64,16>, by default only on
