@@ -16,7 +16,9 @@ value   : whole-job rows/s of the setup.  N>1 (DESIGN.md "Multi-GPU"): one setup
           replicated hierarchy with sharded kernels; --mode replicas: N independent
           setups (value = N x rows / max time, scaling "weak").
 roofline: the dominant kernel by time, the long-row SpMV (k_spmv_pair<false,RW,PER,..>
-          for products with x, k_spmv_pipe<false,RW,PER,false> for ordered row sums;
+          for products with x -- k_spmv_pair_amx<RW,PER> in find_support's full sweeps,
+          which also tracks each row's first largest product for the fused selection --
+          k_spmv_pipe<false,RW,PER,false> for ordered row sums;
           whole-matrix products: find_support's sweeps, PCG, Lanczos), event-timed
           live on the library stream; algorithmic bytes = 12 B per entry + 8 B per
           column (x read once) + 16 B per row; the rate with x gathered
@@ -362,8 +364,10 @@ def main():
                          "traffic_source": t_src,
                          "launches_per_setup": mv_n / steps,
                          "algorithmic_bytes_per_launch": mv_strict / mv_n if mv_n else None,
-                         "kernel": "k_spmv_pair<false,RW,PER,..> (products with x) / k_spmv_pipe<false,RW,PER,false> "
-                                   "(row sums): whole-matrix long-row SpMV (ordered row sums; "
+                         "kernel": "k_spmv_pair<false,RW,PER,..> (products with x; k_spmv_pair_amx in find_support's "
+                                   "full sweeps, + the fused selection's row maxima) / "
+                                   "k_spmv_pipe<false,RW,PER,false> (row sums): whole-matrix "
+                                   "long-row SpMV (ordered row sums; "
                                    "find_support sweeps, PCG, Lanczos), the setup's dominant kernel by time, "
                                    "HIP-event timed",
                          "algorithmic_bytes_per_setup": mv_strict / steps,

@@ -14,7 +14,7 @@ for C in FETCH_SIZE WRITE_SIZE; do
   r=$?; echo "calib $C rc=$r"; [ $r -eq 0 ] || exit 1
 done
 for K in spmv rap; do
-  if [ $K = spmv ]; then RX='k_spmv_(pipe|pair)<false'; else RX='k_sg_(row|kseq)<[0-9]+, [0-9]+, 1, 1>|k_sg_win<[0-9]+, 1>|k_sg_wwin<[0-9]+, 1, 1>|k_spgemm_long<1, 1>'; fi
+  if [ $K = spmv ]; then RX='k_spmv_(pipe|pair)<false|k_spmv_pair_amx'; else RX='k_sg_(row|kseq)<[0-9]+, [0-9]+, 1, 1>|k_sg_win<[0-9]+, 1>|k_sg_wwin<[0-9]+, 1, 1>|k_spgemm_long<1, 1>'; fi
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "$RX" -d $D/traffic_${K}_$C -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/probe_scale.py 256 > $D/traffic_${K}_$C.log 2>&1
     r=$?; echo "$K $C rc=$r"; [ $r -eq 0 ] || exit 1
