@@ -404,7 +404,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024", "mv_pair")
+          "qf_t512", "qf_t1024", "mv_pair", "fs_amx")
 
 
 def route_stats(reset: bool = True) -> dict:

@@ -34,6 +34,8 @@ int amgd_rt_init(int device);            /* idempotent; 0 on success */
 const char *amgd_last_error(void);
 void amgd_set_error(const char *msg);
 void *amgd_alloc(size_t bytes);          /* arena; out of HBM: unwinds to amgd_try, else aborts */
+void *amgd_alloc_f64(size_t bytes);      /* the same, for arrays of doubles (AMGD_POISON=1: NaN-filled) */
+void amgd_set_poison(int on);
 void amgd_set_hbm_cap(size_t bytes);     /* cap on live bytes (tests; 0: none) */
 /* run fn(arg); if an allocation runs out of HBM inside it, every block allocated since
    the call is released and -2 returned (amgd_last_error() has the text) */
@@ -50,6 +52,12 @@ uint32_t amgd_max_row_len(const dcsr *M);   /* longest row of a pinned matrix, e
 void amgd_rowmax_pin(const dcsr *M);           /* pattern fixed until unpinned / freed */
 void amgd_rowmax_unpin(const dcsr *M);
 void amgd_spmv_split_forget(const void *ro);   /* drop cached SpMV shard splits of a freed buffer */
+/* partitioned-setup diagnostics (tests): interp_lmop calls on gathered data / with a dirty
+   prefix; eager exchanges / those that took the second round; forced rare paths */
+void amgd_part_stats(uint64_t *out2);
+void amgd_part_set_force_gather(int on);
+void pm_eager_stats(uint64_t *calls, uint64_t *second);
+void pm_eager_force_slot(int64_t bytes);
 void amgd_rt_shutdown(void);             /* free everything; pointers become invalid */
 void amgd_pool_release(void);            /* return every cached block to the driver */
 size_t amgd_pool_bytes_in_use(void);
@@ -84,7 +92,7 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
 enum { AMGD_R_SPMV_PIPE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WWIN,
        AMGD_R_SG_WWIN_SYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
        AMGD_R_MV_RW4, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_MV_RW16, AMGD_R_MV_RW64,
-       AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_MV_PAIR, AMGD_R_N };
+       AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_MV_PAIR, AMGD_R_FS_AMX, AMGD_R_N };
 extern uint64_t amgd_route_ctr[32];
 #define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
 

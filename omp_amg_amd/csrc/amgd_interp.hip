@@ -970,7 +970,7 @@ static bool qfactor_split(uint32_t c, const dcsr *Wt, const dcsr *A, uint64_t w0
     uint64_t *qoff_s = (uint64_t *)amgd_alloc(((size_t)ncomp + 1) * 8);
     k_qsize<<<grid_for(ncomp), 256, 0, s>>>(sub.ro, ncomp, qoff_s);
     const uint64_t tot_s = amgd_scan_u64(qoff_s, ncomp);
-    double *Qs = (double *)amgd_alloc(tot_s * 8 + 8);
+    double *Qs = (double *)amgd_alloc_f64(tot_s * 8 + 8);
     g_qf_split_depth++;
     qfactor_range(&sub, A, qoff_s, Qs, 0, ncomp, tot_s);
     g_qf_split_depth--;
@@ -1091,7 +1091,7 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
   std::vector<uint32_t> big, bignz;
   std::vector<unsigned *> bigstat;
   auto launch_coop = [&](uint32_t c, uint32_t nz) {
-    double *s1b = (double *)amgd_alloc((size_t)nz * 8 * 4 + 8);
+    double *s1b = (double *)amgd_alloc_f64((size_t)nz * 8 * 4 + 8);
     double *s2v = s1b + 2 * (size_t)nz, *qk = s1b + 3 * (size_t)nz;
     unsigned *bar = (unsigned *)amgd_alloc(16);
     HIPCK(hipMemsetAsync(bar, 0, 16, s2));
@@ -1301,7 +1301,7 @@ extern "C" double *amgd_qfactor_reuse(const dcsr *Wt, const dcsr *A, uint64_t **
   uint64_t *qoff = (uint64_t *)amgd_alloc(L * 8);
   if (rn) k_qsize<<<grid_for(rn), 256, 0, s>>>(Wt->ro, rn, qoff);
   uint64_t tot = amgd_scan_u64(qoff, rn);
-  double *Q = (double *)amgd_alloc(tot * 8 + 8);
+  double *Q = (double *)amgd_alloc_f64(tot * 8 + 8);
   if (Wp && Qp && qpoff && Wp->rn == rn && rn && qf_reuse_on()) {
     g_qskip = (uint8_t *)amgd_alloc((size_t)rn + 1);
     unsigned *ns = (unsigned *)amgd_alloc(16);
@@ -1575,7 +1575,7 @@ static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, 
     amgd_d2h(ro.data(), Wt->ro, ((size_t)Wt->rn + 1) * 8);
     amgd_d2h(qo.data(), qoff, ((size_t)Wt->rn + 1) * 8);
     std::vector<uint32_t> keep;
-    double *scr = (double *)amgd_alloc(2 * rs.maxnz * 8 + 16);
+    double *scr = (double *)amgd_alloc_f64(2 * rs.maxnz * 8 + 16);
     for (uint32_t c : bl) {
       const uint32_t nz = (uint32_t)(ro[c + 1] - ro[c]);
       if (nz <= g_qa_huge) { keep.push_back(c); continue; }
@@ -1634,7 +1634,7 @@ static void qapply_range(const dcsr *Wt, const double *Q, const uint64_t *qoff, 
   if (rs.nb) {
     int g = (int)std::min<unsigned>(rs.nb, 1024u);
     uint64_t stride = 2 * rs.maxnz + 8;
-    double *scr = (double *)amgd_alloc((size_t)g * stride * 8);
+    double *scr = (double *)amgd_alloc_f64((size_t)g * stride * 8);
     k_qapply<256, true><<<g, 256, 0, s>>>(rs.bl, rs.nb, Wt->ro, Wt->col, Q, qoff, Bt->ro, Bt->col,
                                           Bt->a, u, lambda, out, scr, stride);
     amgd_free(scr);
@@ -2130,7 +2130,7 @@ static bool lmop_pruned(dcsr *S, const dcsr *Wt, const double *Q, uint64_t qo, u
   const uint64_t n = amgd_scan_u64(koff, nz);
   amgd_free(hs); amgd_free(skey);
   uint64_t *k1 = (uint64_t *)amgd_alloc(n * 8 + 8), *k2 = (uint64_t *)amgd_alloc(n * 8 + 8);
-  double *v1 = (double *)amgd_alloc(n * 8 + 8), *v2 = (double *)amgd_alloc(n * 8 + 8);
+  double *v1 = (double *)amgd_alloc_f64(n * 8 + 8), *v2 = (double *)amgd_alloc_f64(n * 8 + 8);
   k_lmop_land_pr<<<grid_for(nz, 64, 65536), 64, 0, s>>>(Wt->col + w0, nz, S->ro, S->col, S->rn,
                                                        S->nnz, rmax, b64, b4k, compid, rank,
                                                        koff, k1);
@@ -2179,7 +2179,7 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
   }
   const uint64_t CH = std::max<uint64_t>(1, std::min<uint64_t>(hcoff[ce] - hcoff[cb], 1ull << 26));
   uint64_t *key = (uint64_t *)amgd_alloc(CH * 8 + 8), *key2 = (uint64_t *)amgd_alloc(CH * 8 + 8);
-  double *val = (double *)amgd_alloc(CH * 8 + 8), *val2 = (double *)amgd_alloc(CH * 8 + 8);
+  double *val = (double *)amgd_alloc_f64(CH * 8 + 8), *val2 = (double *)amgd_alloc_f64(CH * 8 + 8);
   size_t tb = 0;
   int eb = 1;
   while (eb < 64 && (S->nnz >> eb) != 0) eb++;   // keys are 0..S->nnz
@@ -2212,7 +2212,7 @@ extern "C" void amgd_lmop_general(dcsr *S, const dcsr *Wt, const double *Q, cons
     if (n > CH) {   // one huge support: grow buffers for it
       amgd_free(key); amgd_free(key2); amgd_free(val); amgd_free(val2); amgd_free(tmp);
       key = (uint64_t *)amgd_alloc(n * 8); key2 = (uint64_t *)amgd_alloc(n * 8);
-      val = (double *)amgd_alloc(n * 8); val2 = (double *)amgd_alloc(n * 8);
+      val = (double *)amgd_alloc_f64(n * 8); val2 = (double *)amgd_alloc_f64(n * 8);
       tb = 0;
       HIPCK(rocprim::radix_sort_pairs(nullptr, tb, key, key2, val, val2, (size_t)n, 0, eb, s));
       tmp = amgd_alloc(tb + 16);
@@ -2801,7 +2801,7 @@ extern "C" uint64_t amgd_expand_pick(const dcsr *Xf, const uint8_t *bad, uint32_
                                      uint32_t **pj) {
   hipStream_t s = amgd_s();
   uint32_t *scol = (uint32_t *)amgd_alloc(Xf->nnz * 4 + 4);
-  double *sval = (double *)amgd_alloc(Xf->nnz * 8 + 8);
+  double *sval = (double *)amgd_alloc_f64(Xf->nnz * 8 + 8);
   uint32_t *tj = (uint32_t *)amgd_alloc(Xf->nnz * 4 + 4);
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)Xf->rn + 1) * 8);
   if (Xf->rn) {

@@ -534,7 +534,7 @@ extern "C" int amgd_lmop(dcsr *S, const dcsr *Wskel, const uint32_t *kpos, const
     while (cb < nc && hsz[cb + 1] - hsz[ca] <= budget) cb++;
     const uint64_t need = hsz[cb] - hsz[ca];
     if (need == 0) { ca = cb; continue; }
-    double *QQ = (double *)amgd_alloc(need * 8 + 8);
+    double *QQ = (double *)amgd_alloc_f64(need * 8 + 8);
     const double *QQb = QQ - hsz[ca];     // qqoff (= sz prefix) is global: rebase
     // small supports
     k_qq_small<<<(int)std::min<uint32_t>(cb - ca, 65536u), 64, 0, s>>>(Wt->ro, dirty, ca, cb, Q,

@@ -168,7 +168,7 @@ extern "C" void pm_list_sync_n(int nv, double *const *z, const uint32_t *const *
     off[(size_t)(2 * v + 1) * (N + 1) + N] = 8 * t;
     tot[v] = t;
     oi[v] = (uint32_t *)amgd_alloc(4 * t + 8);
-    ov[v] = (double *)amgd_alloc(8 * t + 8);
+    ov[v] = (double *)amgd_alloc_f64(8 * t + 8);
     bufs[2 * v] = oi[v];
     bufs[2 * v + 1] = ov[v];
     const uint64_t at = off[(size_t)(2 * v) * (N + 1) + me] / 4;
@@ -202,7 +202,20 @@ __global__ void k_eager_hdr(const uint64_t *rec, int N, uint64_t rs8, uint64_t *
   if (p < N) { out[2 * p] = rec[p * rs8]; out[2 * p + 1] = rec[p * rs8 + 1]; }
 }
 static uint64_t g_eager_gen = 1;
+static uint64_t g_eager_calls = 0, g_eager_second = 0;
 extern "C" void pm_eager_new_setup(void) { g_eager_gen++; }
+// AMGD_EAGER_SLOT=<bytes> / pm_eager_force_slot (tests): every call site's slot fixed at that
+// size (>= 8), below the usual shares, so the exact second round runs on nearly every call
+static int64_t g_eager_forced = -1;
+extern "C" void pm_eager_force_slot(int64_t bytes) { g_eager_forced = bytes; }
+static uint64_t eager_forced() {
+  if (g_eager_forced < 0) {
+    const char *e = getenv("AMGD_EAGER_SLOT");
+    g_eager_forced = e && *e ? atoll(e) : 0;
+  }
+  return g_eager_forced > 0 ? (uint64_t)(g_eager_forced < 8 ? 8 : g_eager_forced) : 0;
+}
+extern "C" void pm_eager_stats(uint64_t *calls, uint64_t *second) { *calls = g_eager_calls; *second = g_eager_second; }
 extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes, uint64_t user, uint64_t *len,
                                   uint64_t *users, uint64_t *total) {
   // slots adapt within one setup only: a rank's earlier setups must not change its record
@@ -217,6 +230,8 @@ extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes,
     return out;
   }
   if (e->slot == 0) e->slot = 4096;
+  if (eager_forced()) e->slot = eager_forced();
+  g_eager_calls++;
   const uint64_t slot = (e->slot + 7) & ~7ull, rs = 16 + slot;       // record bytes
   char *rec = (char *)amgd_alloc((uint64_t)N * rs + 8);
   const uint64_t hdr[2] = {bytes, user};
@@ -254,6 +269,7 @@ extern "C" char *pm_allgather_dyn(pm_eager *e, const void *mine, uint64_t bytes,
   }
   amgd_free(rec);
   if (over) {                          // the rest of the long shares, exactly
+    g_eager_second++;
     std::vector<uint64_t> ro(N + 1, 0);
     for (int p = 0; p < N; p++) ro[p + 1] = ro[p] + (len[p] > slot ? len[p] - slot : 0);
     char *rem = (char *)amgd_alloc(ro[N] + 8);
@@ -442,7 +458,7 @@ extern "C" pmat *pm_transpose(const pmat *A) {
   for (int q = 0; q < N; q++) rpre[q + 1] = rpre[q] + cnt[(size_t)q * N + me];
   const uint64_t nz = rpre[N];
   uint32_t *rcol = (uint32_t *)amgd_alloc(4 * nz + 8);
-  double *ra = (double *)amgd_alloc(8 * nz + 8);
+  double *ra = (double *)amgd_alloc_f64(8 * nz + 8);
   std::vector<uint64_t> s4(N + 1), r4(N + 1), s8(N + 1), r8(N + 1);
   for (int p = 0; p <= N; p++) {
     s4[p] = 4 * tro[p]; s8[p] = 8 * tro[p];
@@ -463,7 +479,7 @@ extern "C" pmat *pm_transpose(const pmat *A) {
   X->nnz = nz;
   X->ro = (uint64_t *)amgd_alloc(((size_t)nl + 1) * 8);
   X->col = (uint32_t *)amgd_alloc(4 * nz + 8);
-  X->a = (double *)amgd_alloc(8 * nz + 8);
+  X->a = (double *)amgd_alloc_f64(8 * nz + 8);
   if (nl) k_sum_lens<<<grid_for(nl), 256, 0, s>>>(rlens, N, nl, X->ro);
   KCHECK();
   amgd_scan_u64(X->ro, nl);
@@ -609,7 +625,7 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   }
   const bool cols = Bm->col != nullptr;     // NULL: a values-only pseudo-matrix (Q factors)
   uint32_t *scol = cols ? (uint32_t *)amgd_alloc(4 * nsend + 8) : nullptr;
-  double *sa = (double *)amgd_alloc(8 * nsend + 8);
+  double *sa = (double *)amgd_alloc_f64(8 * nsend + 8);
   if (nreq) k_req_copy<<<wave_rows_grid(nreq), 256, 0, s>>>(req, nreq, r0, Bm->ro, Bm->col, Bm->a, roff, scol, sa);
   KCHECK();
   // 5. the extended matrix: row offsets first, then the halo rows received straight into
@@ -628,7 +644,7 @@ extern "C" dcsr *pm_halo_rows(const pmat *B, const dcsr *L) {
   E->nnz = amgd_scan_u64(E->ro, n);
   const uint64_t ownnz = Bm->nnz;
   E->col = cols ? (uint32_t *)amgd_alloc(4 * E->nnz + 8) : nullptr;
-  E->a = (double *)amgd_alloc(8 * E->nnz + 8);
+  E->a = (double *)amgd_alloc_f64(8 * E->nnz + 8);
   std::vector<uint64_t> s4(N + 1), r4(N + 1), s8(N + 1), r8(N + 1);
   for (int p = 0; p <= N; p++) {
     const uint64_t at = rb[p] + (p > me ? ownnz : 0);
@@ -689,7 +705,7 @@ static dcsr *gather_rows(const pmat *A, bool vals) {
   F->rn = P->n; F->cn = A->m->cn; F->nnz = base[N];
   F->ro = (uint64_t *)amgd_alloc(((size_t)P->n + 1) * 8);
   F->col = cols ? (uint32_t *)amgd_alloc(base[N] * 4 + 4) : nullptr;
-  F->a = vals ? (double *)amgd_alloc(base[N] * 8 + 8) : nullptr;
+  F->a = vals ? (double *)amgd_alloc_f64(base[N] * 8 + 8) : nullptr;
   amgd_memset(F->ro, 0, 8);
   const uint32_t r0 = P->split[me], nl = A->m->rn;
   if (nl) k_ro_place<<<grid_for(nl), 256, 0, amgd_s()>>>(A->m->ro, nl, base[me], F->ro + r0 + 1);
@@ -820,7 +836,7 @@ extern "C" pmat *pm_coo_ones(const uint32_t *ri, const uint32_t *cj, uint64_t n,
   KCHECK();
   unsigned h = 0;
   amgd_d2h(&h, cnt, 4);
-  double *ones = (double *)amgd_alloc(8ull * h + 8);
+  double *ones = (double *)amgd_alloc_f64(8ull * h + 8);
   if (h) k_fill1<<<grid_for(h), 256, 0, amgd_s()>>>(ones, h);
   KCHECK();
   dcsr *X = amgd_coo2csr(h, oi, oj, ones, r1 - r0, cp->n, 1);
@@ -889,7 +905,7 @@ extern "C" uint64_t pm_route_coo(uint64_t nz, const uint32_t *I, const uint32_t 
     amgd_free(dp);
   }
   uint32_t *sI = (uint32_t *)amgd_alloc(4 * nz + 8), *sJ = (uint32_t *)amgd_alloc(4 * nz + 8);
-  double *sV = (double *)amgd_alloc(8 * nz + 8);
+  double *sV = (double *)amgd_alloc_f64(8 * nz + 8);
   if (nz) {
     k_permute<uint32_t><<<grid_for(nz), 256, 0, s>>>(I, perm, nz, sI);
     k_permute<uint32_t><<<grid_for(nz), 256, 0, s>>>(J, perm, nz, sJ);
@@ -905,7 +921,7 @@ extern "C" uint64_t pm_route_coo(uint64_t nz, const uint32_t *I, const uint32_t 
   const uint64_t m = rp[N];
   *Io = (uint32_t *)amgd_alloc(4 * m + 8);
   *Jo = (uint32_t *)amgd_alloc(4 * m + 8);
-  *Vo = (double *)amgd_alloc(8 * m + 8);
+  *Vo = (double *)amgd_alloc_f64(8 * m + 8);
   std::vector<uint64_t> s4(N + 1), r4(N + 1), s8(N + 1), r8(N + 1);
   for (int p = 0; p <= N; p++) { s4[p] = 4 * pos[p]; s8[p] = 8 * pos[p]; r4[p] = 4 * rp[p]; r8[p] = 8 * rp[p]; }
   amgd_pcomm_alltoallv(sI, s4.data(), *Io, r4.data());

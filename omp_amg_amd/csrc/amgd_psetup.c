@@ -39,7 +39,7 @@
 #include "amgd_part.h"
 #include "amgd_psetup.h"
 
-static double *dalloc(uint64_t n) { return (double *)amgd_alloc(n * 8 + 8); }
+static double *dalloc(uint64_t n) { return (double *)amgd_alloc_f64(n * 8 + 8); }
 static double *dones(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 1.0); return p; }
 static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0); return p; }
 
@@ -59,6 +59,19 @@ static int verbose(void) {
   return g_verbose && g_me == 0;
 }
 static uint64_t g_lmop_full;        /* interp_lmop calls done on gathered data */
+static uint64_t g_lmop_prefix;      /* interp_lmop calls with a dirty prefix walked on the whole S pattern */
+/* AMGD_PART_LMOP_GATHER=1 / amgd_part_force(1, ..): every interp_lmop of a partitioned setup
+   takes the gathered path (tests: the rare fallback exercised at every level) */
+static int g_force_gather = -1;
+static int force_gather(void) {
+  if (g_force_gather < 0) { const char *e = getenv("AMGD_PART_LMOP_GATHER"); g_force_gather = e && *e ? atoi(e) : 0; }
+  return g_force_gather;
+}
+void amgd_part_set_force_gather(int on) { g_force_gather = on; }
+void amgd_part_stats(uint64_t *out) {       /* lmop gathered calls, lmop prefix calls */
+  out[0] = g_lmop_full;
+  out[1] = g_lmop_prefix;
+}
 
 /* sum / OR / max of one u64 per rank, identical on every rank */
 static uint64_t all_sum(uint64_t v) {
@@ -513,6 +526,7 @@ static void p_lmop(pmat *S, const pmat *Wskel, pfactor *f, const double *u) {
   dl = dl ? f->Wt->rp->split[g_me] + dl : 0;
   const uint32_t D = (uint32_t)all_max(dl);
   if (D) {
+    g_lmop_prefix++;
     p_lmop_prefix(S, f, &qp, u, D);
     amgd_lmop_set_prefix(D);
   }
@@ -544,7 +558,7 @@ static void p_lmop(pmat *S, const pmat *Wskel, pfactor *f, const double *u) {
   amgd_lmop_set_prefix(0);
   pm_gview_free(&gS);
   pm_gview_free(&gW);
-  if (all_max((uint64_t)st) != 0) {
+  if (all_max((uint64_t)st) != 0 || force_gather()) {
     g_lmop_full++;
     dcsr *Sf = pm_gather_full(S), *Wsf = pm_gather_full(Wskel), *Qf = pm_gather_full(&qp);
     uint64_t *perm = NULL;
@@ -1054,6 +1068,7 @@ __attribute__((visibility("hidden"))) int amgd_psetup_body(uint64_t nz, const ui
   g_pst = st;
   g_plvl = 0;
   g_lmop_full = 0;
+  g_lmop_prefix = 0;
   (void)amgd_pool_ipeak_take();
   amgd_sync();
   double t_start = amgd_wtime(), t0 = t_start;

@@ -227,6 +227,17 @@ extern "C" void *amgd_alloc(size_t bytes) {
   return p;
 }
 
+// Arrays of doubles.  AMGD_POISON=1 (tests): every such block starts as all-ones bytes, a NaN
+// in every slot, instead of whatever the arena held -- a value read before it is written
+// then turns the hierarchy into NaNs (a digest mismatch) instead of passing by luck
+static int g_poison = -1;
+extern "C" void amgd_set_poison(int on) { g_poison = on; }
+extern "C" void *amgd_alloc_f64(size_t bytes) {
+  void *p = amgd_alloc(bytes);
+  if (g_poison < 0) { const char *e = getenv("AMGD_POISON"); g_poison = e && *e ? atoi(e) : 0; }
+  if (g_poison > 0 && bytes) HIPCK(hipMemsetAsync(p, 0xff, bytes, amgd_s()));
+  return p;
+}
 extern "C" void amgd_free(void *p) {
   if (!p) return;
   amgd_spmv_split_forget(p);
@@ -423,7 +434,7 @@ extern "C" dcsr *dcsr_new(uint32_t rn, uint32_t cn, uint64_t nnz) {
   A->rn = rn; A->cn = cn; A->nnz = nnz;
   A->ro = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
   A->col = (uint32_t *)amgd_alloc(nnz * 4 + 4);
-  A->a = (double *)amgd_alloc(nnz * 8 + 8);
+  A->a = (double *)amgd_alloc_f64(nnz * 8 + 8);
   return A;
 }
 extern "C" void dcsr_free(dcsr **A) {
@@ -1161,7 +1172,7 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
   hipStream_t st = amgd_s();
   const uint64_t gmax = max_entries / BN_TILE + nmax + 1;
   uint64_t *choff = (uint64_t *)amgd_alloc(((size_t)nmax + 1) * 8);
-  double *csum = (double *)amgd_alloc(gmax * 8);
+  double *csum = (double *)amgd_alloc_f64(gmax * 8);
   SpecRec *rec = (SpecRec *)amgd_alloc(gmax * sizeof(SpecRec));
   const int G = (int)std::min<uint64_t>(gmax, 1024);
   const int R = (int)std::min<uint32_t>(nmax, 256);
@@ -1189,7 +1200,7 @@ static void dot_exact_launch(const double *a, const double *b, uint64_t n, doubl
     return;
   }
   uint64_t G = (n + BN_TILE - 1) / BN_TILE;
-  double *csum = (double *)amgd_alloc(G * 8 + 8);
+  double *csum = (double *)amgd_alloc_f64(G * 8 + 8);
   SpecRec *rec = (SpecRec *)amgd_alloc(G * sizeof(SpecRec) + 64);
   int g = (int)std::min<uint64_t>(G, 8192);
   k_dot_csum<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum);

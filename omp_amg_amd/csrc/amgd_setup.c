@@ -32,7 +32,7 @@
 
 #define API __attribute__((visibility("default")))
 
-static double *dalloc(uint64_t n) { return (double *)amgd_alloc(n * 8 + 8); }
+static double *dalloc(uint64_t n) { return (double *)amgd_alloc_f64(n * 8 + 8); }
 static double *dones(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 1.0); return p; }
 static double *dzeros(uint64_t n) { double *p = dalloc(n); amgd_vfill(p, n, 0.0); return p; }
 #define SWAPD(a, b) do { double *t_ = (a); (a) = (b); (b) = t_; } while (0)
@@ -556,6 +556,7 @@ static dcsr *find_support(const dcsr *R, dcsr *Rt, uint64_t *perm, double goal, 
     if (theta == 0) { UB(1); break; }                   /* reference spins forever */
     if (nf <= 1) { UB(2); break; }                      /* maski = 1: never terminates */
     uint32_t nrem = 0;
+    if (amx_ok) amgd_route_hit(AMGD_R_FS_AMX);
     uint32_t nsel = amx_ok ? amgd_fs_select_amx(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, amx, si + ns,
                                                 sj + ns, &nrem)
                            : amgd_fs_select(Rl, Rt, perm, rs, w, sumR, (1 + theta) * goal, si + ns, sj + ns, &nrem);

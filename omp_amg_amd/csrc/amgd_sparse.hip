@@ -84,7 +84,7 @@ extern "C" dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J,
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
   HIPCK(hipMemsetAsync(cnt, 0, ((size_t)rn + 1) * 8, s));
   uint64_t *key = (uint64_t *)amgd_alloc(nz * 8 + 8), *key2 = (uint64_t *)amgd_alloc(nz * 8 + 8);
-  double *v2 = (double *)amgd_alloc(nz * 8 + 8);
+  double *v2 = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (nz) {
     k_coo_keys<<<grid_for(nz), 256, 0, s>>>(I, J, V, nz, rn, drop_zero, key, cnt);
     KCHECK();
@@ -100,7 +100,7 @@ extern "C" dcsr *amgd_coo2csr(uint64_t nz, const uint32_t *I, const uint32_t *J,
   A->rn = rn; A->cn = cn; A->nnz = kept;
   A->ro = cnt;
   A->col = (uint32_t *)amgd_alloc(kept * 4 + 4);
-  A->a = (double *)amgd_alloc(kept * 8 + 8);
+  A->a = (double *)amgd_alloc_f64(kept * 8 + 8);
   if (kept) {
     k_coo_split<<<grid_for(kept), 256, 0, s>>>(key2, v2, kept, A->col, A->a);
     KCHECK();
@@ -227,7 +227,7 @@ extern "C" dcsr *amgd_sub_mat(const dcsr *A, const uint8_t *vr, const uint8_t *v
   dcsr *S = (dcsr *)malloc(sizeof(dcsr));
   S->rn = srn; S->cn = scn; S->nnz = nz; S->ro = cnt;
   S->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  S->a = (double *)amgd_alloc(nz * 8 + 8);
+  S->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (A->rn && lr)
     k_sub_fill_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, vr, vc, rmap, cmap,
                                                       S->ro, S->col, S->a);
@@ -342,7 +342,7 @@ extern "C" dcsr *amgd_transpose(const dcsr *A, uint64_t **perm_out) {
   dcsr *T = (dcsr *)malloc(sizeof(dcsr));
   T->rn = A->cn; T->cn = A->rn; T->nnz = nz; T->ro = cnt;
   T->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  T->a = (double *)amgd_alloc(nz * 8 + 8);
+  T->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (nz) {
     uint32_t *row = (uint32_t *)amgd_alloc(nz * 4 + 4);
     if (long_rows(nz, A->rn)) k_row_of_entry_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->rn, row);
@@ -385,7 +385,7 @@ extern "C" dcsr *amgd_drop_zeros(const dcsr *A) {
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (A->rn && nz) k_nz_fill<<<grid_for(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, X->ro, X->col, X->a);
   KCHECK();
   return X;
@@ -422,7 +422,7 @@ extern "C" dcsr *amgd_rows_masked(const dcsr *A, const uint8_t *mask) {
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (A->rn && nz && long_rows(A->nnz, A->rn))
     k_rowmask_fill_wave<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, mask, X->ro,
                                                           X->col, X->a);
@@ -483,7 +483,7 @@ extern "C" dcsr *amgd_cols_masked(const dcsr *A, const uint8_t *mask) {
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (A->rn && nz)
     k_colmask_fill<<<wave_grid(A->rn), 256, 0, s>>>(A->ro, A->col, A->a, A->rn, mask, X->ro, X->col, X->a);
   KCHECK();
@@ -1682,7 +1682,7 @@ extern "C" dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (use_w)
     k_mpm_wave<true><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn, alpha,
                                         beta, lr, nullptr, X->ro, X->col, X->a);
@@ -1794,7 +1794,7 @@ extern "C" dcsr *amgd_mxmpoint(const dcsr *A, const dcsr *B) {
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = A->rn; X->cn = A->cn; X->nnz = nz; X->ro = cnt;
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   if (A->rn && wave)
     k_pointwise_wave<true><<<gw, 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a, A->rn,
                                               nullptr, X->ro, X->col, X->a);
@@ -2781,7 +2781,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   const uint32_t *densel = lists + 4 * L;
   int nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
   if (hn[4]) {                    // recount (rows past the hash capacity carry OVERFLOW_MARK)
-    slab_v = (double *)amgd_alloc((size_t)nlb * B->cn * 8 + 8);
+    slab_v = (double *)amgd_alloc_f64((size_t)nlb * B->cn * 8 + 8);
     slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
     HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
     k_spgemm_long<0><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col, B->a,
@@ -2790,7 +2790,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
   uint64_t dist = amgd_scan_u64(cnt, rn);   // cnt := offsets of the distinct layout
   uint32_t *tcol = (uint32_t *)amgd_alloc(dist * 4 + 4);
-  double *ta = (double *)amgd_alloc(dist * 8 + 8);
+  double *ta = (double *)amgd_alloc_f64(dist * 8 + 8);
   uint64_t *cnt2 = (uint64_t *)amgd_alloc(L * 8);
   HIPCK(hipMemsetAsync(cnt2, 0, L * 8, s));
   if (hn[4]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
@@ -2918,7 +2918,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   } else {                        // compact away exact-zero sums
     X->ro = cnt2;
     X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-    X->a = (double *)amgd_alloc(nz * 8 + 8);
+    X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
     amgd_compact_rows(cnt, tcol, ta, cnt2, rn, X->col, X->a);
     amgd_free(cnt); amgd_free(tcol); amgd_free(ta);
   }
@@ -3002,7 +3002,7 @@ extern "C" dcsr *amgd_spgemm(const dcsr *A, const dcsr *B) {
   X->nnz = nz;
   X->ro = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
   X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
-  X->a = (double *)amgd_alloc(nz * 8 + 8);
+  X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
   hipStream_t s = amgd_s();
   HIPCK(hipMemsetAsync(X->ro, 0, 8, s));
   for (int q = f; q < l; q++) {
@@ -3136,7 +3136,7 @@ extern "C" dcsr *amgd_bench_matrix(uint32_t rn, uint32_t cn, uint32_t len0, uint
   dcsr *A = (dcsr *)malloc(sizeof(dcsr));
   A->rn = rn; A->cn = cn; A->nnz = nnz; A->ro = ro;
   A->col = (uint32_t *)amgd_alloc(nnz * 4 + 4);
-  A->a = (double *)amgd_alloc(nnz * 8 + 8);
+  A->a = (double *)amgd_alloc_f64(nnz * 8 + 8);
   k_bench_fill<<<grid_for(rn), 256, 0, s>>>(ro, rn, cn, gap, A->col, A->a);
   KCHECK();
   return A;

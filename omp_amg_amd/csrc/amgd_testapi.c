@@ -247,6 +247,17 @@ API void amgd_test_fs_amx(int on) { amgd_fs_set_amx(on); }
 extern void amgd_qa_set_tile(int t);
 API void amgd_test_qa_tile(int t) { amgd_qa_set_tile(t); }
 API void amgd_test_d2h_poll(int on) { amgd_set_d2h_poll(on); }
+/* partitioned setup: [interp_lmop calls on gathered data, calls with a dirty prefix,
+   eager exchanges, eager exchanges that took the exact second round] of the last setup(s) */
+API void amgd_test_part_stats(uint64_t *out) {
+  amgd_part_stats(out);
+  pm_eager_stats(out + 2, out + 3);
+}
+/* forced rare paths: every interp_lmop on gathered data; a fixed eager slot (bytes, 0: adaptive) */
+API void amgd_test_part_force(int lmop_gather, int64_t eager_slot) {
+  amgd_part_set_force_gather(lmop_gather);
+  pm_eager_force_slot(eager_slot);
+}
 API void amgd_test_spmv_rw_bounds(int lo, int hi) { amgd_spmv_set_rw_bounds(lo, hi); }
 API void amgd_test_spmv_pair(int on) { amgd_spmv_set_pair(on); }
 extern void amgd_qfactor_set_coop_lds(int m);

@@ -127,3 +127,66 @@ def compare(h1: Hierarchy, h2: Hierarchy, *, exact: bool = True, rtol: float = 1
             if not ok:
                 bad.append(f"L{l}.{f} values err={err:.3g}")
     return bad
+
+
+def first_diff(h1: Hierarchy, h2: Hierarchy) -> list[dict]:
+    """Every differing array of two hierarchies with its first differing position: for a
+    CSR, the first row whose offsets, columns or values differ, with both rows' (column,
+    value) lists from the first differing entry on (a few each); for a vector, the first
+    index and both values.  Used by the partitioned tests' failure reports."""
+    out: list[dict] = []
+    nl = min(h1.nlevels, h2.nlevels)
+    if h1.nlevels != h2.nlevels:
+        out.append({"what": "nlevels", "a": int(h1.nlevels), "b": int(h2.nlevels)})
+    for l in range(nl):
+        a, b = h1.levels[l], h2.levels[l]
+        for f in _VEC_FIELDS:
+            x, y = getattr(a, f), getattr(b, f)
+            if x is None or y is None:
+                if (x is None) != (y is None):
+                    out.append({"what": f"L{l}_{f}", "missing": "a" if x is None else "b"})
+                continue
+            x, y = np.asarray(x), np.asarray(y)
+            if x.shape != y.shape:
+                out.append({"what": f"L{l}_{f}", "len": [int(x.size), int(y.size)]})
+                continue
+            xv = x.view(np.uint64) if x.dtype == np.float64 else x
+            yv = y.view(np.uint64) if y.dtype == np.float64 else y
+            d = np.nonzero(xv != yv)[0]
+            if d.size:
+                i = int(d[0])
+                out.append({"what": f"L{l}_{f}", "count": int(d.size), "index": i,
+                            "a": x[i].item(), "b": y[i].item()})
+        for f in _CSR_FIELDS:
+            x, y = getattr(a, f), getattr(b, f)
+            if x is None or y is None:
+                if (x is None) != (y is None):
+                    out.append({"what": f"L{l}_{f}", "missing": "a" if x is None else "b"})
+                continue
+            if (x.rn, x.cn) != (y.rn, y.cn):
+                out.append({"what": f"L{l}_{f}", "shape": [[x.rn, x.cn], [y.rn, y.cn]]})
+                continue
+            ro1, ro2 = x.row_off.astype(np.int64), y.row_off.astype(np.int64)
+            bad_rows = []
+            for r in range(x.rn):
+                s1, e1, s2, e2 = ro1[r], ro1[r + 1], ro2[r], ro2[r + 1]
+                if e1 - s1 != e2 - s2 or not np.array_equal(x.col[s1:e1], y.col[s2:e2]) or \
+                        not np.array_equal(x.a[s1:e1].view(np.uint64), y.a[s2:e2].view(np.uint64)):
+                    bad_rows.append(r)
+                    if len(bad_rows) > 64:
+                        break
+            if not bad_rows:
+                continue
+            r = bad_rows[0]
+            s1, e1, s2, e2 = ro1[r], ro1[r + 1], ro2[r], ro2[r + 1]
+            c1, c2 = x.col[s1:e1], y.col[s2:e2]
+            v1, v2 = x.a[s1:e1], y.a[s2:e2]
+            k = 0
+            while k < min(len(c1), len(c2)) and c1[k] == c2[k] and v1[k].view(np.uint64) == v2[k].view(np.uint64):
+                k += 1
+            out.append({"what": f"L{l}_{f}", "first_row": int(r), "rows_differing_at_least": len(bad_rows),
+                        "row_len": [int(e1 - s1), int(e2 - s2)], "entry": int(k),
+                        "a": [[int(c), float(v)] for c, v in zip(c1[k:k + 4], v1[k:k + 4])],
+                        "b": [[int(c), float(v)] for c, v in zip(c2[k:k + 4], v2[k:k + 4])],
+                        "pattern_same": bool(np.array_equal(ro1, ro2) and np.array_equal(x.col, y.col))})
+    return out

@@ -50,6 +50,10 @@ def main():
         shard.init_host(rank, size)
     if not os.environ.get("PART_DEFAULT"):     # PART_DEFAULT: crs_setup's own default (partitioned)
         oa.lib().amgd_comm_set_partitioned(1)
+    # forced rare paths (tests): every interp_lmop on gathered data; a fixed eager slot
+    L.amgd_test_part_force.argtypes = [C.c_int, C.c_int64]
+    L.amgd_test_part_force(int(os.environ.get("PART_LMOP_GATHER", "0")),
+                           int(os.environ.get("PART_EAGER_SLOT", "0")))
     shard.stats(reset=True)
     Ai64, Aj64, Av = np.asarray(Ai, np.int64), np.asarray(Aj, np.int64), np.asarray(Av)
     guard = os.environ.get("PART_GUARD")
@@ -130,7 +134,11 @@ def main():
         ds.close()
     st = shard.stats()
     out["peak_bytes"] = int(oa.stats()["peak_bytes"])
-    shard.free()
+    ps = (C.c_uint64 * 4)()
+    L.amgd_test_part_stats(ps)
+    out["lmop_gathered"], out["lmop_prefix"], out["eager_calls"], out["eager_second"] = (int(v) for v in ps)
+    rs = oa.route_stats()
+    out["routes"] = {k: v for k, v in rs.items() if v}
     out["leak_bytes"] = int(L.amgd_test_pool_inuse()) - int(before)
     if ref is not None:
         bad = parity.compare(ref, h, exact=True)
@@ -139,7 +147,15 @@ def main():
         got = md.hierarchy_digest(h)
         exp = digest["arrays"]
         bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
-    out.update(calls=st["calls"], bytes=st["bytes"], bad=bad[:5], levels=h.nlevels)
+        if bad:
+            # every differing array with its first differing row / entry against the one-GPU
+            # setup of the whole matrix (amg_setup takes the whole matrix and makes no
+            # exchange under any communicator; the one-GPU hierarchy is the digest's)
+            h1 = abi.run_setup(oa.lib(), Ai64, Aj64, Av)
+            ok1 = md.hierarchy_digest(h1) == exp
+            out["one_gpu_matches_digest"] = ok1
+            out["first_diff"] = parity.first_diff(h1, h)
+    out.update(calls=st["calls"], bytes=st["bytes"], bad=bad, levels=h.nlevels)
     print(json.dumps(out), flush=True)
     dist.destroy_process_group()
     sys.exit(0 if not bad and st["calls"] > 0 and out["leak_bytes"] == 0 else 1)

@@ -47,11 +47,11 @@ EXPECT_ROUTES = {
     "p7_48": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
               "qf_reuse"),
     "p7_64": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
-              "qf_reuse"),
+              "qf_reuse", "mv_pair", "fs_amx"),
     "p7_96": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024"),
+              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx"),
     "p7_128": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024"),
+               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx"),
     "aniso_20": ("fs_inc",),
     "aniso_32": ("fs_inc", "spmv_pipe"),
     "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin", "sg_wwin_sym"),
@@ -91,10 +91,12 @@ def test_gpu_matches_digest_unfused_selection(case):
     d = _db()["cases"][case]
     Ai, Aj, Av = mk.generate(d["gen"])
     oa.fs_amx(0)
+    oa.route_stats(reset=True)
     try:
         h = abi.run_setup(oa.lib(), Ai, Aj, Av)
     finally:
         oa.fs_amx(-1)
+    assert oa.route_stats(reset=True)["fs_amx"] == 0
     got = mk.hierarchy_digest(h)
     exp = d["arrays"]
     bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))

@@ -49,12 +49,16 @@ def _run(size, case, crs="", timeout=110, extra_env=None):
     res = []
     if any(rc != 0 for rc, _, _ in outs):
         # every rank's tail: the first failing rank is usually not rank 0
-        raise AssertionError("\n".join(f"--- rank {r} rc={rc}\n{o[-1500:]}\n{e}" for r, (rc, o, e) in enumerate(outs)))
+        # the whole last line of each rank: the full list of differing arrays and, for digest
+        # cases, the first differing row of each against the one-GPU setup (part_worker.py)
+        raise AssertionError("\n".join(f"--- rank {r} rc={rc}\n{o[-30000:]}\n{e}" for r, (rc, o, e) in enumerate(outs)))
     for rc, o, e in outs:
         assert rc == 0, (o[-2000:], e)
         d = json.loads(o.strip().splitlines()[-1])
         assert not d["bad"] and d["calls"] > 0 and d["leak_bytes"] == 0, d
         res.append(d)
+    print(size, case, json.dumps({k: res[0].get(k) for k in ("calls", "lmop_gathered", "lmop_prefix",
+                                                              "eager_calls", "eager_second", "levels")}))
     return res
 
 
@@ -88,6 +92,24 @@ def test_partitioned_eight_ranks(case):
     (configs[3]'s stencil: the densified levels, interp_lmop's dirty points past clean
     ones -- the reference-checked hierarchy)"""
     _run(8, case, timeout=240)
+
+
+@pytest.mark.parametrize("force", ["lmop_gather", "eager_slot"])
+def test_partitioned_forced_rare_paths(force):
+    """the r05t1 case (4 ranks, incremental sweeps, 7-point 64^3) with a rare path forced
+    at every call: interp_lmop redone on gathered data (its fallback when a view walk
+    spills or a clean contribution misses: 0 calls at 128^3 by default), or an 8-byte eager
+    slot, so every variable-length exchange (BFS hops, find_support expansions and
+    selections) that moves more than 8 bytes takes the exact second round -- the stored
+    digest either way, with the forced path counted on every rank"""
+    env = {"AMGD_CS_INC": "1", "AMGD_FS_INC": "1"}
+    env.update({"PART_LMOP_GATHER": "1"} if force == "lmop_gather" else {"PART_EAGER_SLOT": "8"})
+    res = _run(4, "digest:p7_64", timeout=240, extra_env=env)
+    for d in res:
+        if force == "lmop_gather":
+            assert d["lmop_gathered"] > 0, d
+        else:
+            assert d["eager_second"] > 0 and 2 * d["eager_second"] > d["eager_calls"], d
 
 
 def test_partitioned_crs_setup():
