@@ -57,6 +57,13 @@ static uint64_t g_bytes = 0, g_calls = 0;
 static uint64_t g_kstat[3][2];
 static int g_kind_small = 0;
 static int g_inner = 0;        // host-transport alltoallv staging: its allgathervs are not counted
+// set for a scope, restored on every exit -- also when a peer's FAIL record unwinds the setup
+// through amgd_throw_oom inside the scope (a stuck flag would stop counting collectives)
+struct FlagScope {
+  int &f, old;
+  explicit FlagScope(int &flag) : f(flag), old(flag) { f = 1; }
+  ~FlagScope() { f = old; }
+};
 static uint64_t g_seq = 0, g_guard_calls = 0;   // collective guard: records exchanged (below)
 static double g_ms = 0;
 
@@ -412,7 +419,9 @@ void amgd_allgatherv_(int nbuf, void *const *bufs, const uint64_t *off) {
     }
     NCCK(R.GroupEnd());
     // no host sync: the send/recv pairs run on the library stream, so every consumer
-    // (kernels, copies, frees of the arena) is ordered after them already
+    // (kernels, copies, frees of the arena) is ordered after them already.  So on RCCL
+    // g_ms (amgd_comm_stats' ms) is the host's enqueue time only, not the transfer time;
+    // with more than one rank this stream-ordered path is unverified until an 8-GPU run
   }
   g_ms += (amgd_wtime() - t0) * 1e3;
 }
@@ -497,9 +506,10 @@ void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m) {
   std::vector<uint64_t> off(N + 1);
   for (int s = 0; s <= N; s++) off[s] = 8ull * s * m;
   void *b = d;
-  g_kind_small = 1;
-  amgd_allgatherv(1, &b, off.data());
-  g_kind_small = 0;
+  {
+    FlagScope small_(g_kind_small);
+    amgd_allgatherv(1, &b, off.data());
+  }
   amgd_d2h(vals_h, d, 8ull * N * m);
   amgd_free(d);
 }
@@ -514,7 +524,7 @@ void amgd_pcomm_allgather_u64_(uint64_t *vals_h, int m) {
 // rank (r - k) mod N -- staging per round ~1/N of the data, not all of it
 static void a2a_host(const void *send, const uint64_t *soff, void *recv, const uint64_t *roff) {
   const int N = amgd_pcomm_size(), me = amgd_pcomm_rank();
-  g_inner = 1;
+  FlagScope inner_(g_inner);
   std::vector<uint64_t> so((size_t)N * (N + 1));
   uint64_t *dt = (uint64_t *)amgd_alloc(8ull * N * (N + 1) + 8);
   amgd_h2d(dt + (size_t)me * (N + 1), soff, 8ull * (N + 1));
@@ -556,7 +566,6 @@ static void a2a_host(const void *send, const uint64_t *soff, void *recv, const u
     amgd_sync();
     amgd_free(stage);
   }
-  g_inner = 0;
 }
 
 // nb personalised exchanges in one collective (RCCL: one group of send/recv pairs)

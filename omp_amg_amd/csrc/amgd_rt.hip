@@ -317,8 +317,25 @@ static bool pub_ready() {
 // (A/B, tests) 0: blocking copies, 1: polled, -1: as AMGD_D2H_POLL says
 extern "C" void amgd_set_d2h_poll(int on) {
   if (on == 0) { if (g_pub_on < 0) pub_ready(); if (g_pub_on > 0) g_pub_on = 2; return; }
-  if (g_pub_on == 2) g_pub_on = 1;
-  (void)on;
+  if (on == 1) {                        // polled, whatever AMGD_D2H_POLL said
+    if (!g_pub) {
+      void *p = nullptr;
+      if (hipHostMalloc(&p, 64 + PUB_MAX, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        g_pub_on = 0;
+        return;
+      }
+      g_pub = (uint8_t *)p;
+      memset(g_pub, 0, 64 + PUB_MAX);
+      g_pub_seq = 0;
+    }
+    g_pub_on = 1;
+    return;
+  }
+  g_pub_on = -1;                        // -1: as the environment says (re-read on next use)
+  if (g_pub) g_pub_on = 1;
+  const char *e = getenv("AMGD_D2H_POLL");
+  if (e && *e == '0') g_pub_on = g_pub ? 2 : 0;
 }
 extern "C" void amgd_d2h(void *h, const void *d, size_t n) {
   if (n && n <= PUB_MAX && pub_ready() && g_pub_on == 1) {

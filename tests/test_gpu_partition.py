@@ -28,7 +28,10 @@ def _spawn(size, case, crs="", extra_env=None):
     port = _free_port()
     # every partitioned test runs with the collective-consistency guard on
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(size),
-               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_ARENA_GB="8", AMGD_COMM_CHECK="1",
+               PART_CASE=case, PART_CRS=crs, PYTHONPATH=ROOT, AMGD_COMM_CHECK="1",
+               # PART_ARENA_GB: each rank's arena (0: every block from hipMalloc, the mode a
+               # rank falls into when the GPU has too little free memory for an arena)
+               AMGD_ARENA_GB=os.environ.get("PART_ARENA_GB", "8"),
                **(extra_env or {}))
     return [subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "part_worker.py")],
                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
