@@ -268,6 +268,33 @@ def test_spmv_f(A: abi.Csr, x=None, alpha=0.0, y=None, beta=1.0, f=None):
     return z
 
 
+def test_spmv_tab(A: abi.Csr, x, alpha=0.0, y=None, beta=1.0, f=None, amx=False):
+    """amgd_spmv on a pinned matrix: the gather-table kernel (k_spmv_tab).  Returns
+    (z, amx or None, {builds, tiles, direct})"""
+    init()
+    L = lib()
+    L.amgd_test_spmv_tab.argtypes = [C.POINTER(HCsr), C.c_void_p, C.c_double, C.c_void_p, C.c_double,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    ha = _to_hcsr(A.row_off, A.col, A.a, A.rn, A.cn)
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    yy = None if y is None else np.ascontiguousarray(y, dtype=np.float64)
+    ff = None if f is None else np.ascontiguousarray(f, dtype=np.uint8)
+    z = np.zeros(A.rn)
+    m = np.zeros(A.rn, dtype=np.uint64) if amx else None
+    st = np.zeros(3, dtype=np.uint64)
+    rc = L.amgd_test_spmv_tab(C.byref(ha), xx.ctypes.data, alpha, None if yy is None else yy.ctypes.data, beta,
+                              None if ff is None else ff.ctypes.data, z.ctypes.data,
+                              None if m is None else m.ctypes.data, st.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"amgd_test_spmv_tab failed rc={rc}")
+    return z, m, {"builds": int(st[0]), "tiles": int(st[1]), "direct": int(st[2])}
+
+
+def spmv_tab(on: int) -> None:
+    """gather tables for pinned long-row matrices (1 default, 0 off, -1 environment)"""
+    lib().amgd_test_spmv_tab_on(int(on))
+
+
 def test_spmv_rows(A: abi.Csr, rows, x=None, z0=None):
     """amgd_spmv_rows: products (x None: ordered sums) of the listed rows only; the
     other entries of z keep z0"""
@@ -404,7 +431,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024", "mv_pair", "fs_amx")
+          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab")
 
 
 def route_stats(reset: bool = True) -> dict:

@@ -178,6 +178,7 @@ extern "C" int amgd_try(int (*fn)(void *), void *arg) {
   } catch (const amgd_oom_error &) {
     rc = -2;
     (void)hipDeviceSynchronize();      // the side stream of the Q factors as well
+    amgd_spmv_split_clear();           // cached SpMV splits, pins and gather tables first
     std::vector<void *> live;
     for (auto &u : g_used)
       if (u.second.serial >= mark) live.push_back(u.first);

@@ -978,6 +978,407 @@ __global__ __launch_bounds__(256) void k_spmv_pair_amx(const uint64_t *ro, const
   spmv_pair_body<false, RW, PER, 2, 1, 2, true>(ro, col, a, n, nullptr, x, z, 0.0, nullptr, 1.0, nullptr,
                                                 0xffffffffu, amx);
 }
+// ---------------------------------------------------------------------------
+// Tabled long-row SpMV (round 6).  The lane kernels above are bound by texture-address
+// work on the x gathers: ~30 distinct 128-B lines per 64-lane gather instruction, TA busy
+// 87-96 % (profiles/r05/mvctr/).  But a tile of consecutive rows gathers from few
+// distinct x entries: at 256^3, 256 rows of level 1's R gather 2.7-3.3 K distinct columns
+// for 11-15 K entries (~250 lines), 16-64 rows of levels 3-5 3-7 K for 20-120 K entries
+// (profiles/r06/mvstat256_r06d.txt, AMGD_MVSTAT=1).  find_support multiplies the same
+// patterns 35-240 times per call (only values change: removed entries are zeroed), so
+// per pinned matrix (amgd_rowmax_pin) the rows are cut into tiles of TR rows and for each
+// tile its distinct columns (ascending: `tab`) and, per entry, the 16-bit slot of its
+// column in them are built once (k_tab_count / k_tab_fill: a bit map over the tile's
+// column span in LDS).  A product then loads the tile's x[tab] into LDS once (sorted
+// columns: whole lines) and every entry gathers xs[slot] from LDS instead of x[col] --
+// the same value, so the same products summed in the same order (the lane kernel's
+// rounds, rows and ordered adds are unchanged): bit-identical.  Entry stream: 8 B value +
+// 2 B slot instead of 8 B + 4 B.  A tile whose distinct columns exceed the LDS table, or
+// whose column span exceeds the build's bit map, runs the plain gathers ("direct").
+// AMGD_MV_TAB=0 / amgd_spmv_set_tab(0): off.
+// ---------------------------------------------------------------------------
+#define TAB_BM_WORDS 16384                // build bit map: 524288 columns of span
+#define TAB_DIRECT 0xffffffffu
+template <int RW> struct TabShape;
+template <> struct TabShape<64> { static constexpr int PER = 16, TMAX = 5120; };
+template <> struct TabShape<16> { static constexpr int PER = 16, TMAX = 5632; };
+template <> struct TabShape<4> { static constexpr int PER = 8, TMAX = 7680; };
+// per tile: distinct columns (or TAB_DIRECT) and the smallest column
+__global__ __launch_bounds__(256) void k_tab_count(const uint64_t *ro, const uint32_t *col, uint32_t n,
+                                                   uint32_t TR, uint32_t ntiles, uint32_t tmax,
+                                                   uint32_t *nd_out, uint2 *span_out) {
+  extern __shared__ uint32_t bm[];                // TAB_BM_WORDS
+  __shared__ uint32_t red[4][2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t r0 = t * TR, r1 = min(n, r0 + TR);
+    uint32_t lo = 0xffffffffu, hi = 0;
+    for (uint32_t r = r0 + tid; r < r1; r += 256)
+      if (ro[r + 1] > ro[r]) { lo = min(lo, col[ro[r]]); hi = max(hi, col[ro[r + 1] - 1]); }
+    for (int o = 32; o; o >>= 1) { lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64)); hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64)); }
+    if (lane == 0) { red[w][0] = lo; red[w][1] = hi; }
+    __syncthreads();
+    lo = min(min(red[0][0], red[1][0]), min(red[2][0], red[3][0]));
+    hi = max(max(red[0][1], red[1][1]), max(red[2][1], red[3][1]));
+    __syncthreads();
+    uint32_t nd = 0;
+    if (lo <= hi) {
+      const uint64_t span = (uint64_t)hi - lo + 1;
+      if (span > 32ull * TAB_BM_WORDS) {
+        nd = TAB_DIRECT;
+      } else {
+        const uint32_t nw = (uint32_t)((span + 31) >> 5);
+        for (uint32_t q = tid; q < nw; q += 256) bm[q] = 0;
+        __syncthreads();
+        for (uint64_t k = ro[r0] + tid; k < ro[r1]; k += 256) {
+          const uint32_t c = col[k] - lo;
+          atomicOr(&bm[c >> 5], 1u << (c & 31));
+        }
+        __syncthreads();
+        uint32_t s = 0;
+        for (uint32_t q = tid; q < nw; q += 256) s += __popc(bm[q]);
+        for (int o = 32; o; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o, 64);
+        if (lane == 0) red[w][0] = s;
+        __syncthreads();
+        nd = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        if (nd > tmax) nd = TAB_DIRECT;
+        __syncthreads();
+      }
+    }
+    if (tid == 0) { nd_out[t] = nd; span_out[t] = make_uint2(lo, hi); }
+  }
+}
+// tab (the tile's distinct columns, ascending) and every entry's slot in it
+__global__ __launch_bounds__(256) void k_tab_fill(const uint64_t *ro, const uint32_t *col, uint32_t n,
+                                                  uint32_t TR, uint32_t ntiles, const uint32_t *nd_in,
+                                                  const uint2 *span_in, const uint64_t *toff,
+                                                  uint32_t *tab, uint16_t *slot) {
+  extern __shared__ uint32_t tab_sh[];         // bm[TAB_BM_WORDS] then pre (u16)[TAB_BM_WORDS]
+  uint32_t *bm = tab_sh;
+  uint16_t *pre = reinterpret_cast<uint16_t *>(tab_sh + TAB_BM_WORDS);
+  __shared__ uint32_t wtot[4];
+  const int tid = threadIdx.x;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t nd = nd_in[t];
+    if (nd == 0 || nd == TAB_DIRECT) continue;            // uniform per block
+    const uint32_t r0 = t * TR, r1 = min(n, r0 + TR), lo = span_in[t].x, hi = span_in[t].y;
+    const uint32_t nw = (hi - lo + 32) >> 5;
+    for (uint32_t q = tid; q < nw; q += 256) bm[q] = 0;
+    __syncthreads();
+    const uint64_t e0 = ro[r0], e1 = ro[r1];
+    for (uint64_t k = e0 + tid; k < e1; k += 256) {
+      const uint32_t c = col[k] - lo;
+      atomicOr(&bm[c >> 5], 1u << (c & 31));
+    }
+    __syncthreads();
+    // exclusive prefix of the words' popcounts: contiguous chunks per thread, then a block scan
+    const uint32_t per = (nw + 255) / 256, q0 = min(nw, tid * per), q1 = min(nw, q0 + per);
+    uint32_t s = 0;
+    for (uint32_t q = q0; q < q1; q++) s += __popc(bm[q]);
+    const uint32_t incl = block_incl_scan<256>(s, wtot);
+    uint32_t run = incl - s;
+    for (uint32_t q = q0; q < q1; q++) { pre[q] = (uint16_t)run; run += __popc(bm[q]); }
+    __syncthreads();
+    uint32_t *tb = tab + toff[t];
+    for (uint32_t q = tid; q < nw; q += 256) {
+      uint32_t b = bm[q], p = pre[q];
+      while (b) {
+        const int bit = __ffs(b) - 1;
+        tb[p++] = lo + 32 * q + bit;
+        b &= b - 1;
+      }
+    }
+    for (uint64_t k = e0 + tid; k < e1; k += 256) {
+      const uint32_t c = col[k] - lo, q = c >> 5;
+      slot[k] = (uint16_t)(pre[q] + __popc(bm[q] & ((1u << (c & 31)) - 1u)));
+    }
+    __syncthreads();
+  }
+}
+// One tile of rows [r0, r1) for a workgroup of 4 wavefronts: k_spmv_pair's rounds (pair
+// loads, masked leading / trailing slots, ordered adds, AMX maxima), the gather from the
+// LDS table xs (TAB: loaded by the caller) or from x (direct tiles).
+template <int RW, int PER, int TMAX, bool TAB, bool AMX>
+__device__ __forceinline__ void spmv_tab_rows(const uint64_t *ro, const uint32_t *col, const uint16_t *slot,
+                                              const double *a, uint32_t r0, uint32_t r1, const double *x,
+                                              const uint32_t *tb, uint32_t nd, double *xs, double *z,
+                                              double alpha, const double *y, double beta, const uint8_t *f,
+                                              uint64_t *amx, double (*buf)[RW][64 * PER / RW + 1],
+                                              uint64_t (*rk0)[RW], uint32_t (*rlen)[RW]) {
+  constexpr int SEG = 64 * PER / RW, PH = PER / 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double2 *a2p = reinterpret_cast<const double2 *>(a);
+  const uint2 *c2p = reinterpret_cast<const uint2 *>(col);
+  const uint32_t *s2p = reinterpret_cast<const uint32_t *>(slot);
+  auto pk = [&](uint32_t off, int p, uint32_t &m) -> uint64_t {
+    const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+    const uint32_t en = off + sub, info = rlen[w][rr], vl = info & 0x7fffffffu;
+    const bool any = en < vl;
+    m |= (any && en >= (info >> 31) ? 1u : 0u) << (2 * p);
+    m |= (en + 1 < vl ? 1u : 0u) << (2 * p + 1);
+    return any ? rk0[w][rr] + (en >> 1) : 0;
+  };
+  // values and gather indices (slots or columns) of round `off`
+  auto ldc = [&](uint32_t off, double *av, uint32_t *cv) -> uint32_t {
+    uint32_t m = 0;
+#pragma unroll
+    for (int p = 0; p < PH; p++) {
+      const uint64_t k = pk(off, p, m);
+      const double2 v = a2p[k];
+      av[2 * p] = v.x; av[2 * p + 1] = v.y;
+      if (TAB) {
+        const uint32_t s = s2p[k];
+        cv[2 * p] = s & 0xffffu; cv[2 * p + 1] = s >> 16;
+      } else {
+        const uint2 c = c2p[k];
+        cv[2 * p] = c.x; cv[2 * p + 1] = c.y;
+      }
+    }
+    return m;
+  };
+  auto gat = [&](const uint32_t *cv, uint32_t m, double *gv) {
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const uint32_t c = (m >> q) & 1u ? cv[q] : 0u;
+      gv[q] = TAB ? xs[c] : x[c];
+    }
+  };
+  for (uint64_t rb = (uint64_t)r0 + (uint64_t)w * RW; rb < r1; rb += 4 * RW) {
+    const uint64_t r = rb + lane;
+    const bool own = lane < RW && r < r1;
+    const uint32_t i = own ? (uint32_t)r : 0u;
+    const uint64_t k0 = own ? ro[i] : 0, k1 = own ? ro[i + 1] : 0;
+    const uint32_t lead = k1 > k0 ? (uint32_t)(k0 & 1) : 0u;
+    const uint32_t vlen = (uint32_t)(k1 - k0) + lead;
+    if (lane < RW) {
+      rk0[w][lane] = (k0 - lead) >> 1;
+      rlen[w][lane] = vlen | lead << 31;
+    }
+    uint32_t mx = vlen;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { uint32_t u = __shfl_xor(mx, o, 64); mx = u > mx ? u : mx; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double va[2][PER], gv[PER];
+    uint32_t cq[PER], ct[PER], ms[2];
+    ms[0] = ldc(0, va[0], ct);
+    ms[1] = ldc(SEG, va[1], cq);
+    gat(ct, ms[0], gv);
+    double t = 0, mxv = -DBL_MAX;
+    uint32_t mxp = 0xffffffffu;
+    for (uint32_t off = 0; off < mx; off += SEG) {
+#pragma unroll
+      for (int p = 0; p < PH; p++) {
+        const int fl = 2 * (p * 64 + lane), rr = fl / SEG, sub = fl % SEG;
+        buf[w][rr][sub] = (ms[0] >> (2 * p)) & 1u ? va[0][2 * p] * gv[2 * p] : 0.0;
+        buf[w][rr][sub + 1] = (ms[0] >> (2 * p + 1)) & 1u ? va[0][2 * p + 1] * gv[2 * p + 1] : 0.0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (AMX) {
+        constexpr int LPR = 64 / RW, EPL = SEG / LPR;
+        const int rr = lane / LPR, part = lane % LPR;
+        const uint32_t info = rlen[w][rr], vl = info & 0x7fffffffu, ld0 = info >> 31;
+        double bv = -DBL_MAX;
+        uint32_t bp = 0xffffffffu;
+#pragma unroll
+        for (int e = 0; e < EPL; e++) {
+          const uint32_t sub = (uint32_t)(part * EPL + e), pos = off + sub;
+          const double v = buf[w][rr][sub];
+          if (pos < vl && pos >= ld0 && v > bv) { bv = v; bp = pos; }
+        }
+#pragma unroll
+        for (int o = LPR / 2; o > 0; o >>= 1) {
+          const double ov = __shfl_xor(bv, o, 64);
+          const uint32_t op = (uint32_t)__shfl_xor((int)bp, o, 64);
+          if (ov > bv || (ov == bv && op < bp)) { bv = ov; bp = op; }
+        }
+        const double sv = __shfl(bv, (lane % RW) * LPR, 64);
+        const uint32_t sp = (uint32_t)__shfl((int)bp, (lane % RW) * LPR, 64);
+        if (lane < RW && sv > mxv) { mxv = sv; mxp = sp; }
+      }
+#pragma unroll
+      for (int q = 0; q < PER; q++) va[0][q] = va[1][q];
+      ms[0] = ms[1];
+      gat(cq, ms[0], gv);                                      // round off + SEG
+      ms[1] = ldc(off + 2 * SEG, va[1], cq);                   // round off + 2 SEG
+      if (lane < RW && off < vlen) {
+        const uint32_t m = min((uint32_t)SEG, vlen - off);
+        if (m == SEG) {
+          constexpr int U = SEG < 16 ? SEG : 16;
+#pragma unroll
+          for (int e0 = 0; e0 < SEG; e0 += U) {
+            double u[U];
+#pragma unroll
+            for (int e = 0; e < U; e++) u[e] = buf[w][lane][e0 + e];
+#pragma unroll
+            for (int e = 0; e < U; e++) t += u[e];
+          }
+        } else {
+          for (uint32_t e = 0; e < m; e++) t += buf[w][lane][e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (own) {
+      double v = (alpha == 0.0 || y == nullptr) ? beta * t : alpha * y[i] + beta * t;
+      if (f) v = v * (f[i] ? 1.0 : 0.0);
+      z[i] = v;
+      if (AMX) amx[i] = mxp == 0xffffffffu ? ~0ull : k0 - lead + mxp;
+    }
+  }
+}
+template <int RW, bool AMX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spmv_tab(const uint64_t *ro, const uint32_t *col, const uint16_t *slot,
+                                                  const double *a, uint32_t n, uint32_t TR, uint32_t ntiles,
+                                                  const uint32_t *tnd, const uint64_t *toff, const uint32_t *tab,
+                                                  const double *x, double *z, double alpha, const double *y,
+                                                  double beta, const uint8_t *f, uint64_t *amx) {
+  constexpr int PER = TabShape<RW>::PER, TMAX = TabShape<RW>::TMAX, SEG = 64 * PER / RW;
+  __shared__ double xs[TMAX];
+  __shared__ double buf[4][RW][SEG + 1];
+  __shared__ uint64_t rk0[4][RW];
+  __shared__ uint32_t rlen[4][RW];
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t r0 = t * TR, r1 = min(n, r0 + TR), nd = tnd[t];
+    if (nd > (uint32_t)TMAX)                   // TAB_DIRECT (and never past the LDS table)
+      spmv_tab_rows<RW, PER, TMAX, false, AMX>(ro, col, slot, a, r0, r1, x, nullptr, 0, xs, z, alpha, y, beta, f,
+                                               amx, buf, rk0, rlen);
+    else {
+      // the tile's table: every load of it in flight at once (nothing else is live
+      // here), then LDS, then one barrier
+      constexpr int TL = (TMAX + 255) / 256;
+      const uint32_t *tb = tab + toff[t];
+      uint32_t tc[TL];
+      double tv[TL];
+#pragma unroll
+      for (int u = 0; u < TL; u++) {
+        const uint32_t q = (uint32_t)u * 256 + threadIdx.x;
+        tc[u] = tb[q < nd ? q : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < TL; u++) tv[u] = x[tc[u]];
+#pragma unroll
+      for (int u = 0; u < TL; u++) {
+        const uint32_t q = (uint32_t)u * 256 + threadIdx.x;
+        if (q < nd) xs[q] = tv[u];
+      }
+      __syncthreads();
+      spmv_tab_rows<RW, PER, TMAX, true, AMX>(ro, col, slot, a, r0, r1, x, tb, nd, xs, z, alpha, y, beta, f, amx,
+                                              buf, rk0, rlen);
+    }
+    __syncthreads();
+  }
+}
+struct MvTab {
+  const uint64_t *ro;
+  uint32_t rn;
+  uint64_t nnz;
+  int rw;
+  uint32_t TR, ntiles, ndirect;
+  uint32_t *tnd;
+  uint64_t *toff;
+  uint32_t *tab;
+  uint16_t *slot;
+};
+static std::vector<MvTab> g_mvtab;
+static int g_mv_tab = -1;
+extern "C" void amgd_spmv_set_tab(int on) { g_mv_tab = on; }
+static bool mv_tab_on() {
+  if (g_mv_tab < 0) { const char *e = getenv("AMGD_MV_TAB"); g_mv_tab = e && *e ? atoi(e) : 1; }
+  return g_mv_tab > 0;
+}
+static uint64_t g_tab_builds = 0, g_tab_tiles = 0, g_tab_direct = 0;
+extern "C" void amgd_spmv_tab_stats(uint64_t *out3) { out3[0] = g_tab_builds; out3[1] = g_tab_tiles; out3[2] = g_tab_direct; }
+static void mv_tab_free(MvTab &t) {
+  amgd_free(t.tnd); amgd_free(t.toff); amgd_free(t.tab); amgd_free(t.slot);
+}
+// rows per wavefront of the tabled kernel, by the mean row: long rows (coarse levels) 4 per
+// wavefront, so a tile can be 16 rows; short ones 64 (tiles of 256 rows)
+static int tab_rw(uint64_t mean) { return mean >= 256 ? 4 : mean >= 96 ? 16 : 64; }
+// Tables only for mean rows below TAB_MEAN_MAX: for the coarse levels' long rows (mean >=
+// 256, 4 rows per wavefront) the tiled kernel measured 1.1-1.8x slower per product than
+// k_spmv_pair (a tile of 16 rows per workgroup: one table load and barrier per 4 rows per
+// wavefront; profiles/r06/mvlog_ab_r06g.txt)
+#define TAB_MEAN_MAX 256
+static void mv_tab_build(const dcsr *M) {
+  if (!mv_tab_on() || M->rn == 0 || M->nnz < 32ull * M->rn || (int64_t)M->rn < sl_min_whole()) return;
+  if (((uintptr_t)M->a & 15) || ((uintptr_t)M->col & 7)) return;
+  for (const MvTab &e : g_mvtab)
+    if (e.ro == M->ro && e.rn == M->rn && e.nnz == M->nnz) return;
+  hipStream_t s = amgd_s();
+  const uint64_t mean = M->nnz / M->rn;
+  if (mean >= TAB_MEAN_MAX) return;
+  MvTab t{};
+  t.ro = M->ro; t.rn = M->rn; t.nnz = M->nnz;
+  t.rw = tab_rw(mean);
+  // tiles of ~12 K entries (3-6 K distinct columns at 256^3), at least one round of rows
+  const uint32_t unit = 4u * (uint32_t)t.rw;
+  uint64_t tr = 12288 / std::max<uint64_t>(mean, 1);
+  tr = std::max<uint64_t>(unit, (tr / unit) * unit);
+  t.TR = (uint32_t)tr;
+  t.ntiles = (uint32_t)((M->rn + tr - 1) / tr);
+  t.tnd = (uint32_t *)amgd_alloc(4ull * t.ntiles + 8);
+  uint2 *span = (uint2 *)amgd_alloc(8ull * t.ntiles + 8);
+  // the LDS table of the kernel that will read it (k_spmv_tab<rw>: xs[TMAX])
+  const uint32_t tmax = t.rw == 4 ? TabShape<4>::TMAX : t.rw == 16 ? TabShape<16>::TMAX : TabShape<64>::TMAX;
+  const int g = (int)std::min<uint32_t>(t.ntiles, 16384u);
+  static bool attr = false;
+  if (!attr) {
+    HIPCK(hipFuncSetAttribute((const void *)k_tab_count, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * TAB_BM_WORDS));
+    HIPCK(hipFuncSetAttribute((const void *)k_tab_fill, hipFuncAttributeMaxDynamicSharedMemorySize, 6 * TAB_BM_WORDS));
+    attr = true;
+  }
+  k_tab_count<<<g, 256, 4 * TAB_BM_WORDS, s>>>(M->ro, M->col, M->rn, t.TR, t.ntiles, tmax, t.tnd, span);
+  KCHECK();
+  t.toff = (uint64_t *)amgd_alloc(8ull * t.ntiles + 16);
+  std::vector<uint32_t> hnd(t.ntiles);
+  HIPCK(hipMemcpyAsync(hnd.data(), t.tnd, 4ull * t.ntiles, hipMemcpyDeviceToHost, s));
+  HIPCK(hipStreamSynchronize(s));
+  std::vector<uint64_t> hoff(t.ntiles + 1, 0);
+  for (uint32_t q = 0; q < t.ntiles; q++) {
+    const uint32_t nd = hnd[q];
+    if (nd == TAB_DIRECT) t.ndirect++;
+    hoff[q + 1] = hoff[q] + (nd == TAB_DIRECT ? 0 : nd);
+  }
+  amgd_h2d(t.toff, hoff.data(), 8ull * (t.ntiles + 1));
+  t.tab = (uint32_t *)amgd_alloc(4 * hoff[t.ntiles] + 8);
+  t.slot = (uint16_t *)amgd_alloc(2 * M->nnz + 16);
+  k_tab_fill<<<g, 256, 6 * TAB_BM_WORDS, s>>>(M->ro, M->col, M->rn, t.TR, t.ntiles, t.tnd, span, t.toff, t.tab, t.slot);
+  KCHECK();
+  amgd_free(span);
+  g_tab_builds++;
+  g_tab_tiles += t.ntiles;
+  g_tab_direct += t.ndirect;
+  g_mvtab.push_back(t);
+}
+static const MvTab *mv_tab_find(const dcsr *M) {
+  for (const MvTab &e : g_mvtab)
+    if (e.ro == M->ro && e.rn == M->rn && e.nnz == M->nnz) return &e;
+  return nullptr;
+}
+static void mv_tab_drop(const void *ro) {
+  for (size_t q = 0; q < g_mvtab.size();)
+    if ((const void *)g_mvtab[q].ro == ro) { MvTab t = g_mvtab[q]; g_mvtab.erase(g_mvtab.begin() + q); mv_tab_free(t); }
+    else q++;
+}
+static void mv_tab_launch(const MvTab *tb, const dcsr *M, const double *x, double *z, double alpha,
+                          const double *y, double beta, const uint8_t *f, uint64_t *amx) {
+  const int g = (int)std::min<uint32_t>(tb->ntiles, 65536u);
+#define TAB_L(RW, AMX_)                                                                             \
+  k_spmv_tab<RW, AMX_><<<g, 256, 0, amgd_s()>>>(M->ro, M->col, tb->slot, M->a, M->rn, tb->TR, tb->ntiles, \
+                                                tb->tnd, tb->toff, tb->tab, x, z, alpha, y, beta, f, amx)
+  if (amx) {
+    if (tb->rw == 64) TAB_L(64, true); else if (tb->rw == 16) TAB_L(16, true); else TAB_L(4, true);
+  } else {
+    if (tb->rw == 64) TAB_L(64, false); else if (tb->rw == 16) TAB_L(16, false); else TAB_L(4, false);
+  }
+#undef TAB_L
+}
 // Products with x take k_spmv_pair by default (round 5: long-row SpMV 5.02 -> 4.88 s per
 // 256^3 setup, profiles/r05/pair/); AMGD_MV_PAIR=0 / amgd_spmv_set_pair(0) (tests, A/B):
 // k_spmv_pipe.  Measured and dropped (profiles/r05/pair/): values one round ahead at 3
@@ -1171,6 +1572,8 @@ extern "C" void amgd_spmv(const dcsr *M, const double *x, double *z, double alph
   const double ms = (amgd_wtime() - t0) * 1e3;
   const int64_t slm = sl_min_whole();
   const char *k = M->nnz >= 32ull * M->rn ? ((int64_t)M->rn >= slm ? "lane" : "wave") : "stream";
+  const MvTab *tb = x ? mv_tab_find(M) : nullptr;
+  if (tb) fprintf(stderr, "spmvtab rw %d tr %u tiles %u direct %u\n", tb->rw, tb->TR, tb->ntiles, tb->ndirect);
   fprintf(stderr, "spmv %u x %u nnz %lu %s x%d %.3f ms %.0f GB/s\n", M->rn, M->cn,
           (unsigned long)M->nnz, k, x ? 1 : 0, ms,
           (12.0 * M->nnz + 16.0 * M->rn + (x ? 8.0 * M->nnz : 0.0)) / (ms * 1e6));
@@ -1204,9 +1607,55 @@ __global__ void k_row_max(const uint64_t *ro, uint32_t rn, unsigned *mx) {
   for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
   if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
 }
+// AMGD_MVSTAT=1 (analysis): for a pinned long-row matrix, the x locality of its products --
+// per block of B consecutive rows, the distinct columns and distinct 128-B lines of x they
+// gather, against the entries (a sample of the blocks); and per 64-entry chunk of a row (one
+// gather instruction of the lane kernels) the distinct lines.  Host-side, stderr.
+#include <algorithm>
+static void mv_pattern_stats(const dcsr *M) {
+  static int on = -1;
+  if (on < 0) { const char *e = getenv("AMGD_MVSTAT"); on = e && *e ? atoi(e) : 0; }
+  if (!on || M->rn == 0 || M->nnz < 32ull * M->rn) return;
+  amgd_sync();
+  std::vector<uint64_t> ro(M->rn + 1);
+  std::vector<uint32_t> col(M->nnz);
+  HIPCK(hipMemcpy(ro.data(), M->ro, (M->rn + 1) * 8, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(col.data(), M->col, M->nnz * 4, hipMemcpyDeviceToHost));
+  double chunk_lines = 0, chunks = 0;
+  for (uint32_t i = 0; i < M->rn; i += 61) {
+    for (uint64_t k = ro[i]; k < ro[i + 1]; k += 64) {
+      const uint64_t e = std::min(ro[i + 1], k + 64);
+      uint32_t last = 0xffffffffu, d = 0;
+      for (uint64_t q = k; q < e; q++) { const uint32_t l = col[q] >> 4; if (l != last) { d++; last = l; } }
+      chunk_lines += d; chunks++;
+    }
+  }
+  fprintf(stderr, "mvstat rn %u cn %u nnz %lu mean %.1f | lines per 64-entry chunk %.1f", M->rn, M->cn,
+          (unsigned long)M->nnz, (double)M->nnz / M->rn, chunks ? chunk_lines / chunks : 0.0);
+  std::vector<uint32_t> tmp;
+  for (uint32_t B : {16u, 64u, 256u, 1024u}) {
+    double ent = 0, dist = 0, lines = 0, blocks = 0, span = 0;
+    const uint32_t nb = (M->rn + B - 1) / B, step = std::max<uint32_t>(1, nb / 400);
+    for (uint32_t b = 0; b < nb; b += step) {
+      const uint32_t r0 = b * B, r1 = std::min(M->rn, r0 + B);
+      tmp.assign(col.begin() + ro[r0], col.begin() + ro[r1]);
+      if (tmp.empty()) continue;
+      std::sort(tmp.begin(), tmp.end());
+      uint32_t d = 0, l = 0, lastc = 0xffffffffu, lastl = 0xffffffffu;
+      for (uint32_t c : tmp) { if (c != lastc) { d++; lastc = c; } if ((c >> 4) != lastl) { l++; lastl = c >> 4; } }
+      ent += tmp.size(); dist += d; lines += l; blocks++; span += tmp.back() - tmp.front();
+    }
+    if (blocks)
+      fprintf(stderr, " | B%u: ent %.0f distinct %.0f (%.2f/ent) lines %.0f span %.0f", B, ent / blocks, dist / blocks,
+              dist / ent, lines / blocks, span / blocks);
+  }
+  fprintf(stderr, "\n");
+}
 extern "C" void amgd_rowmax_pin(const dcsr *M) {
   for (const RowMax &e : g_rowmax)
     if (e.ro == M->ro && e.rn == M->rn && e.nnz == M->nnz) return;
+  mv_pattern_stats(M);
+  mv_tab_build(M);
   unsigned h = 0;
   if (M->rn) {
     unsigned *d = (unsigned *)amgd_alloc(4);
@@ -1218,6 +1667,7 @@ extern "C" void amgd_rowmax_pin(const dcsr *M) {
   g_rowmax.push_back({M->ro, M->rn, M->nnz, h});
 }
 extern "C" void amgd_rowmax_unpin(const dcsr *M) {
+  mv_tab_drop(M->ro);
   for (size_t q = 0; q < g_rowmax.size();)
     if (g_rowmax[q].ro == M->ro) g_rowmax.erase(g_rowmax.begin() + q);
     else q++;
@@ -1228,6 +1678,7 @@ extern "C" uint32_t amgd_max_row_len(const dcsr *M) {
   return 0xffffffffu;
 }
 void amgd_spmv_split_forget(const void *ro) {
+  if (!g_mvtab.empty()) mv_tab_drop(ro);
   for (size_t q = 0; q < g_rowmax.size();)
     if ((const void *)g_rowmax[q].ro == ro) g_rowmax.erase(g_rowmax.begin() + q);
     else q++;
@@ -1236,7 +1687,11 @@ void amgd_spmv_split_forget(const void *ro) {
     if ((const void *)g_mv_split[q].ro == ro) g_mv_split.erase(g_mv_split.begin() + q);
     else q++;
 }
-void amgd_spmv_split_clear(void) { g_mv_split.clear(); g_rowmax.clear(); }
+void amgd_spmv_split_clear(void) {
+  g_mv_split.clear();
+  g_rowmax.clear();
+  while (!g_mvtab.empty()) mv_tab_drop(g_mvtab.back().ro);
+}
 static uint64_t g_mv_shard_calls = 0;
 extern "C" uint64_t amgd_spmv_shard_calls(void) { return g_mv_shard_calls; }   // (test API)
 static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alpha, const double *y,
@@ -1295,7 +1750,15 @@ static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, c
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
     const int rwi = lane_rw(M->rn) == 64 ? 2 : lane_rw(M->rn) == 16 ? 1 : 0;
     amgd_timer_start2(1, 2 + rwi);             // roofline: whole-matrix long-row products,
-    if (g_amx && x && alpha == 0.0 && beta == 1.0 && !f && mv_pair(M)) {
+    const MvTab *tb = x ? mv_tab_find(M) : nullptr;
+    if (tb) {                                  // tabled gathers (pinned pattern)
+      const bool amx = g_amx && alpha == 0.0 && beta == 1.0 && !f;
+      amgd_route_hit(AMGD_R_SPMV_PIPE);
+      amgd_route_hit(AMGD_R_MV_TAB);
+      amgd_route_hit(rwi == 2 ? AMGD_R_MV_RW64 : rwi == 1 ? AMGD_R_MV_RW16 : AMGD_R_MV_RW4);
+      mv_tab_launch(tb, M, x, z, alpha, y, beta, f, amx ? g_amx : nullptr);
+      if (amx) g_amx_done = 1;
+    } else if (g_amx && x && alpha == 0.0 && beta == 1.0 && !f && mv_pair(M)) {
       const int rw_ = lane_rw(M->rn);          // + each row's first largest product
       const int gp_ = (int)std::min<uint64_t>(((uint64_t)M->rn + 4 * rw_ - 1) / (4 * rw_), 65536);
       amgd_route_hit(AMGD_R_SPMV_PIPE);

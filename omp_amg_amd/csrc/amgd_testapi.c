@@ -103,6 +103,41 @@ API int amgd_test_spmv(const hcsr *HA, const double *x, double alpha, const doub
   return 0;
 }
 
+/* z = alpha*y + beta*(A x), f row mask, through the gather-table kernel: the matrix is
+   pinned (amgd_rowmax_pin builds its tiles) for the product and unpinned after; amx != NULL:
+   the fused-selection form (alpha 0, beta 1, no y / f) with each row's first largest
+   product.  stats (3): table builds, tiles, direct tiles of this call. */
+API int amgd_test_spmv_tab(const hcsr *HA, const double *x, double alpha, const double *y, double beta,
+                           const uint8_t *f, double *z, uint64_t *amx, uint64_t *stats) {
+  if (amgd_rt_init(0) != 0) return -1;
+  dcsr *A = up(HA);
+  double *dx = (double *)amgd_alloc((size_t)HA->cn * 8 + 8), *dz = (double *)amgd_alloc((size_t)HA->rn * 8 + 8);
+  double *dy = NULL;
+  uint8_t *df = NULL;
+  uint64_t *dm = NULL;
+  amgd_h2d(dx, x, (size_t)HA->cn * 8);
+  if (y) { dy = (double *)amgd_alloc((size_t)HA->rn * 8 + 8); amgd_h2d(dy, y, (size_t)HA->rn * 8); }
+  if (f) { df = (uint8_t *)amgd_alloc((size_t)HA->rn + 8); amgd_h2d(df, f, (size_t)HA->rn); }
+  uint64_t s0[3], s1[3];
+  amgd_spmv_tab_stats(s0);
+  amgd_rowmax_pin(A);
+  if (amx) {
+    dm = (uint64_t *)amgd_alloc((size_t)HA->rn * 8 + 8);
+    if (!amgd_spmv_amax(A, dx, dz, dm)) { amgd_rowmax_unpin(A); return -2; }
+    amgd_d2h(amx, dm, (size_t)HA->rn * 8);
+  } else {
+    amgd_spmv(A, dx, dz, alpha, dy, beta, df);
+  }
+  amgd_spmv_tab_stats(s1);
+  for (int q = 0; q < 3; q++) stats[q] = s1[q] - s0[q];
+  amgd_d2h(z, dz, (size_t)HA->rn * 8);
+  amgd_rowmax_unpin(A);
+  amgd_free(dx); amgd_free(dz); if (dy) amgd_free(dy); if (df) amgd_free(df); if (dm) amgd_free(dm);
+  dcsr_free(&A);
+  return 0;
+}
+API void amgd_test_spmv_tab_on(int on) { amgd_spmv_set_tab(on); }
+
 /* build_csr on host COO (u32 indices) */
 API int amgd_test_build(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V, hcsr *HX) {
   if (amgd_rt_init(0) != 0) return -1;

@@ -899,3 +899,70 @@ def test_mpm_long_rows_rank_placement(seed):
         col[s + 1] = col[s]
     D = refops.Csr(A.rn, A.cn, A.row_off.copy(), col, A.a.copy())
     assert refops.same(oa.test_csr_op(2, D, C, 1.0, -1.0), refops.mpm(1.0, D, -1.0, C))
+
+
+def _tab_matrix(rng, rn, cn, mean, far_every=0):
+    """long rows clustered around their diagonal position (a band of ~1200 columns, like
+    a coarse level's R), ragged lengths, some empty rows; every (40 far_every)-th row also
+    takes 8000 columns across the whole range (its tile has too many distinct columns for
+    the gather table: it runs the direct gathers)"""
+    ro, cols = [0], []
+    for i in range(rn):
+        L = 0 if i % 97 == 5 else int(rng.integers(mean // 2, 3 * mean // 2 + 1))
+        L = min(L, cn)
+        c0 = int(i * cn / rn)
+        band = np.arange(max(0, c0 - 600), min(cn, c0 + 600))
+        c = rng.choice(band, size=min(L, len(band)), replace=False)
+        if far_every and i % (far_every * 40) == 3:
+            c = np.concatenate([c, rng.choice(cn, size=8000, replace=False)])
+        c = np.unique(c)
+        cols.extend(c.tolist())
+        ro.append(len(cols))
+    n = len(cols)
+    v = rng.standard_normal(n) * 2.0 ** rng.integers(-30, 30, n)
+    v[rng.random(n) < 0.05] = 0.0
+    v[rng.random(n) < 0.02] *= -0.0
+    return refops.Csr(rn, cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64), v)
+
+
+@pytest.mark.parametrize("mean,far", [(48, 0), (60, 41), (150, 0), (150, 13), (700, 0), (700, 9)],
+                         ids=["rw64", "rw64-direct", "rw16", "rw16-direct", "rw4", "rw4-direct"])
+def test_spmv_gather_table(mean, far):
+    """the gather-table SpMV of pinned long-row matrices (k_spmv_tab: per tile of rows the
+    distinct columns' x in LDS, 16-bit slots per entry; tiles too wide run the direct
+    gathers): bit for bit the sequential products -- plain, with alpha*y + beta, the f row
+    mask, and the fused selection's first largest product per row -- in every RW shape"""
+    rng = np.random.default_rng(mean + far)
+    rn = 4800
+    A = _tab_matrix(rng, rn, 40000, mean, far)
+    x = rng.standard_normal(A.cn) * 2.0 ** rng.integers(-8, 8, A.cn)
+    y = rng.standard_normal(rn)
+    f = (rng.random(rn) < 0.8).astype(np.uint8)
+    oa.spmv_sl_min(0)
+    try:
+        z, _, st = oa.test_spmv_tab(A, x)
+        z2, _, _ = oa.test_spmv_tab(A, x, 1.0, y, -1.0, f)
+        z3, amx, _ = oa.test_spmv_tab(A, x, amx=True)
+        zp = oa.test_spmv(A, x)
+    finally:
+        oa.spmv_sl_min(-1)
+    assert st["builds"] == 1 and st["tiles"] > 0, st
+    if far:
+        assert 0 < st["direct"] < st["tiles"], st
+    else:
+        assert st["direct"] == 0, st
+    want = refops.spmv(A, x)
+    assert np.array_equal(z.view(np.uint64), want.view(np.uint64))
+    assert np.array_equal(zp.view(np.uint64), want.view(np.uint64))
+    want2 = refops.spmv(A, x, 1.0, y, -1.0) * (f != 0)
+    assert np.array_equal(z2.view(np.uint64), want2.view(np.uint64))
+    assert np.array_equal(z3.view(np.uint64), want.view(np.uint64))
+    # first largest product per row, strict > from -DBL_MAX (k_fs_select's rule)
+    for i in range(rn):
+        s, e = int(A.row_off[i]), int(A.row_off[i + 1])
+        p = A.a[s:e] * x[A.col[s:e]]
+        best, bv = ~np.uint64(0), -np.finfo(np.float64).max
+        for q in range(e - s):
+            if p[q] > bv:
+                bv, best = p[q], np.uint64(s + q)
+        assert amx[i] == best, (i, amx[i], best)

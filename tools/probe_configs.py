@@ -24,7 +24,8 @@ def _beat():
         print(f"[probe] {time.time() - _t0:.0f} s", file=sys.stderr, flush=True)
 
 
-threading.Thread(target=_beat, daemon=True).start()
+if os.environ.get("PROBE_BEAT", "1") != "0":      # off under rocprofv3 (a live thread at exit)
+    threading.Thread(target=_beat, daemon=True).start()
 
 CONFIGS = {
     "aniso256": ("anisotropic 3D 7-point Poisson 256^3, eps=1e-3 (BASELINE configs[4])",
