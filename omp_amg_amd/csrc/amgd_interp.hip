@@ -1041,15 +1041,36 @@ __global__ void k_supp_same(const uint64_t *ro, const uint32_t *col, const uint6
     if (t) atomicAdd(nsame, t);
   }
 }
-// copy the packed triangles of the skipped supports cb <= c < ce (one block per support)
+// copy the packed triangles of the skipped supports cb <= c < ce (one block per support);
+// triangles past QCOPY_BIG doubles (the orphan support: 10^4 - 10^5 points, up to GBs) are
+// listed instead and copied by the whole grid (k_qcopy_big): one block per such support
+// took 88 ms per call on the anisotropic 256^3 setup (1.9 s of its 33.7 s,
+// profiles/r06/aniso256_kernel_stats_r06d.csv)
+#define QCOPY_BIG (1ull << 18)
 __global__ void k_qcopy(const uint8_t *skip, const uint64_t *wro, uint32_t cb, uint32_t ce,
-                        const uint64_t *poff, const double *Qp, const uint64_t *qoff, double *Q) {
+                        const uint64_t *poff, const double *Qp, const uint64_t *qoff, double *Q,
+                        uint32_t *big, unsigned *nbig) {
   for (uint64_t c = cb + blockIdx.x; c < ce; c += gridDim.x) {
     if (!skip[c]) continue;
     const uint64_t nz = wro[c + 1] - wro[c], tn = nz * (nz + 1) / 2;
+    if (tn > QCOPY_BIG) {
+      if (threadIdx.x == 0) big[atomicAdd(nbig, 1u)] = (uint32_t)c;
+      continue;
+    }
     const double *src = Qp + poff[c];
     double *dst = Q + qoff[c];
     for (uint64_t t = threadIdx.x; t < tn; t += blockDim.x) dst[t] = src[t];
+  }
+}
+__global__ void k_qcopy_big(const uint32_t *big, const unsigned *nbig, const uint64_t *wro, const uint64_t *poff,
+                            const double *Qp, const uint64_t *qoff, double *Q) {
+  const unsigned n = *nbig;
+  for (unsigned b = 0; b < n; b++) {
+    const uint32_t c = big[b];
+    const uint64_t nz = wro[c + 1] - wro[c], tn = nz * (nz + 1) / 2;
+    const double *src = Qp + poff[c];
+    double *dst = Q + qoff[c];
+    GRID_STRIDE(t, tn) dst[t] = src[t];
   }
 }
 
@@ -1075,11 +1096,16 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
     k_bin_nz<<<grid_for(ce - cb), 256, 0, s>>>(Wt->ro, cb, ce,
                                               BinLim{{QF_T0, QF_T1, QF_T2, 256, 512, QF_T3}}, NB,
                                               lists, cnt, L, skip);
-    if (skip)
+    uint32_t *bigc = nullptr;
+    if (skip) {
+      bigc = (uint32_t *)amgd_alloc(4ull * (ce - cb) + 4);
       k_qcopy<<<(int)std::min<uint32_t>(ce - cb, 16384u), 256, 0, s>>>(skip, Wt->ro, cb, ce, g_qp_off,
-                                                                      g_qp_q, qoff, Q);
+                                                                        g_qp_q, qoff, Q, bigc, cnt + NB);
+      k_qcopy_big<<<2048, 256, 0, s>>>(bigc, cnt + NB, Wt->ro, g_qp_off, g_qp_q, qoff, Q);
+    }
     KCHECK();
     amgd_d2h(hn, cnt, NB * 4);
+    if (bigc) amgd_free(bigc);
   }
   // Huge supports (the orphan support gathered at coarse point 0): one cooperative
   // launch each on a side stream, issued before the other tiers so that its
@@ -2050,6 +2076,70 @@ __global__ void k_lmop_land_pr(const uint32_t *Qj, uint32_t nz, const uint64_t *
     }
   }
 }
+// k_lmop_land_pr with one wavefront per walk k (k_lmop_land_wave's steps: the next 64
+// columns searched from the current position at once, the prefix of exact matches taken,
+// then the first non-exact step or the row skip), keys written for the same-component m.
+// The thread-per-walk form walked 10^4 - 3*10^4 steps per thread on the anisotropic
+// level-1 orphan support: 186 ms per call, 1.5 s of the anisotropic 256^3 setup
+// (profiles/r06/aniso256_kernel_stats_r06d.csv)
+__global__ __launch_bounds__(256) void k_lmop_land_wave_pr(
+    const uint32_t *Qj, uint32_t nz, const uint64_t *sro, const uint32_t *scol, uint32_t srn, uint64_t snnz,
+    const int64_t *rmax, const int64_t *b64, const int64_t *b4k, const uint32_t *compid, const uint32_t *rank,
+    const uint64_t *koff, uint64_t *key) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t k = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; k < nz;
+       k += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t ck = compid[k];
+    const uint64_t o = koff[k];
+    uint32_t r = Qj[k];
+    uint64_t t = sro[r];
+    bool live = sro[r + 1] != t;
+    uint32_t m = 0;
+    while (m < nz) {
+      if (!live) {
+        for (uint32_t q = m + lane; q < nz; q += 64)
+          if (compid[q] == ck) key[o + rank[q]] = snnz;
+        break;
+      }
+      const uint64_t end = sro[r + 1];
+      const uint32_t nv = min(64u, nz - m);
+      const bool valid = (uint32_t)lane < nv;
+      const uint32_t xm = valid ? Qj[m + lane] : 0u;
+      uint64_t L = end;
+      bool inrow = false, exact = false;
+      if (valid && t < end) {
+        L = lower_bound_u32(scol, t, end, xm);
+        inrow = L < end;
+        exact = inrow && scol[L] == xm;
+      }
+      const uint64_t vmask = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+      const uint64_t nonex = ~(uint64_t)__ballot(exact) & vmask;
+      const uint32_t f = nonex ? (uint32_t)(__ffsll((long long)nonex) - 1) : nv;
+      const bool finrow = f < nv && __shfl((int)inrow, (int)f, 64) != 0;
+      const uint32_t acc = f + (finrow ? 1u : 0u);
+      if ((uint32_t)lane < acc && compid[m + lane] == ck) key[o + rank[m + lane]] = L;
+      if (acc) {
+        t = __shfl((unsigned long long)L, (int)acc - 1, 64) + 1;
+        m += acc;
+      }
+      if (f < nv && !finrow) {                        // step m leaves row r (uniform)
+        const uint32_t xf = Qj[m];
+        const uint32_t r2 = next_row_ge(rmax, b64, b4k, srn, r, (int64_t)xf);
+        uint64_t land = snnz;
+        if (r2 >= srn) {
+          if (d_lmop_spill_on) d_lmop_spill = 1;
+          live = false;                               // reference runs off the end of St (UB)
+        } else {
+          r = r2;
+          land = lower_bound_u32(scol, sro[r2], sro[r2 + 1], xf);
+          t = land + 1;
+        }
+        if (lane == 0 && compid[m] == ck) key[o + rank[m]] = land;
+        m++;
+      }
+    }
+  }
+}
 __global__ void k_lmop_val_pr(uint64_t n, uint32_t nz, const uint64_t *koff, const uint32_t *compid,
                               const uint32_t *rank, const uint32_t *members, const uint64_t *cro,
                               const double *Qc, double uc, const uint64_t *key, uint64_t snnz,
@@ -2131,9 +2221,17 @@ static bool lmop_pruned(dcsr *S, const dcsr *Wt, const double *Q, uint64_t qo, u
   amgd_free(hs); amgd_free(skey);
   uint64_t *k1 = (uint64_t *)amgd_alloc(n * 8 + 8), *k2 = (uint64_t *)amgd_alloc(n * 8 + 8);
   double *v1 = (double *)amgd_alloc_f64(n * 8 + 8), *v2 = (double *)amgd_alloc_f64(n * 8 + 8);
-  k_lmop_land_pr<<<grid_for(nz, 64, 65536), 64, 0, s>>>(Wt->col + w0, nz, S->ro, S->col, S->rn,
-                                                       S->nnz, rmax, b64, b4k, compid, rank,
-                                                       koff, k1);
+  const int wmin = lmop_land_wave_min();
+  if (wmin > 0 && nz >= (uint32_t)wmin) {
+    amgd_route_hit(AMGD_R_LMOP_WAVE);
+    k_lmop_land_wave_pr<<<grid_for((uint64_t)nz * 64, 256, 65536), 256, 0, s>>>(Wt->col + w0, nz, S->ro, S->col,
+                                                                               S->rn, S->nnz, rmax, b64, b4k,
+                                                                               compid, rank, koff, k1);
+  } else {
+    k_lmop_land_pr<<<grid_for(nz, 64, 65536), 64, 0, s>>>(Wt->col + w0, nz, S->ro, S->col, S->rn,
+                                                         S->nnz, rmax, b64, b4k, compid, rank,
+                                                         koff, k1);
+  }
   k_lmop_val_pr<<<grid_for(n, 256, 65536), 256, 0, s>>>(n, nz, koff, compid, rank, members, cro, U,
                                                        uc, k1, S->nnz, v1);
   KCHECK();
@@ -2316,7 +2414,7 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
   const uint64_t gs = (uint64_t)gridDim.x * (256 / G);
   for (uint64_t r = g0; r < n; r += gs) {
     const uint32_t c = list[r];
-    if (tro[c + 1] - tro[c] > maxlen) continue;      // k_fs_select_long
+    if (tro[c + 1] - tro[c] > maxlen) continue;      // long columns: k_fsl_part / k_fsl_fin
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
     // U entries per lane per step: their (row, value) loads, then their rs gathers, are in
@@ -2356,41 +2454,94 @@ __global__ __launch_bounds__(256) void k_fs_select(const uint64_t *tro, const ui
     }
   }
 }
-// bad columns past fs_long() entries: one 1024-thread block each (k_fs_select skips them);
-// llist holds their slots in the bad list
-__global__ __launch_bounds__(1024) void k_fs_select_long(const uint64_t *tro, const uint32_t *trow,
-                                                         const uint64_t *perm, double *ta, double *a,
-                                                         const double *rs, const uint32_t *list,
-                                                         const uint32_t *llist, const unsigned *nl,
-                                                         uint32_t *si, uint32_t *sj,
-                                                         unsigned *removed) {
-  __shared__ double smx[16];
-  __shared__ unsigned long long sbest[16];
+// Bad columns past fs_long() entries (k_fs_select skips them; llist holds their slots in
+// the bad list): the same selection spread over the grid -- chunks of FSL_CH entries
+// of every long column (offsets from a one-block scan of the device-side count), a
+// (value, first position) maximum per chunk, then per column the chunks in order -- the
+// first largest product of the column.  One 1024-thread block per column (round 5) took
+// 142 us per call on the orphan column of anisotropic levels (1.9 s
+// of the anisotropic 256^3 setup, profiles/r06/aniso256_kernel_stats_r06d.csv).
+#define FSL_CH 2048
+__global__ __launch_bounds__(256) void k_fsl_prep(const uint64_t *tro, const uint32_t *list, const uint32_t *llist,
+                                                  const unsigned *nl, uint64_t *choff) {
+  __shared__ uint32_t wt[4];
+  __shared__ uint64_t carry;
   const unsigned n = *nl;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (unsigned b = 0; b < n; b += 256) {
+    const unsigned t = b + threadIdx.x;
+    uint32_t c = 0;
+    if (t < n) {
+      const uint32_t col = list[llist[t]];
+      c = (uint32_t)((tro[col + 1] - tro[col] + FSL_CH - 1) / FSL_CH);
+    }
+    const uint32_t incl = block_incl_scan<256>(c, wt);
+    const uint64_t base = carry;
+    if (t < n) choff[t] = base + incl - c;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = base + incl;     // the batch's total (past n: zeros)
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) choff[n] = carry;
+}
+__device__ __forceinline__ unsigned fsl_row_of(const uint64_t *choff, unsigned n, uint64_t g) {
+  unsigned lo = 0, hi = n;                       // last t with choff[t] <= g
+  while (hi - lo > 1) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (choff[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(256) void k_fsl_part(const uint64_t *tro, const uint32_t *trow, const double *ta,
+                                                  const double *rs, const uint32_t *list, const uint32_t *llist,
+                                                  const unsigned *nl, const uint64_t *choff, double *pv,
+                                                  uint64_t *pp) {
+  __shared__ double smx[4];
+  __shared__ unsigned long long sbest[4];
+  const unsigned n = *nl;
+  if (!n) return;
+  const uint64_t G = choff[n];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (unsigned t = blockIdx.x; t < n; t += gridDim.x) {
-    const uint32_t r = llist[t], c = list[r];
+  for (uint64_t g = blockIdx.x; g < G; g += gridDim.x) {
+    const unsigned t = fsl_row_of(choff, n, g);
+    const uint32_t c = list[llist[t]];
+    const uint64_t q0 = tro[c] + (g - choff[t]) * FSL_CH, q1 = min(tro[c + 1], q0 + FSL_CH);
     double mx = -DBL_MAX;
     uint64_t best = ~0ull;
-    for (uint64_t q = tro[c] + threadIdx.x; q < tro[c + 1]; q += 1024) {
-      double x = ta[q] * rs[trow[q]];
+    for (uint64_t q = q0 + threadIdx.x; q < q1; q += 256) {
+      const double x = ta[q] * rs[trow[q]];
       if (x > mx) { mx = x; best = q; }
     }
     for (int o = 32; o > 0; o >>= 1) {
-      double om = __shfl_xor(mx, o, 64);
-      unsigned long long ob = __shfl_xor((unsigned long long)best, o, 64);
+      const double om = __shfl_xor(mx, o, 64);
+      const unsigned long long ob = __shfl_xor((unsigned long long)best, o, 64);
       if (om > mx || (om == mx && ob < best)) { mx = om; best = ob; }
     }
     if (lane == 0) { smx[w] = mx; sbest[w] = best; }
     __syncthreads();
     if (threadIdx.x == 0) {
-      for (int q = 1; q < 16; q++)
+      for (int q = 1; q < 4; q++)
         if (smx[q] > mx || (smx[q] == mx && sbest[q] < best)) { mx = smx[q]; best = sbest[q]; }
-      si[r] = best != ~0ull ? trow[best] : 0u;
-      sj[r] = c;
-      if (best != ~0ull) { ta[best] = 0.0; if (perm) a[perm[best]] = 0.0; *removed = 1u; }
+      pv[g] = mx;
+      pp[g] = best;
     }
     __syncthreads();
+  }
+}
+__global__ void k_fsl_fin(const uint32_t *trow, const uint64_t *perm, double *ta, double *a, const uint32_t *list,
+                          const uint32_t *llist, const unsigned *nl, const uint64_t *choff, const double *pv,
+                          const uint64_t *pp, uint32_t *si, uint32_t *sj, unsigned *removed) {
+  const unsigned n = *nl;
+  GRID_STRIDE(t, n) {
+    const uint32_t r = llist[t], c = list[r];
+    double mx = -DBL_MAX;
+    uint64_t best = ~0ull;
+    for (uint64_t g = choff[t]; g < choff[t + 1]; g++)
+      if (pv[g] > mx) { mx = pv[g]; best = pp[g]; }        // chunks in order: the first wins ties
+    si[r] = best != ~0ull ? trow[best] : 0u;
+    sj[r] = c;
+    if (best != ~0ull) { ta[best] = 0.0; if (perm) a[perm[best]] = 0.0; *removed = 1u; }
   }
 }
 // short rows: one thread per listed row, in order
@@ -2563,8 +2714,17 @@ extern "C" uint32_t amgd_fs_select_ex(const dcsr *Rl, const dcsr *Rt, const uint
     if (amgd_max_row_len(Rt) > ml) {                  // outlier columns present
       k_pick_long<<<grid_for(nc, 256, 1024), 256, 0, s>>>(Rt->ro, list, nc, cnt + 2, ml, 1,
                                                          llist, cnt + 3);
-      k_fs_select_long<<<64, 1024, 0, s>>>(Rt->ro, Rt->col, perm, Rt->a, Rl->a, rs, list, llist,
-                                           cnt + 3, sel_i, sel_j, cnt + 1);
+      // long columns over the grid: at most nnz / (ml + 1) of them
+      const uint64_t nmax = std::min<uint64_t>(nc, Rt->nnz / ((uint64_t)ml + 1) + 1);
+      const uint64_t gmax = Rt->nnz / FSL_CH + nmax + 1;
+      uint64_t *choff = (uint64_t *)amgd_alloc(8 * (nmax + 1) + 8), *pp = (uint64_t *)amgd_alloc(8 * gmax + 8);
+      double *pv = (double *)amgd_alloc_f64(8 * gmax + 8);
+      k_fsl_prep<<<1, 256, 0, s>>>(Rt->ro, list, llist, cnt + 3, choff);
+      k_fsl_part<<<(int)std::min<uint64_t>(gmax, 4096), 256, 0, s>>>(Rt->ro, Rt->col, Rt->a, rs, list, llist,
+                                                                     cnt + 3, choff, pv, pp);
+      k_fsl_fin<<<grid_for(nmax), 256, 0, s>>>(Rt->col, perm, Rt->a, Rl->a, list, llist, cnt + 3, choff, pv, pp,
+                                               sel_i, sel_j, cnt + 1);
+      amgd_free(choff); amgd_free(pp); amgd_free(pv);
     }
     uint64_t avg = (Rt->nnz + nc - 1) / nc;
     int G = 4;

@@ -995,7 +995,7 @@ __global__ __launch_bounds__(256) void k_spmv_pair_amx(const uint64_t *ro, const
 // rounds, rows and ordered adds are unchanged): bit-identical.  Entry stream: 8 B value +
 // 2 B slot instead of 8 B + 4 B.  A tile whose distinct columns exceed the LDS table, or
 // whose column span exceeds the build's bit map, runs the plain gathers ("direct").
-// AMGD_MV_TAB=0 / amgd_spmv_set_tab(0): off.
+// AMGD_MV_TAB=1 / amgd_spmv_set_tab(1): on (off by default, measured below).
 // ---------------------------------------------------------------------------
 #define TAB_BM_WORDS 16384                // build bit map: 524288 columns of span
 #define TAB_DIRECT 0xffffffffu
@@ -1289,7 +1289,9 @@ static std::vector<MvTab> g_mvtab;
 static int g_mv_tab = -1;
 extern "C" void amgd_spmv_set_tab(int on) { g_mv_tab = on; }
 static bool mv_tab_on() {
-  if (g_mv_tab < 0) { const char *e = getenv("AMGD_MV_TAB"); g_mv_tab = e && *e ? atoi(e) : 1; }
+  // off by default: per product 0.84x (level 1's R, 64 rows per wavefront) to 1.34x, and
+  // no change end to end at 256^3 (SpMV 5.01 s per setup either way; profiles/r06/)
+  if (g_mv_tab < 0) { const char *e = getenv("AMGD_MV_TAB"); g_mv_tab = e && *e ? atoi(e) : 0; }
   return g_mv_tab > 0;
 }
 static uint64_t g_tab_builds = 0, g_tab_tiles = 0, g_tab_direct = 0;

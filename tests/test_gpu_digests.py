@@ -125,3 +125,25 @@ def test_gpu_matches_digest_rw64_forced(case):
     assert not bad, f"{len(bad)} arrays differ: {bad[:12]}"
     assert routes["mv_rw64"] > 0 and routes["mv_rw16"] == 0 and routes["mv_rw4"] == 0, routes
     print(case, routes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["aniso_32", "p27_24"])
+def test_gpu_matches_digest_long_paths_forced(case):
+    """the outlier-row paths forced from 8 entries on (find_support's grid-wide expansion,
+    the chunked long-column selection k_fsl_*, the exact long-row products) on digests
+    whose orphan columns span many 2048-entry chunks: the stored digest"""
+    mk = _mk()
+    d = _db()["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    oa.fs_long(8)
+    oa.mv_long(8)
+    try:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.fs_long(-1)
+        oa.mv_long(-1)
+    got = mk.hierarchy_digest(h)
+    exp = d["arrays"]
+    bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    assert not bad, f"{len(bad)} arrays differ: {bad[:12]}"

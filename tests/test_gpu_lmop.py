@@ -49,6 +49,7 @@ def test_lmop_fast_equals_general(gen, small):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("wave", [-1, 1, 0], ids=["wave64", "wave", "thread"])
 @pytest.mark.parametrize("mode", [0, 1], ids=["rowpull", "general"])
 @pytest.mark.parametrize("gen", [
     ("aniso_14", lambda: problems.poisson3d(14, eps=1e-3)),
@@ -56,19 +57,21 @@ def test_lmop_fast_equals_general(gen, small):
     ("p7_16", lambda: problems.poisson3d(16)),
     ("sem_e3_N3", lambda: problems.sem_laplacian(3, 3, 3, 3, seed=5, jitter=0.3)),
 ], ids=lambda g: g[0])
-def test_lmop_pruned_equals_full(gen, mode):
+def test_lmop_pruned_equals_full(gen, mode, wave):
     """the general walk with supports of >= 8 points pruned to same-component
     contributions of their factor graph (default: >= 4096 points) against no pruning:
     every double of the two hierarchies agrees.  In "general" mode every support takes
     the walk; in "rowpull" only the dirty ones (the orphan support of anisotropic levels)"""
     Ai, Aj, Av = gen[1]()
     oa.lmop_prune(0)
+    oa.lmop_wave(wave)       # walks per wavefront from 64 points (default), always, never
     try:
         h_full, s_full = _run(Ai, Aj, Av, mode)
         oa.lmop_prune(8)
         h_pr, s_pr = _run(Ai, Aj, Av, mode)
     finally:
         oa.lmop_prune(-1)
+        oa.lmop_wave(-1)
     assert s_full["pruned"] == 0
     if mode == 1 or gen[0].startswith("aniso"):
         assert s_pr["pruned"] > 0, s_pr

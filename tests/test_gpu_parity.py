@@ -183,18 +183,22 @@ def test_gpu_fs_incremental_bitexact_fixture(case, mode, monkeypatch):
 
 # lmop: every support takes the general walk, supports of >= 8 points pruned to the
 # components of their factor graph -- against the reference's fixtures
+# (the pruned walk one wavefront per k at every support size, or one thread per k)
+@pytest.mark.parametrize("wave", [1, 0], ids=["wave", "thread"])
 @pytest.mark.parametrize("case", ["p7_12", "aniso_12", "sem_e3_N2"])
-def test_gpu_lmop_pruned_bitexact_fixture(case):
+def test_gpu_lmop_pruned_bitexact_fixture(case, wave):
     z = np.load(os.path.join(GOLD, case + ".npz"))
     ref = parity.from_npz(z)
     oa.lmop_mode(1)
     oa.lmop_prune(8)
+    oa.lmop_wave(wave)
     oa.lmop_stats(reset=True)
     try:
         h = abi.run_setup(oa.lib(), z["in_Ai"], z["in_Aj"], z["in_Av"])
     finally:
         oa.lmop_mode(0)
         oa.lmop_prune(-1)
+        oa.lmop_wave(-1)
     assert oa.lmop_stats(reset=True)["pruned"] > 0
     bad = parity.compare(ref, h, exact=True)
     assert not bad, bad
