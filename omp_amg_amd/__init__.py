@@ -290,6 +290,12 @@ def test_spmv_tab(A: abi.Csr, x, alpha=0.0, y=None, beta=1.0, f=None, amx=False)
     return z, m, {"builds": int(st[0]), "tiles": int(st[1]), "direct": int(st[2])}
 
 
+def resolve_wave(on: int) -> None:
+    """exact sums' (dots, long rows) resolution walk: 1 one wavefront (default), 0 one
+    1024-thread block, -1 environment (AMGD_RESOLVE)"""
+    lib().amgd_test_resolve_wave(int(on))
+
+
 def spmv_tab(on: int) -> None:
     """gather tables for pinned long-row matrices (1 default, 0 off, -1 environment)"""
     lib().amgd_test_spmv_tab_on(int(on))

@@ -684,6 +684,12 @@ __device__ __forceinline__ double bn_product(const double *a, const double *b, u
 // the whole block adds products [lo, hi) to the running sum s (uniform), in order
 // MODE 0: a[i]*b[i], 1: a[i]^2, 2: (a[i]*b[i])*b[i], 3: a[i]*b[gcol[i]] (a row of a
 // sparse matrix times a gathered vector), 4: a[i]
+// AMGD_SEGSTAT=1 (analysis): exact-sum counters -- [0] k_seg_resolve rows, [1] chunks,
+// [2] chunks that failed their speculation (binade_range), [3] binade_range rounds,
+// [4] elements summed one by one (rounds > 48 or subnormal sums), [5] zero-skip steps;
+// printed at process exit
+__device__ unsigned long long d_segstat[8];
+__device__ int d_segstat_on = 0;
 template <int MODE>
 __device__ double binade_range(const double *a, const double *b, uint64_t lo, uint64_t hi, double s,
                                double *tile, long long *sh, double *s_sh, int *viol_sh,
@@ -703,6 +709,7 @@ __device__ double binade_range(const double *a, const double *b, uint64_t lo, ui
       // sequential steps where the grid argument does not apply (s == 0,
       // subnormal s), or once a tile has needed too many re-scans
       if (s == 0.0 && rounds <= 48) {
+        if (d_segstat_on && tid == 0) atomicAdd(&d_segstat[5], 1ull);
         // 0 + p == p exactly (and +0 for a zero p): jump to the first nonzero product
         if (tid == 0) (*viol_sh) = 0x7fffffff;
         __syncthreads();
@@ -719,6 +726,7 @@ __device__ double binade_range(const double *a, const double *b, uint64_t lo, ui
         if (tid == 0) {
           double t = s;
           int stop = rounds > 48 ? tlen : j + 1;
+          if (d_segstat_on) atomicAdd(&d_segstat[4], (unsigned long long)(stop - j));
           for (int q = j; q < stop; q++) t += tile[q];
           (*s_sh) = t;
         }
@@ -729,6 +737,7 @@ __device__ double binade_range(const double *a, const double *b, uint64_t lo, ui
         continue;
       }
       rounds++;
+      if (d_segstat_on && tid == 0) atomicAdd(&d_segstat[3], 1ull);
       int e = ilogb(s);
       double u = ldexp(1.0, e - 52);
       long long S0 = (long long)ldexp(s, 52 - e);       // |S0| in [2^52, 2^53)
@@ -1141,6 +1150,7 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
   for (unsigned r = blockIdx.x; r < n; r += gridDim.x) {
     const uint32_t i = list[r];
     const uint64_t c0 = choff[r], c1 = choff[r + 1], k0 = ro[i], k1 = ro[i + 1];
+    if (d_segstat_on && tid == 0) { atomicAdd(&d_segstat[0], 1ull); atomicAdd(&d_segstat[1], c1 - c0); }
     double s = 0.0;
     uint64_t c = c0;
     while (c < c1) {
@@ -1172,6 +1182,7 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
       __syncthreads();
       c = run_end;
       if (c < ce) {
+        if (d_segstat_on && tid == 0) atomicAdd(&d_segstat[2], 1ull);
         const uint64_t lo = k0 + (c - c0) * BN_TILE, hi = min(k1, lo + BN_TILE);
         s = binade_range<MODE>(a, x, lo, hi, s, tile, sh, &s_sh, &viol_sh, col);
         c++;
@@ -1181,12 +1192,176 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
     __syncthreads();
   }
 }
+// ---------------------------------------------------------------------------
+// Wavefront resolution (round 6).  The walks above take one 1024-thread block per row (per
+// dot): every step -- a batch of chunk records, or a round of binade_range inside a chunk
+// that failed its speculation -- costs a block scan and four to six barriers of 16
+// wavefronts.  On the anisotropic levels' orphan rows (~119 K entries, 29 chunks, 30 % of
+// them failing: every strong entry is a jump of ~10^3 over the running sum, a binade
+// crossing) that was 184 us per row and 7 s of the anisotropic 256^3 setup
+// (AMGD_SEGSTAT: 40 753 rows, 1.18 M chunks, 350 K failed, 1.40 M rounds;
+// profiles/r06/aniso256_kernel_stats_r06d.csv).  Here one wavefront walks a row: the
+// records 64 at a time (a wave scan of the chunks' integer sums, the first failing chunk
+// by ballot), and a failed chunk 64 products at a time: the products scaled to the
+// running sum's binade grid u = 2^(e-52) and rounded (exact power-of-two scaling), a wave
+// scan of the integers, the first step that leaves the binade (or is a tie / too large) by
+// ballot; the steps before it are exact (fl(s + p) = s + RN_u(p) while the sum stays in
+// the binade), that step is added the ordinary way.  The same arithmetic as binade_range
+// and k_dot_resolve with wave-level scans instead of block-level ones: the sequential sum,
+// bit for bit.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long wave_incl_scan_u64(unsigned long long v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  return v;
+}
+// s + p_lo + ... + p_{hi-1} in order (products by prod(k)), one wavefront
+template <typename Prod>
+__device__ double wave_binade_range(Prod prod, uint64_t lo, uint64_t hi, double s, int lane) {
+  const long long LO = (1ll << 52), HI = (1ll << 53);
+  for (uint64_t base = lo; base < hi; base += 64) {
+    const uint32_t nv = (uint32_t)min((uint64_t)64, hi - base);
+    const bool valid = (uint32_t)lane < nv;
+    const double p = valid ? prod(base + lane) : 0.0;
+    uint32_t j = 0;
+    while (j < nv) {                                       // uniform over the wavefront
+      if (s == 0.0) {                                      // 0 + p == p: to the first nonzero p
+        const unsigned long long nz = __ballot(valid && (uint32_t)lane >= j && p != 0.0);
+        if (!nz) break;
+        const uint32_t f = (uint32_t)(__ffsll((long long)nz) - 1);
+        s = s + __shfl(p, (int)f, 64);
+        j = f + 1;
+        continue;
+      }
+      if (!(fabs(s) >= 2.2250738585072014e-308) || !(fabs(s) < 1.0e300)) {
+        s = s + __shfl(p, (int)j, 64);                     // subnormal / huge / non-finite: one step
+        j++;
+        continue;
+      }
+      const int e = ilogb(s);
+      const double u = ldexp(1.0, e - 52);
+      const long long S0 = (long long)ldexp(s, 52 - e);
+      const bool act = valid && (uint32_t)lane >= j;
+      long long m = 0;
+      bool bad = false;
+      if (act) {
+        const double xq = p / u;                           // exact: power-of-two scaling
+        const double r = rint(xq);
+        if (!(fabs(xq) < 4.6e18) || fabs(r - xq) == 0.5) bad = true;
+        else m = (long long)r;
+      }
+      const long long run = (long long)((unsigned long long)S0 + wave_incl_scan_u64((unsigned long long)m, lane));
+      const bool inside = S0 > 0 ? (run > LO && run < HI) : (run < -LO && run > -HI);
+      const unsigned long long viol = __ballot(act && (bad || !inside));
+      if (!viol) {
+        s = ldexp((double)__shfl(run, (int)nv - 1, 64), e - 52);
+        j = nv;
+      } else {
+        const uint32_t v = (uint32_t)(__ffsll((long long)viol) - 1);
+        const long long pre = __shfl(run, (int)(v > 0 ? v - 1 : 0), 64);
+        const double sc = v > j ? ldexp((double)pre, e - 52) : s;   // the exact prefix
+        s = sc + __shfl(p, (int)v, 64);
+        j = v + 1;
+      }
+    }
+  }
+  return s;
+}
+// records [c0, c1) of one sum: the runs of passing chunks (wave scan, ballot), a failing
+// chunk added by wave_binade_range (chunk c covers products [k0 + (c - c0) * BN_TILE, ..))
+template <typename Prod>
+__device__ double wave_resolve(Prod prod, const SpecRec *rec, uint64_t c0, uint64_t c1, uint64_t k0, uint64_t k1,
+                               int lane) {
+  const long long LO = (1ll << 52), HI = (1ll << 53);
+  double s = 0.0;
+  uint64_t c = c0;
+  while (c < c1) {
+    const uint64_t ce = min(c1, c + 64);
+    const bool normal = fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1.0e300;
+    const int e = normal ? ilogb(s) : 0;
+    const long long S = normal ? (long long)ldexp(s, 52 - e) : 0ll;
+    const uint64_t q = c + (uint64_t)lane;
+    SpecRec rc;
+    rc.M = 0; rc.mn = 0; rc.mx = 0; rc.e = 0; rc.flag = 1;
+    if (q < ce) rc = rec[q];
+    bool ok = q < ce && normal && !rc.flag && rc.e == e;
+    const long long mv = ok ? rc.M : 0ll;
+    const unsigned long long inc = wave_incl_scan_u64((unsigned long long)mv, lane);
+    if (ok) {
+      const long long base = (long long)((unsigned long long)S + inc - (unsigned long long)mv);
+      ok = S > 0 ? (base + rc.mn > LO && base + rc.mx < HI) : (base + rc.mx < -LO && base + rc.mn > -HI);
+    }
+    const unsigned long long fails = __ballot(q < ce && !ok);
+    const uint64_t f = fails ? (uint64_t)(__ffsll((long long)fails) - 1) : ce - c;   // chunks c .. c+f-1 pass
+    const long long tot = (long long)((unsigned long long)S + __shfl(inc, (int)(f > 0 ? f - 1 : 0), 64));
+    if (f > 0) s = ldexp((double)tot, e - 52);
+    c += f;
+    if (c < ce) {
+      if (d_segstat_on && lane == 0) atomicAdd(&d_segstat[2], 1ull);
+      const uint64_t lo = k0 + (c - c0) * BN_TILE, hi = min(k1, lo + BN_TILE);
+      s = wave_binade_range(prod, lo, hi, s, lane);
+      c++;
+    }
+  }
+  return s;
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_seg_resolve_w(const uint64_t *ro, const uint32_t *col, const double *a,
+                                                       const double *x, const uint32_t *list, const unsigned *nl,
+                                                       const uint64_t *choff, const SpecRec *rec, double *z) {
+  const int lane = threadIdx.x & 63;
+  const unsigned n = *nl;
+  auto prod = [&](uint64_t k) { return seg_product(a, x, col, k, MODE); };
+  for (uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n;
+       r += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t i = list[r];
+    const uint64_t c0 = choff[r], c1 = choff[r + 1];
+    if (d_segstat_on && lane == 0) { atomicAdd(&d_segstat[0], 1ull); atomicAdd(&d_segstat[1], c1 - c0); }
+    const double s = wave_resolve(prod, rec, c0, c1, ro[i], ro[i + 1], lane);
+    if (lane == 0) z[i] = s;
+  }
+}
+template <int MODE>
+__global__ __launch_bounds__(64) void k_dot_resolve_w(const double *a, const double *b, uint64_t n,
+                                                      const SpecRec *rec, double *out) {
+  const int lane = threadIdx.x & 63;
+  auto prod = [&](uint64_t i) { return bn_product(a, b, i, MODE); };
+  const double s = wave_resolve(prod, rec, 0, (n + BN_TILE - 1) / BN_TILE, 0, n, lane);
+  if (lane == 0) *out = s;
+}
+// AMGD_RESOLVE=block (A/B): the block-per-sum walks above instead of the wavefront ones
+static int g_resolve_wave = -1;
+extern "C" void amgd_set_resolve_wave(int on) { g_resolve_wave = on; }
+static bool resolve_wave() {
+  if (g_resolve_wave < 0) { const char *e = getenv("AMGD_RESOLVE"); g_resolve_wave = !(e && e[0] == 'b'); }
+  return g_resolve_wave > 0;
+}
 // max_entries: an upper bound on the listed rows' total length (the matrix's nnz),
 // nmax on their count: sizes the chunk records
+static void segstat_report() {
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(d_segstat), sizeof h) != hipSuccess) return;
+  fprintf(stderr, "segstat rows %llu chunks %llu failed %llu rounds %llu serial %llu zeroskip %llu\n", h[0], h[1],
+          h[2], h[3], h[4], h[5]);
+}
+static void segstat_init() {
+  static int done = 0;
+  if (done) return;
+  done = 1;
+  const char *e = getenv("AMGD_SEGSTAT");
+  if (!(e && *e && atoi(e))) return;
+  const int one = 1;
+  HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(d_segstat_on), &one, sizeof one));
+  atexit(segstat_report);
+}
 extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
                                 const double *x, const uint32_t *list, const unsigned *nlist,
                                 uint32_t nmax, uint64_t max_entries, double *z) {
   if (!nmax) return;
+  segstat_init();
   hipStream_t st = amgd_s();
   const uint64_t gmax = max_entries / BN_TILE + nmax + 1;
   uint64_t *choff = (uint64_t *)amgd_alloc(((size_t)nmax + 1) * 8);
@@ -1199,12 +1374,18 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
     k_seg_csum<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
     k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
     k_seg_spec<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
-    k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+    if (resolve_wave())
+      k_seg_resolve_w<3><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+    else
+      k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
   } else {
     k_seg_csum<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
     k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
     k_seg_spec<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
-    k_seg_resolve<4><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+    if (resolve_wave())
+      k_seg_resolve_w<4><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+    else
+      k_seg_resolve<4><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
   }
   KCHECK();
   amgd_free(choff); amgd_free(csum); amgd_free(rec);
@@ -1224,7 +1405,8 @@ static void dot_exact_launch(const double *a, const double *b, uint64_t n, doubl
   k_dot_csum<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum);
   k_dot_approx_prefix<<<1, 1024, 0, st>>>(csum, G);
   k_dot_spec<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum, rec);
-  k_dot_resolve<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, rec, out);
+  if (resolve_wave()) k_dot_resolve_w<MODE><<<1, 64, 0, st>>>(a, b, n, rec, out);
+  else k_dot_resolve<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, rec, out);
   amgd_free(csum);
   amgd_free(rec);
 }

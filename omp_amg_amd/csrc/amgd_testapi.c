@@ -137,6 +137,9 @@ API int amgd_test_spmv_tab(const hcsr *HA, const double *x, double alpha, const 
   return 0;
 }
 API void amgd_test_spmv_tab_on(int on) { amgd_spmv_set_tab(on); }
+/* exact sums' resolution: 1 one wavefront per sum (default), 0 one 1024-thread block, -1 env */
+extern void amgd_set_resolve_wave(int on);
+API void amgd_test_resolve_wave(int on) { amgd_set_resolve_wave(on); }
 
 /* build_csr on host COO (u32 indices) */
 API int amgd_test_build(uint64_t nz, const uint32_t *I, const uint32_t *J, const double *V, hcsr *HX) {

@@ -441,7 +441,7 @@ def mv_long(request):
 
 
 @pytest.mark.parametrize("sl_min", [1 << 40, 0], ids=["wave", "lane"])
-def test_spmv_adversarial_rows(sl_min, rw, mv_long, chunk):
+def test_spmv_adversarial_rows(sl_min, rw, mv_long, chunk, resolve):
     """long-row SpMV / row sums / listed rows on adversarial rows through the wave-per-row
     and the lane-per-row kernels (every RW) and, for listed rows past the long-row
     threshold, the block-per-row binade scan, bit for bit against the sequential loop
@@ -466,7 +466,7 @@ def test_spmv_adversarial_rows(sl_min, rw, mv_long, chunk):
                                                                        w[~np.isnan(w)].view(np.uint64))
 
 
-def test_spmv_rows_multichunk_exact():
+def test_spmv_rows_multichunk_exact(resolve):
     """listed rows of 4097 - 130000 entries (many 4096-entry chunks each) through the
     grid-wide speculation + per-row resolve: sums growing across binades, exact ties,
     cancellation to zero, mixed magnitudes, an inf -- bit for bit the sequential loop,
@@ -604,11 +604,20 @@ def _seq(p):
     return s
 
 
+@pytest.fixture(params=[1, 0], ids=["wave_resolve", "block_resolve"])
+def resolve(request):
+    """the speculation's resolution walk: one wavefront per sum (default) or one block"""
+    oa.resolve_wave(request.param)
+    yield request.param
+    oa.resolve_wave(-1)
+
+
 @pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel",
                                   "hover", "big", "pos_big", "spikes"])
-def test_exact_dot_matches_sequential(kind):
+def test_exact_dot_matches_sequential(kind, resolve):
     """The binade-parallel exact sum (single block below 64K products, chunk
-    speculation over all CUs above) equals the left-to-right loop bit for bit."""
+    speculation over all CUs above, resolved by one wavefront or one block) equals the
+    left-to-right loop bit for bit."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
     n = 3000000 if kind in ("big", "pos_big", "spikes") else 300000
     if kind == "normal":
