@@ -1210,44 +1210,22 @@ static void qfactor_range(const dcsr *Wt, const dcsr *A, const uint64_t *qoff, d
   }
   // tiers by support size: the LDS triangle sized to the tier keeps small supports at
   // high occupancy (nz <= 32: 4 KB per wavefront)
-  static int t2blk = -1;
-  if (t2blk < 0) t2blk = getenv("AMGD_QF_T2BLK") ? atoi(getenv("AMGD_QF_T2BLK")) : 3;
-  if (hn[0] && (t2blk & 4))
-    k_qfactor_blk<QF_T0, 8, 64><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
-        lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  else if (hn[0])
+  // <= 32 points: the LDS triangle; 33-64 / 65-128: the blocked kernel, 4 k-steps per pass
+  // (round 5 A/Bs: 8 steps per pass or the LDS kernel on these tiers measured slower)
+  if (hn[0])
     k_qfactor_lds<QF_T0, 64><<<(int)std::min<unsigned>(hn[0], 65536u), 64, 0, s>>>(
         lists, hn[0], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  static int bsm = -1;      // AMGD_QF_BSMALL: k-steps per pass of the 64- / 128-point tiers
-  if (bsm < 0) bsm = getenv("AMGD_QF_BSMALL") ? atoi(getenv("AMGD_QF_BSMALL")) : 4;
-  if (hn[1] && (t2blk & 2) && bsm == 4)
+  if (hn[1])
     k_qfactor_blk<QF_T1, 4, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
         lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  else if (hn[1] && (t2blk & 2))
-    k_qfactor_blk<QF_T1, 8, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
-        lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  else if (hn[1])
-    k_qfactor_lds<QF_T1, 64><<<(int)std::min<unsigned>(hn[1], 65536u), 64, 0, s>>>(
-        lists + L, hn[1], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  if (hn[2] && (t2blk & 1) && bsm == 4)
+  if (hn[2])
     k_qfactor_blk<QF_T2, 4, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
-        lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  else if (hn[2] && (t2blk & 1))
-    k_qfactor_blk<QF_T2, 8, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
-        lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-  else if (hn[2])
-    k_qfactor_lds<QF_T2, 128><<<(int)std::min<unsigned>(hn[2], 65536u), 128, 0, s>>>(
         lists + 2 * L, hn[2], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
   if (qf_blocked()) {
     // B = 4 k-steps per pass for the 256- and 512-point tiers: the waves mostly wait
     // (SQ_WAIT_ANY ~80 %), and the smaller S1/S2 tiles let 4 blocks share a CU
     // (512 tier, 47782-column call at 256^3: B 8 -> 4: 419 -> 318 ms)
-    static int v256 = -1;   // AMGD_QF_B256: steps per pass of the 256-point tier (4 or 8)
-    if (v256 < 0) v256 = getenv("AMGD_QF_B256") ? atoi(getenv("AMGD_QF_B256")) : 4;
-    if (hn[3] && v256 == 8)
-      k_qfactor_blk<256, 8><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
-          lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
-    else if (hn[3])
+    if (hn[3])
       k_qfactor_blk<256, 4><<<(int)std::min<unsigned>(hn[3], 8192u), 256, 0, s>>>(
           lists + 3 * L, hn[3], Wt->ro, Wt->col, A->ro, A->col, A->a, qoff, Q);
     if (hn[4]) amgd_route_hit(AMGD_R_QF_T512);

@@ -1739,14 +1739,6 @@ static bool spmv_sharded(const dcsr *M0, const double *x, double *z, double alph
 static void spmv_impl(const dcsr *M, const double *x, double *z, double alpha, const double *y,
                       double beta, const uint8_t *f) {
   if (M->rn == 0) return;
-  static int mode = -1;
-  if (mode < 0) mode = getenv("AMGD_SPMV_MODE") ? atoi(getenv("AMGD_SPMV_MODE")) : 0;
-  if (mode == 1) {
-    int g = (int)std::min<uint64_t>((M->rn + SPMV_ROWS - 1) / SPMV_ROWS, 16384);
-    k_spmv<<<g, 256, 0, amgd_s()>>>(M->ro, M->col, M->a, M->rn, x, z, alpha, y, beta, f);
-    KCHECK();
-    return;
-  }
   if (M->nnz >= 32ull * M->rn && spmv_sharded(M, x, z, alpha, y, beta, f)) return;
   const int64_t sl_min = sl_min_whole();
   if (M->nnz >= 32ull * M->rn && (int64_t)M->rn >= sl_min) {
@@ -2126,10 +2118,8 @@ extern "C" dcsr *amgd_mpm(double alpha, const dcsr *A, double beta, const dcsr *
     abort();
   }
   hipStream_t s = amgd_s();
-  static int wave = -1;
-  if (wave < 0) wave = getenv("AMGD_MPM_WAVE") ? atoi(getenv("AMGD_MPM_WAVE")) : 1;
   // the wave kernel pays for rows averaging >= MPM_LONG / 4 entries
-  const bool use_w = wave && A->rn && (A->nnz + B->nnz) >= (uint64_t)A->rn * (MPM_LONG / 4);
+  const bool use_w = A->rn && (A->nnz + B->nnz) >= (uint64_t)A->rn * (MPM_LONG / 4);
   uint8_t *lr = nullptr;
   const int gw = (int)std::min<uint64_t>(((uint64_t)A->rn + 3) / 4, 65536);
   uint64_t *cnt = (uint64_t *)amgd_alloc(((size_t)A->rn + 1) * 8);
@@ -3317,34 +3307,23 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
       k_sg_wwin<W_, 1, 0><<<gw, 256, 0, s>>>(rows_, nrw, A->ro, A->col, A->a, B->ro, B->col,     \
                                              B->a, cnt2, cnt, tcol, ta, curs);                  \
   } while (0)
-  // threads per row of the 4096- / 8192-slot k-sequential kernels (AMGD_SG_NT2 / _NT3):
-  // one row per work-group walks its layers one dependent step at a time, so more
-  // wavefronts per table keep more of each layer's loads in flight (256^3: RAP
-  // kernels 1876 -> 1619 ms with 1024 threads on the 8192-slot bin)
-  static int nt3 = -1, nt2 = -1;
-  if (nt3 < 0) { const char *e = getenv("AMGD_SG_NT3"); nt3 = e ? atoi(e) : 1024; }
-  if (nt2 < 0) { const char *e = getenv("AMGD_SG_NT2"); nt2 = e ? atoi(e) : 512; }
+  // threads per row of the 4096- / 8192-slot k-sequential kernels: 512 / 1024 -- one row per
+  // work-group walks its layers one dependent step at a time, so more wavefronts per table
+  // keep more of each layer's loads in flight (256^3: RAP kernels 1876 -> 1619 ms with 1024
+  // threads on the 8192-slot bin; 256 threads on both measured slower, round 2)
   if (hn[0] || hn[1] || hn[2] || hn[3]) amgd_route_hit(kseq ? AMGD_R_SG_KSEQ : AMGD_R_SG_ROW);
   if (win && (wn[0] || wn[2])) amgd_route_hit(AMGD_R_SG_WWIN);
   if (hn[4]) amgd_route_hit(AMGD_R_SG_LONG);
   if (kseq && wide) {
     SG_NUM(k_sg_kseq, 256, 9, 0, 16384u)
     SG_NUM(k_sg_kseq, 256, 11, 1, 16384u)
-    if (nt2 == 1024) { SG_NUM(k_sg_kseq, 1024, 12, 2, 16384u) }
-    else if (nt2 == 512) { SG_NUM(k_sg_kseq, 512, 12, 2, 16384u) }
-    else { SG_NUM(k_sg_kseq, 256, 12, 2, 16384u) }
-    if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
-    else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
-    else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
+    SG_NUM(k_sg_kseq, 512, 12, 2, 16384u)
+    SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u)
   } else if (kseq) {
     SG_NUM(k_sg_kseq, 64, 9, 0, 65536u)
     SG_NUM(k_sg_kseq, 64, 11, 1, 65536u)
-    if (nt2 == 1024) { SG_NUM(k_sg_kseq, 1024, 12, 2, 16384u) }
-    else if (nt2 == 512) { SG_NUM(k_sg_kseq, 512, 12, 2, 16384u) }
-    else { SG_NUM(k_sg_kseq, 256, 12, 2, 16384u) }
-    if (nt3 == 1024) { SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u) }
-    else if (nt3 == 512) { SG_NUM(k_sg_kseq, 512, 13, 3, 8192u) }
-    else { SG_NUM(k_sg_kseq, 256, 13, 3, 8192u) }
+    SG_NUM(k_sg_kseq, 512, 12, 2, 16384u)
+    SG_NUM(k_sg_kseq, 1024, 13, 3, 8192u)
   } else {
     SG_NUM(k_sg_row, 64, 9, 0, 65536u)
     SG_NUM(k_sg_row, 64, 11, 1, 65536u)
