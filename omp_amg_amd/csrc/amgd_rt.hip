@@ -999,6 +999,12 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
 // records (binade_range for a chunk that fails).  The row list and its length live on
 // the device; every kernel reads the length there.
 // ---------------------------------------------------------------------------
+// The long rows' chunks are SEG_TILE = 512 products (the dots keep BN_TILE = 4096): on the
+// anisotropic levels' orphan rows every strong entry is a jump of the running sum into a
+// higher binade, which fails its chunk's speculation -- ~9 of a row's 29 4096-chunks, each
+// then re-summed by binade_range; finer chunks confine a jump to 512 products
+#define SEG_TILE 512
+#define SEG_PER (SEG_TILE / SP_T)
 __device__ __forceinline__ double seg_product(const double *a, const double *x, const uint32_t *col,
                                              uint64_t k, int MODE_) {
   return MODE_ == 3 ? a[k] * x[col[k]] : a[k];
@@ -1014,7 +1020,7 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_prep(const uint64_t *ro, con
     long long c = 0;
     if (r < n) {
       const uint32_t i = list[r];
-      c = (long long)((ro[i + 1] - ro[i] + BN_TILE - 1) / BN_TILE);
+      c = (long long)((ro[i + 1] - ro[i] + SEG_TILE - 1) / SEG_TILE);
     }
     long long total;
     const long long pre = bn_block_excl_scan(c, sh, &total);
@@ -1042,7 +1048,7 @@ __global__ __launch_bounds__(SP_T) void k_seg_csum(const uint64_t *ro, const uin
   for (uint64_t g = blockIdx.x; g < G; g += gridDim.x) {
     const unsigned r = seg_row_of(choff, n, g);
     const uint32_t i = list[r];
-    const uint64_t lo = ro[i] + (g - choff[r]) * BN_TILE, hi = min(ro[i + 1], lo + BN_TILE);
+    const uint64_t lo = ro[i] + (g - choff[r]) * SEG_TILE, hi = min(ro[i + 1], lo + SEG_TILE);
     double t = 0;
     for (uint64_t k = lo + threadIdx.x; k < hi; k += SP_T) t += seg_product(a, x, col, k, MODE);
     red[threadIdx.x] = t;
@@ -1069,7 +1075,7 @@ __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uin
                                                    const uint32_t *list, const unsigned *nl,
                                                    const uint64_t *choff, const double *approx,
                                                    SpecRec *rec) {
-  __shared__ double tile[BN_TILE];
+  __shared__ double tile[SEG_TILE];
   __shared__ long long ssum[SP_T / 64], smin[SP_T / 64], smax[SP_T / 64];
   __shared__ int sflag;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1078,7 +1084,7 @@ __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uin
   for (uint64_t g = blockIdx.x; g < G; g += gridDim.x) {
     const unsigned r = seg_row_of(choff, n, g);
     const uint32_t i = list[r];
-    const uint64_t lo = ro[i] + (g - choff[r]) * BN_TILE, hi = min(ro[i + 1], lo + BN_TILE);
+    const uint64_t lo = ro[i] + (g - choff[r]) * SEG_TILE, hi = min(ro[i + 1], lo + SEG_TILE);
     const int tlen = (int)(hi - lo);
     for (int q = tid; q < tlen; q += SP_T) tile[q] = seg_product(a, x, col, lo + q, MODE);
     if (tid == 0) sflag = 0;
@@ -1088,8 +1094,8 @@ __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uin
     const int e = flag ? 0 : ilogb(gs);
     const double u = ldexp(1.0, e - 52);
     long long loc = 0, lmin = 0x7fffffffffffffffll, lmax = -0x7fffffffffffffffll;
-    const int first = tid * SP_PER;
-    for (int q = 0; q < SP_PER; q++) {
+    const int first = tid * SEG_PER;
+    for (int q = 0; q < SEG_PER; q++) {
       const int idx = first + q;
       if (idx >= tlen) break;
       const double v = tile[idx] / u;
@@ -1183,7 +1189,7 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
       c = run_end;
       if (c < ce) {
         if (d_segstat_on && tid == 0) atomicAdd(&d_segstat[2], 1ull);
-        const uint64_t lo = k0 + (c - c0) * BN_TILE, hi = min(k1, lo + BN_TILE);
+        const uint64_t lo = k0 + (c - c0) * SEG_TILE, hi = min(k1, lo + SEG_TILE);
         s = binade_range<MODE>(a, x, lo, hi, s, tile, sh, &s_sh, &viol_sh, col);
         c++;
       }
@@ -1274,7 +1280,7 @@ __device__ double wave_binade_range(Prod prod, uint64_t lo, uint64_t hi, double 
 // chunk added by wave_binade_range (chunk c covers products [k0 + (c - c0) * BN_TILE, ..))
 template <typename Prod>
 __device__ double wave_resolve(Prod prod, const SpecRec *rec, uint64_t c0, uint64_t c1, uint64_t k0, uint64_t k1,
-                               int lane) {
+                               int lane, uint64_t tile) {
   const long long LO = (1ll << 52), HI = (1ll << 53);
   double s = 0.0;
   uint64_t c = c0;
@@ -1301,7 +1307,7 @@ __device__ double wave_resolve(Prod prod, const SpecRec *rec, uint64_t c0, uint6
     c += f;
     if (c < ce) {
       if (d_segstat_on && lane == 0) atomicAdd(&d_segstat[2], 1ull);
-      const uint64_t lo = k0 + (c - c0) * BN_TILE, hi = min(k1, lo + BN_TILE);
+      const uint64_t lo = k0 + (c - c0) * tile, hi = min(k1, lo + tile);
       s = wave_binade_range(prod, lo, hi, s, lane);
       c++;
     }
@@ -1320,7 +1326,7 @@ __global__ __launch_bounds__(256) void k_seg_resolve_w(const uint64_t *ro, const
     const uint32_t i = list[r];
     const uint64_t c0 = choff[r], c1 = choff[r + 1];
     if (d_segstat_on && lane == 0) { atomicAdd(&d_segstat[0], 1ull); atomicAdd(&d_segstat[1], c1 - c0); }
-    const double s = wave_resolve(prod, rec, c0, c1, ro[i], ro[i + 1], lane);
+    const double s = wave_resolve(prod, rec, c0, c1, ro[i], ro[i + 1], lane, SEG_TILE);
     if (lane == 0) z[i] = s;
   }
 }
@@ -1329,14 +1335,18 @@ __global__ __launch_bounds__(64) void k_dot_resolve_w(const double *a, const dou
                                                       const SpecRec *rec, double *out) {
   const int lane = threadIdx.x & 63;
   auto prod = [&](uint64_t i) { return bn_product(a, b, i, MODE); };
-  const double s = wave_resolve(prod, rec, 0, (n + BN_TILE - 1) / BN_TILE, 0, n, lane);
+  const double s = wave_resolve(prod, rec, 0, (n + BN_TILE - 1) / BN_TILE, 0, n, lane, BN_TILE);
   if (lane == 0) *out = s;
 }
-// AMGD_RESOLVE=block (A/B): the block-per-sum walks above instead of the wavefront ones
+// AMGD_RESOLVE=wave (A/B): the wavefront walks above instead of the block-per-sum ones.  Off
+// by default: they are bit-identical but slower -- one wavefront's loads (a failed chunk's
+// products 64 at a time, the records 64 at a time) wait their latency step by step where
+// the block has all of a tile's loads in flight: configs[4] 29.1 -> 44.9 s, configs[1]
+// 24.5 -> 25.3 s (profiles/r06/resolve_wave_r06j.txt)
 static int g_resolve_wave = -1;
 extern "C" void amgd_set_resolve_wave(int on) { g_resolve_wave = on; }
 static bool resolve_wave() {
-  if (g_resolve_wave < 0) { const char *e = getenv("AMGD_RESOLVE"); g_resolve_wave = !(e && e[0] == 'b'); }
+  if (g_resolve_wave < 0) { const char *e = getenv("AMGD_RESOLVE"); g_resolve_wave = e && e[0] == 'w'; }
   return g_resolve_wave > 0;
 }
 // max_entries: an upper bound on the listed rows' total length (the matrix's nnz),
@@ -1363,7 +1373,7 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
   if (!nmax) return;
   segstat_init();
   hipStream_t st = amgd_s();
-  const uint64_t gmax = max_entries / BN_TILE + nmax + 1;
+  const uint64_t gmax = max_entries / SEG_TILE + nmax + 1;
   uint64_t *choff = (uint64_t *)amgd_alloc(((size_t)nmax + 1) * 8);
   double *csum = (double *)amgd_alloc_f64(gmax * 8);
   SpecRec *rec = (SpecRec *)amgd_alloc(gmax * sizeof(SpecRec));
