@@ -1875,6 +1875,11 @@ __global__ __launch_bounds__(256) void k_lmop_land_wave(
 }
 static int g_lmop_wave = -1;          // test hook: -1 environment / default
 extern "C" void amgd_lmop_set_wave(int n) { g_lmop_wave = n; }
+static int lmop_land_wave_forced() {   // the pruned walk: per wavefront only when forced
+  if (g_lmop_wave >= 0) return g_lmop_wave;
+  const char *e = getenv("AMGD_LMOP_WAVE");
+  return e && *e ? atoi(e) : 0;
+}
 static int lmop_land_wave_min() {     // support size from which the walk runs per wavefront
   if (g_lmop_wave >= 0) return g_lmop_wave;
   static int v = -2;
@@ -2199,7 +2204,10 @@ static bool lmop_pruned(dcsr *S, const dcsr *Wt, const double *Q, uint64_t qo, u
   amgd_free(hs); amgd_free(skey);
   uint64_t *k1 = (uint64_t *)amgd_alloc(n * 8 + 8), *k2 = (uint64_t *)amgd_alloc(n * 8 + 8);
   double *v1 = (double *)amgd_alloc_f64(n * 8 + 8), *v2 = (double *)amgd_alloc_f64(n * 8 + 8);
-  const int wmin = lmop_land_wave_min();
+  // the wavefront walk only when forced (amgd_lmop_set_wave / AMGD_LMOP_WAVE > 0): on the
+  // anisotropic orphan support it measured slower than one thread per walk (222 vs 186 ms
+  // per call: 64 searches per step against one; profiles/r06/aniso256_kernel_stats_r06l.csv)
+  const int wmin = lmop_land_wave_forced();
   if (wmin > 0 && nz >= (uint32_t)wmin) {
     amgd_route_hit(AMGD_R_LMOP_WAVE);
     k_lmop_land_wave_pr<<<grid_for((uint64_t)nz * 64, 256, 65536), 256, 0, s>>>(Wt->col + w0, nz, S->ro, S->col,

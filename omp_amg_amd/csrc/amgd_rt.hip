@@ -1061,12 +1061,33 @@ __global__ __launch_bounds__(SP_T) void k_seg_csum(const uint64_t *ro, const uin
     __syncthreads();
   }
 }
-// per row: chunk sums -> exclusive prefixes (a guess of the running sum; any order)
-__global__ void k_seg_prefix(const unsigned *nl, const uint64_t *choff, double *csum) {
+// per row: chunk sums -> exclusive prefixes (a guess of the running sum; any order), one
+// block per row scanning 256 chunks at a time (one thread walking a row's ~230 chunks
+// serially took 25 us per call, 1.0 s of the anisotropic 256^3 setup)
+__global__ __launch_bounds__(256) void k_seg_prefix(const unsigned *nl, const uint64_t *choff, double *csum) {
+  __shared__ double wsum[4];
   const unsigned n = *nl;
-  GRID_STRIDE(r, n) {
-    double t = 0;
-    for (uint64_t g = choff[r]; g < choff[r + 1]; g++) { const double v = csum[g]; csum[g] = t; t += v; }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (unsigned r = blockIdx.x; r < n; r += gridDim.x) {
+    double carry = 0.0;
+    for (uint64_t g0 = choff[r]; g0 < choff[r + 1]; g0 += 256) {
+      const uint64_t g = g0 + threadIdx.x;
+      const double v = g < choff[r + 1] ? csum[g] : 0.0;
+      double x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[w] = x;
+      __syncthreads();
+      double add = carry;
+      for (int q = 0; q < w; q++) add += wsum[q];
+      const double tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      if (g < choff[r + 1]) csum[g] = add + x - v;
+      __syncthreads();
+      carry += tot;
+    }
   }
 }
 template <int MODE>
@@ -1382,7 +1403,7 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
   k_seg_prep<<<1, BN_THREADS, 0, st>>>(ro, list, nlist, choff);
   if (x) {
     k_seg_csum<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
-    k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
+    k_seg_prefix<<<(int)std::min<uint32_t>(nmax, 1024), 256, 0, st>>>(nlist, choff, csum);
     k_seg_spec<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
     if (resolve_wave())
       k_seg_resolve_w<3><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
@@ -1390,7 +1411,7 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
       k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
   } else {
     k_seg_csum<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
-    k_seg_prefix<<<grid_for(nmax), 256, 0, st>>>(nlist, choff, csum);
+    k_seg_prefix<<<(int)std::min<uint32_t>(nmax, 1024), 256, 0, st>>>(nlist, choff, csum);
     k_seg_spec<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
     if (resolve_wave())
       k_seg_resolve_w<4><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
