@@ -437,7 +437,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab")
+          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab", "sg_symreuse")
 
 
 def route_stats(reset: bool = True) -> dict:
@@ -462,6 +462,19 @@ def lmop_prune(n: int) -> None:
     components emit same-component contributions only (0: never; -1: default 4096 /
     AMGD_LMOP_PRUNE)"""
     lib().amgd_test_lmop_prune(int(n))
+
+
+def spgemm_sym(mode: int) -> None:
+    """the next one-GPU SpGEMM: 1 keeps its symbolic phase, 2 takes the kept one when the
+    operand patterns match (else runs in full), -1 drops a kept state (tests)"""
+    lib().amgd_test_spgemm_sym(int(mode))
+
+
+def spgemm_sym_stats() -> dict:
+    L = lib()
+    k, r = C.c_uint64(), C.c_uint64()
+    L.amgd_test_spgemm_sym_stats(C.byref(k), C.byref(r))
+    return {"kept": k.value, "reused": r.value}
 
 
 def spgemm_win(w: int) -> None:

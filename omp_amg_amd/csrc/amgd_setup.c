@@ -750,6 +750,9 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
        transposes as they come -- the same entries, values and orders -- and only R is
        transposed back, instead of AfW', W.*Arr and R each being transposed once. */
     int trp = 0;
+    /* the final weights share this product's operand patterns (same skeleton): its
+       symbolic phase is kept for the Galerkin Af*W (amgd_spgemm_sym_next) */
+    if (amgd_nshards() == 1) amgd_spgemm_sym_next(1);
     dcsr *AfWx = spgemm_via_t_raw(Af, AfT, Wtmp, Wtmp_t, &trp);
     dcsr *R, *Rt;
     uint64_t *Rperm = NULL;
@@ -1054,7 +1057,9 @@ static int setup_body(void *arg) {
     /* --- Galerkin coarse operator: A = W'*AfP + A(C,F)*W + A(C,C) --- */
     amgd_spgemm_set_timer(0);
     dcsr *Wt = amgd_transpose(W, NULL);
+    if (amgd_nshards() == 1) amgd_spgemm_sym_next(2);   /* the loop's last Af*W symbolic phase */
     dcsr *AfW = spgemm_via_t(Af, AfT, W, Wt);
+    amgd_spgemm_sym_drop();
     dcsr *AfP = amgd_mpm(1., AfW, 1., Afc);
     dcsr_free(&AfW);
     L->AfP = AfP;

@@ -2810,7 +2810,9 @@ extern "C" void amgd_sparse_reset_state(void) {
   g_sg_slot = -1;
   g_sg_pattern = 0;
 }
+static void sym_forget(void);
 extern "C" void amgd_reset_call_state(void) {
+  sym_forget();
   amgd_sparse_reset_state();
   amgd_interp_reset_state();
 }
@@ -3147,25 +3149,84 @@ static void sort_list(uint32_t *list, unsigned n, uint32_t rn) {
   amgd_free(tmp);
   amgd_free(tmpk);
 }
-static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
-  if (A->cn != B->rn) {
-    fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
-    abort();
+// The symbolic phase of a product (upper bounds, row bins, distinct counts, the distinct
+// layout's offsets, the window split) depends only on the operands' patterns.  The
+// interpolation loop's last Af*W (amgd_setup.c interpolation) and the Galerkin product's
+// Af*W (the final weights on the same skeleton) share both patterns, so the first keeps
+// its symbolic state and the second takes it over: only the numeric kernels run again.
+// A kept state is taken only when a hash of both patterns (row offsets and columns) and
+// the shapes match; otherwise the product runs in full.
+struct SgSym {
+  uint32_t rn, acn, bcn;
+  uint64_t annz, bnnz, hash;
+  uint64_t *ub, *cnt;               // per-row upper bounds; distinct layout offsets (scanned)
+  uint32_t *lists, *wlists;         // row bins (numeric bins, sorted, window-split)
+  unsigned hc[SG_MAXBIN], hn[SG_MAXBIN], wn[4];
+  uint64_t dist;
+  bool kseq, wide;
+  int win, nlb;
+};
+static SgSym *g_sym_kept = nullptr;
+static int g_sym_mode = 0;          // the next local product: 1 keeps its symbolic state, 2 may take the kept one
+static uint64_t g_sym_reused = 0, g_sym_kept_n = 0;
+static void sym_free(SgSym *y) {
+  if (!y) return;
+  amgd_free(y->ub); amgd_free(y->cnt); amgd_free(y->lists);
+  if (y->wlists) amgd_free(y->wlists);
+  free(y);
+}
+extern "C" void amgd_spgemm_sym_next(int mode) { g_sym_mode = mode; }
+extern "C" void amgd_spgemm_sym_drop(void) { sym_free(g_sym_kept); g_sym_kept = nullptr; g_sym_mode = 0; }
+extern "C" void amgd_spgemm_sym_stats(uint64_t *kept, uint64_t *reused) { *kept = g_sym_kept_n; *reused = g_sym_reused; }
+// after an unwound setup the kept blocks were released by the rollback: forget them
+static void sym_forget(void) { if (g_sym_kept) free(g_sym_kept); g_sym_kept = nullptr; g_sym_mode = 0; }
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// order-independent hash of a pattern: wrapping sum of mixed (position, value) keys over
+// the row offsets and then the columns
+__global__ void k_pat_hash(const uint64_t *ro, uint32_t rn, const uint32_t *col, uint64_t nnz, uint64_t salt,
+                           unsigned long long *out) {
+  const uint64_t n = (uint64_t)rn + 1 + nnz;
+  uint64_t h = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t v = i <= rn ? ro[i] : (uint64_t)col[i - rn - 1];
+    h += mix64(salt + i * 0x2545f4914f6cdd1dull + (v << 1));
   }
+  atomicAdd(out, (unsigned long long)h);
+}
+static uint64_t pat_hash2(const dcsr *A, const dcsr *B) {
+  unsigned long long *d = (unsigned long long *)amgd_alloc(16);
+  amgd_memset(d, 0, 16);
   hipStream_t s = amgd_s();
-  static int sglog = -1;
-  if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
-  double t_start = 0;
-  if (sglog) { amgd_sync(); t_start = amgd_wtime(); }
+  k_pat_hash<<<grid_for((uint64_t)A->rn + A->nnz + 1, 256, 4096), 256, 0, s>>>(A->ro, A->rn, A->col, A->nnz,
+                                                                                0x5a17ull, d);
+  k_pat_hash<<<grid_for((uint64_t)B->rn + B->nnz + 1, 256, 4096), 256, 0, s>>>(B->ro, B->rn, B->col, B->nnz,
+                                                                                0xb0b5ull, d + 1);
+  KCHECK();
+  unsigned long long h[2];
+  amgd_d2h(h, d, 16);
+  amgd_free(d);
+  return (uint64_t)h[0] * 0x100000001b3ull ^ (uint64_t)h[1];
+}
+
+// symbolic phase: bins, distinct counts and their offsets, the window split
+static SgSym *sg_symbolic(const dcsr *A, const dcsr *B) {
+  hipStream_t s = amgd_s();
+  SgSym *y = (SgSym *)calloc(1, sizeof(SgSym));
   const uint32_t rn = A->rn;
   const uint64_t L = (uint64_t)rn + 1;
-  uint64_t *ub = (uint64_t *)amgd_alloc(L * 8);
-  uint32_t *lists = (uint32_t *)amgd_alloc((size_t)SG_MAXBIN * L * 4);
+  y->rn = rn; y->acn = A->cn; y->bcn = B->cn; y->annz = A->nnz; y->bnnz = B->nnz;
+  uint64_t *ub = y->ub = (uint64_t *)amgd_alloc(L * 8);
+  uint32_t *lists = y->lists = (uint32_t *)amgd_alloc((size_t)SG_MAXBIN * L * 4);
   unsigned *counts = (unsigned *)amgd_alloc(64);
-  uint64_t *cnt = (uint64_t *)amgd_alloc(L * 8);
+  uint64_t *cnt = y->cnt = (uint64_t *)amgd_alloc(L * 8);
   HIPCK(hipMemsetAsync(counts, 0, 64, s));
   HIPCK(hipMemsetAsync(cnt, 0, L * 8, s));
-  unsigned hc[SG_MAXBIN] = {0};
+  unsigned *hc = y->hc;
   // tiny rows (<= SG_TINY products): their own list (bin slot 5) and kernel, left out
   // of every other bin (AMGD_SG_TINY=0: off)
   static int tiny_on = -1;
@@ -3183,15 +3244,14 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     sort_list(lists + L, hc[1], rn);           // the wide rows (cheap ones: no gain measured)
   }
   const unsigned ntiny = hc[5];
-  if (ntiny) amgd_route_hit(AMGD_R_SG_TINY);
   if (ntiny)
     k_sg_tiny<0><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
                                                             B->col, B->a, cnt, nullptr, nullptr, nullptr);
   // symbolic: distinct count per row (row order in the lists is arbitrary; rows are independent)
   // long B rows (mean >= KSEQ_MIN): the k-sequential kernels; short ones: flat enumeration
   const uint64_t avgB = B->rn ? B->nnz / B->rn : 0;
-  const bool kseq = avgB >= KSEQ_MIN && !sg_force_flat();
-  const bool wide = avgB >= 256;
+  const bool kseq = y->kseq = avgB >= KSEQ_MIN && !sg_force_flat();
+  y->wide = avgB >= 256;
   if (hc[0]) {
     if (kseq)
       k_sg_kseq<64, 12, 0><<<(int)std::min<unsigned>(hc[0], 65536u), 64, 0, s>>>(
@@ -3201,17 +3261,18 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
           lists, hc[0], A->ro, A->col, A->a, B->ro, B->col, B->a, 2048, cnt, nullptr, nullptr, nullptr);
   }
   // wide symbolic rows of long-B-row products: wave-private bit-map windows (k_sg_wwin
-  // MODE 2); their cursors live in `curs` (one per A entry)
-  uint32_t *curs = nullptr;
-  if (kseq) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
+  // MODE 2); their cursors live in `curs` (one per A entry, scratch of each kernel)
   if (hc[1]) {
     if (kseq) {
       amgd_route_hit(AMGD_R_SG_WWIN_SYM);
+      uint32_t *curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
       // bit-map windows of 32768 columns in 4 KB (round 4; the 4096-column byte maps
       // took 1239 against 909 ms per 256^3 setup, profiles/r04/ab_sym_ww)
       k_sg_wwin<32768, 2><<<(int)std::min<unsigned>((hc[1] + 3) / 4, 16384u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, nullptr, B->ro, B->col, nullptr, cnt, nullptr, nullptr,
           nullptr, curs);
+      KCHECK();
+      amgd_free(curs);
     } else {
       k_sg_row<256, 14, 0><<<(int)std::min<unsigned>(hc[1], 8192u), 256, 0, s>>>(
           lists + L, hc[1], A->ro, A->col, A->a, B->ro, B->col, B->a, 8192, cnt, nullptr, nullptr,
@@ -3220,7 +3281,7 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
   KCHECK();
   // numeric bins by distinct count: wave/512, wave/2048, wave/4096, block/8192 slots, dense slab
-  unsigned hn[SG_MAXBIN] = {0};
+  unsigned *hn = y->hn;
   if (rn) {
     HIPCK(hipMemsetAsync(counts, 0, 64, s));
     SgBins b;
@@ -3231,48 +3292,23 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     amgd_d2h(hn, counts, 20);
     for (int q = 1; q < 5; q++) sort_list(lists + q * L, hn[q], rn);
   }
-  double *slab_v = nullptr;
-  uint32_t *slab_s = nullptr;
-  const uint32_t *densel = lists + 4 * L;
-  int nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
+  y->nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
   if (hn[4]) {                    // recount (rows past the hash capacity carry OVERFLOW_MARK)
-    slab_v = (double *)amgd_alloc_f64((size_t)nlb * B->cn * 8 + 8);
-    slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
-    HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
-    k_spgemm_long<0><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col, B->a,
-                                          B->cn, slab_v, slab_s, cnt, nullptr, nullptr, nullptr);
+    double *slab_v = (double *)amgd_alloc_f64((size_t)y->nlb * B->cn * 8 + 8);
+    uint32_t *slab_s = (uint32_t *)amgd_alloc((size_t)y->nlb * B->cn * 4 + 4);
+    HIPCK(hipMemsetAsync(slab_s, 0, (size_t)y->nlb * B->cn * 4, s));
+    k_spgemm_long<0><<<y->nlb, 256, 0, s>>>(lists + 4 * L, hn[4], A->ro, A->col, A->a, B->ro, B->col, B->a,
+                                             B->cn, slab_v, slab_s, cnt, nullptr, nullptr, nullptr);
     KCHECK();
+    amgd_free(slab_v);
+    amgd_free(slab_s);
   }
-  uint64_t dist = amgd_scan_u64(cnt, rn);   // cnt := offsets of the distinct layout
-  uint32_t *tcol = (uint32_t *)amgd_alloc(dist * 4 + 4);
-  double *ta = (double *)amgd_alloc_f64(dist * 8 + 8);
-  uint64_t *cnt2 = (uint64_t *)amgd_alloc(L * 8);
-  HIPCK(hipMemsetAsync(cnt2, 0, L * 8, s));
-  if (hn[4]) HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
-  if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
-#define SG_NUM(KER, NT, LG, bin, gmax)                                                          \
-  if (hn[bin]) {                                                                                \
-    if (pat)                                                                                    \
-      KER<NT, LG, 2, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
-          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
-    else if (rap)                                                                               \
-      KER<NT, LG, 1, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
-          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
-    else                                                                                        \
-      KER<NT, LG, 1, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
-          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
-  }
-  const bool rap = g_sg_slot >= 0;
-  const bool pat = g_sg_pattern != 0;
-  if (ntiny)
-    k_sg_tiny<1><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
-                                                            B->col, B->a, cnt2, cnt, tcol, ta);
-  const int win = kseq ? sg_win() : 0;
+  y->dist = amgd_scan_u64(cnt, rn);   // cnt := offsets of the distinct layout
+  const int win = y->win = kseq ? sg_win() : 0;
   // wide bins (3: block hash, 4: dense slab) split into windowed / hash rows
-  uint32_t *wlists = nullptr;
-  unsigned wn[4] = {0, 0, 0, 0};
+  unsigned *wn = y->wn;
   if (win && (hn[3] || hn[4])) {
-    wlists = (uint32_t *)amgd_alloc(2 * L * 4 + 16);
+    uint32_t *wlists = y->wlists = (uint32_t *)amgd_alloc(2 * L * 4 + 16);
     unsigned *wc = (unsigned *)amgd_alloc(32);
     HIPCK(hipMemsetAsync(wc, 0, 32, s));
     const uint32_t p0 = g_sg_win_forced ? 0u : sg_win_p0();
@@ -3296,7 +3332,57 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     amgd_free(wc);
     hn[3] = wn[1];
     hn[4] = wn[3];
+    y->nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
   }
+  amgd_free(counts);
+  return y;
+}
+
+// numeric phase on a symbolic state: every output the ordered sum of its products
+static dcsr *sg_numeric(const dcsr *A, const dcsr *B, const SgSym *y) {
+  hipStream_t s = amgd_s();
+  const uint32_t rn = A->rn;
+  const uint64_t L = (uint64_t)rn + 1;
+  const uint32_t *lists = y->lists, *wlists = y->wlists, *tlist = lists + 5 * L;
+  const unsigned *hn = y->hn, *wn = y->wn;
+  const unsigned ntiny = y->hc[5];
+  if (ntiny) amgd_route_hit(AMGD_R_SG_TINY);
+  const bool kseq = y->kseq, wide = y->wide;
+  const int win = y->win, nlb = y->nlb;
+  const uint64_t *cnt = y->cnt;
+  const uint64_t dist = y->dist;
+  uint32_t *tcol = (uint32_t *)amgd_alloc(dist * 4 + 4);
+  double *ta = (double *)amgd_alloc_f64(dist * 8 + 8);
+  uint64_t *cnt2 = (uint64_t *)amgd_alloc(L * 8);
+  HIPCK(hipMemsetAsync(cnt2, 0, L * 8, s));
+  const uint32_t *densel = lists + 4 * L;
+  double *slab_v = nullptr;
+  uint32_t *slab_s = nullptr;
+  if (hn[4]) {
+    slab_v = (double *)amgd_alloc_f64((size_t)nlb * B->cn * 8 + 8);
+    slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
+    HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
+  }
+  uint32_t *curs = nullptr;
+  if (win && (wn[0] || wn[2])) curs = (uint32_t *)amgd_alloc(A->nnz * 4 + 4);
+  if (g_sg_slot >= 0) amgd_timer_start(g_sg_slot);
+#define SG_NUM(KER, NT, LG, bin, gmax)                                                          \
+  if (hn[bin]) {                                                                                \
+    if (pat)                                                                                    \
+      KER<NT, LG, 2, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
+          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
+    else if (rap)                                                                               \
+      KER<NT, LG, 1, 1><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
+          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
+    else                                                                                        \
+      KER<NT, LG, 1, 0><<<(int)std::min<unsigned>(hn[bin], gmax), NT, 0, s>>>(                 \
+          lists + (bin) * L, hn[bin], A->ro, A->col, A->a, B->ro, B->col, B->a, 0, cnt2, cnt, tcol, ta); \
+  }
+  const bool rap = g_sg_slot >= 0;
+  const bool pat = g_sg_pattern != 0;
+  if (ntiny)
+    k_sg_tiny<1><<<grid_for(ntiny, 256, 16384), 256, 0, s>>>(tlist, ntiny, A->ro, A->col, A->a, B->ro,
+                                                            B->col, B->a, cnt2, cnt, tcol, ta);
 #define SG_WW(W_, rows_, nrw)                                                                   \
   do {                                                                                          \
     const int gw = (int)std::min<unsigned>((nrw + 3) / 4, 16384u);                              \
@@ -3356,23 +3442,62 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
   }
   dcsr *X = (dcsr *)malloc(sizeof(dcsr));
   X->rn = rn; X->cn = B->cn; X->nnz = nz;
+  X->ro = cnt2;
   if (nz == dist) {               // no cancellation: the distinct layout is final
-    X->ro = cnt2; X->col = tcol; X->a = ta;
-    amgd_free(cnt);
+    X->col = tcol; X->a = ta;
   } else {                        // compact away exact-zero sums
-    X->ro = cnt2;
     X->col = (uint32_t *)amgd_alloc(nz * 4 + 4);
     X->a = (double *)amgd_alloc_f64(nz * 8 + 8);
     amgd_compact_rows(cnt, tcol, ta, cnt2, rn, X->col, X->a);
-    amgd_free(cnt); amgd_free(tcol); amgd_free(ta);
+    amgd_free(tcol); amgd_free(ta);
   }
-  amgd_free(ub); amgd_free(lists); amgd_free(counts);
-  if (wlists) amgd_free(wlists);
   if (curs) amgd_free(curs);
   if (slab_v) { amgd_free(slab_v); amgd_free(slab_s); }
+  return X;
+}
+
+static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
+  if (A->cn != B->rn) {
+    fprintf(stderr, "omp_amg_amd: spgemm inner dimension mismatch (%u vs %u)\n", A->cn, B->rn);
+    abort();
+  }
+  hipStream_t s = amgd_s();
+  static int sglog = -1;
+  if (sglog < 0) sglog = getenv("AMGD_SGLOG") != nullptr;
+  double t_start = 0;
+  if (sglog) { amgd_sync(); t_start = amgd_wtime(); }
+  const uint32_t rn = A->rn;
+  const int mode = g_sym_mode;
+  g_sym_mode = 0;
+  SgSym *y = nullptr;
+  const uint64_t h = mode ? pat_hash2(A, B) : 0;
+  if (mode == 2 && g_sym_kept) {
+    const SgSym *k = g_sym_kept;
+    const bool kseq = B->rn && B->nnz / B->rn >= KSEQ_MIN && !sg_force_flat();
+    if (k->hash == h && k->rn == rn && k->acn == A->cn && k->bcn == B->cn && k->annz == A->nnz &&
+        k->bnnz == B->nnz && k->kseq == kseq && k->win == (kseq ? sg_win() : 0)) {
+      y = g_sym_kept;
+      g_sym_kept = nullptr;
+      g_sym_reused++;
+      amgd_route_hit(AMGD_R_SG_SYMREUSE);
+    }
+  }
+  const bool reused = y != nullptr;
+  if (!y) y = sg_symbolic(A, B);
+  dcsr *X = sg_numeric(A, B, y);
+  const SgSym info = *y;                    // bin counts for the log
+  if (mode == 1) {                          // kept for the next product on these patterns
+    amgd_spgemm_sym_drop();
+    y->hash = h;
+    g_sym_kept = y;
+    g_sym_kept_n++;
+  } else {
+    sym_free(y);
+    if (mode == 2) amgd_spgemm_sym_drop();  // one taker only
+  }
   if (sglog) {
     uint64_t prods = 0;
-    if (rn) {   // products = sum of the per-row upper bounds (recomputed: ub was freed)
+    if (rn) {   // products = sum of the per-row upper bounds
       uint64_t *u2 = (uint64_t *)amgd_alloc(((size_t)rn + 1) * 8);
       k_spgemm_ub<<<grid_for(rn), 256, 0, s>>>(A->ro, A->col, rn, B->ro, u2);
       prods = amgd_scan_u64(u2, rn);
@@ -3381,18 +3506,21 @@ static dcsr *spgemm_local(const dcsr *A, const dcsr *B) {
     amgd_sync();
     double ms = (amgd_wtime() - t_start) * 1e3;
     if (rn) {
-      unsigned long long *h = (unsigned long long *)amgd_alloc(64), hh[6];
-      amgd_memset(h, 0, 48);
-      k_span_hist<<<grid_for(rn), 256, 0, s>>>(X->ro, X->col, rn, h);
-      amgd_d2h(hh, h, 48);
-      amgd_free(h);
+      unsigned long long *hd = (unsigned long long *)amgd_alloc(64), hh[6];
+      amgd_memset(hd, 0, 48);
+      k_span_hist<<<grid_for(rn), 256, 0, s>>>(X->ro, X->col, rn, hd);
+      amgd_d2h(hh, hd, 48);
+      amgd_free(hd);
       fprintf(stderr, "spgemm span hist (rows >= 1024 out): %llu %llu %llu %llu %llu %llu\n", hh[0],
               hh[1], hh[2], hh[3], hh[4], hh[5]);
     }
-    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  %s  sym %u/%u num %u/%u/%u/%u dense %u win %u  %.2f ms\n",
-            rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)nz,
-            (unsigned long)prods, prods / (ms * 1e6), kseq ? (wide ? (win ? "kseq-w+win" : "kseq-w") : (win ? "kseq+win" : "kseq")) : "flat",
-            hc[0], hc[1], hn[0], hn[1], hn[2], hn[3], hn[4], wn[0] + wn[2], ms);
+    const char *kind = info.kseq ? (info.wide ? (info.win ? "kseq-w+win" : "kseq-w") : (info.win ? "kseq+win" : "kseq"))
+                                 : "flat";
+    fprintf(stderr, "spgemm %u x %u x %u  nnzA %lu nnzB %lu -> %lu  prods %lu (%.1f G/s)  %s  sym %u/%u num %u/%u/%u/%u dense %u win %u%s  %.2f ms\n",
+            rn, A->cn, B->cn, (unsigned long)A->nnz, (unsigned long)B->nnz, (unsigned long)X->nnz,
+            (unsigned long)prods, prods / (ms * 1e6), kind, info.hc[0], info.hc[1], info.hn[0], info.hn[1],
+            info.hn[2], info.hn[3], info.hn[4], info.wn[0] + info.wn[2],
+            mode == 1 ? " kept" : reused ? " symbolic-reused" : "", ms);
   }
   return X;
 }

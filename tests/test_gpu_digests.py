@@ -45,16 +45,16 @@ def _mk():
 # kernel tests (test_gpu_kernels.py, mv_long / fs_long fixtures) cover it.
 EXPECT_ROUTES = {
     "p7_48": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
-              "qf_reuse"),
+              "qf_reuse", "sg_symreuse"),
     "p7_64": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
-              "qf_reuse", "mv_pair", "fs_amx"),
+              "qf_reuse", "mv_pair", "fs_amx", "sg_symreuse"),
     "p7_96": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx"),
+              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse"),
     "p7_128": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx"),
+               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse"),
     "aniso_20": ("fs_inc",),
     "aniso_32": ("fs_inc", "spmv_pipe"),
-    "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin", "sg_wwin_sym"),
+    "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin", "sg_wwin_sym", "sg_symreuse"),
     "sem_e3_N7": ("spmv_pipe", "sg_wwin_sym"),
     "sem_e4_N7": ("spmv_pipe", "sg_kseq", "sg_wwin_sym"),
     "sem_e5_N7": ("spmv_pipe", "sg_kseq"),

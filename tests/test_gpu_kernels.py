@@ -193,6 +193,62 @@ def test_spgemm_wave_windows(case, win):
     assert refops.same(X, R)
 
 
+@pytest.mark.parametrize("case", ["flat", "banded", "dense_rows", "tiny"])
+def test_spgemm_symbolic_reuse(case):
+    """a product's symbolic phase kept (amgd_spgemm_sym_next(1)) and taken over by the next
+    product on the same operand patterns with other values (the Galerkin Af*W after the
+    interpolation loop's last one): the numeric kernels alone give mxm's bits, including
+    sums that now cancel to an exact zero; operands of another pattern are refused by the
+    pattern hash and the product runs in full"""
+    rng = np.random.default_rng({"flat": 61, "banded": 62, "dense_rows": 63, "tiny": 64}[case])
+    if case == "flat":
+        A = refops.rand_csr(rng, 300, 200, 0.03, ints=True)
+        B = refops.rand_csr(rng, 200, 250, 0.03, ints=True)
+    elif case == "banded":
+        A, B = _banded(rng, 301, 400, 6000, 60, 0.7, 150, 3000)
+    elif case == "dense_rows":
+        A = refops.rand_csr(rng, 20, 200, 0.3, ints=True)
+        B = refops.rand_csr(rng, 200, 9000, 0.05, ints=True)
+    else:
+        A = refops.rand_csr(rng, 2000, 300, 0.005, ints=True)
+        B = refops.rand_csr(rng, 300, 120, 0.03, ints=True)
+
+    def revalue(M):
+        v = rng.integers(-2, 3, size=M.a.size).astype(float)
+        return refops.Csr(M.rn, M.cn, M.row_off, M.col, v)
+
+    A2, B2 = revalue(A), revalue(B)
+    st0 = oa.spgemm_sym_stats()
+    oa.spgemm_sym(1)
+    X1 = oa.test_csr_op(0, A, B)
+    oa.spgemm_sym(2)
+    X2 = oa.test_csr_op(0, A2, B2)
+    st1 = oa.spgemm_sym_stats()
+    assert refops.same(X1, refops.spgemm(A, B))
+    assert refops.same(X2, refops.spgemm(A2, B2))
+    assert st1["kept"] == st0["kept"] + 1 and st1["reused"] == st0["reused"] + 1
+    # another pattern: one entry of A moved to a free column of its row
+    col = A.col.copy()
+    r = int(np.argmax(np.diff(A.row_off) > 0))
+    k = int(A.row_off[r])
+    free = sorted(set(range(A.cn)) - set(col[A.row_off[r]:A.row_off[r + 1]].tolist()))
+    col[k] = free[0]
+    o = slice(int(A.row_off[r]), int(A.row_off[r + 1]))
+    order = np.argsort(col[o], kind="stable")
+    col[o] = col[o][order]
+    a3 = A.a.copy()
+    a3[o] = a3[o][order]
+    A3 = refops.Csr(A.rn, A.cn, A.row_off, col, a3)
+    oa.spgemm_sym(1)
+    oa.test_csr_op(0, A, B)
+    oa.spgemm_sym(2)
+    X3 = oa.test_csr_op(0, A3, B)
+    st2 = oa.spgemm_sym_stats()
+    assert refops.same(X3, refops.spgemm(A3, B))
+    assert st2["reused"] == st1["reused"], "a kept state was taken by another pattern"
+    oa.spgemm_sym(-1)
+
+
 @pytest.mark.parametrize("case", ["short", "long_b", "wide", "tiny", "nonpositive"])
 def test_spgemm_pattern(case):
     """amgd_spgemm_pattern (the constraint operator's pattern W_skel * W_skel'): operands
