@@ -437,7 +437,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab", "sg_symreuse")
+          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab", "sg_symreuse", "spat_inc")
 
 
 def route_stats(reset: bool = True) -> dict:
@@ -462,6 +462,18 @@ def lmop_prune(n: int) -> None:
     components emit same-component contributions only (0: never; -1: default 4096 /
     AMGD_LMOP_PRUNE)"""
     lib().amgd_test_lmop_prune(int(n))
+
+
+def spat_inc(on: int) -> None:
+    """the constraint operator's pattern grown from the previous iteration's (1, default) or
+    formed whole every iteration (0); -1: as AMGD_SPAT_INC says"""
+    lib().amgd_test_spat_inc(int(on))
+
+
+def spat_stats() -> dict:
+    out = (C.c_uint64 * 3)()
+    lib().amgd_test_spat_stats(out)
+    return {"incremental": out[0], "whole": out[1], "same": out[2]}
 
 
 def spgemm_sym(mode: int) -> None:

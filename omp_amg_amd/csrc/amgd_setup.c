@@ -351,14 +351,92 @@ typedef struct {
   dcsr *W0, *W0t;    /* W0 of this skeleton (lambda = 0) and its transpose, likewise reused */
 } skel_factor;
 
+static dcsr *g_prevS;
 static void factor_free(skel_factor *f) {
   dcsr_free(&f->Wt);
   amgd_free(f->kpos);
   amgd_free(f->Q);
   amgd_free(f->qoff);
-  if (f->S) dcsr_free(&f->S);
+  if (f->S) {                          /* kept: the next iteration's S grows from its pattern */
+    dcsr_free(&g_prevS);
+    g_prevS = f->S;
+    f->S = NULL;
+  }
   if (f->W0) dcsr_free(&f->W0);
   if (f->W0t) dcsr_free(&f->W0t);
+}
+
+/* The constraint operator's pattern S = pattern(Wn Wn') (Wn: W_skel without its zero
+   entries, every value > 0, so no sum cancels -- amgd_spgemm_pattern) across one level's
+   interpolation loop.  expand_support only adds skeleton entries (late iterations +0.004 %
+   to +1 %).  With dW = Wn \ Wn_prev:
+     pattern(Wn Wn') = pattern(Wn_prev Wn_prev') U pattern(Wn dW') U pattern(Wn dW')'
+   (S(i,j) needs a k with Wn(i,k) and Wn(j,k): both old -> the old S; Wn(j,k) new -> Wn dW';
+   Wn(i,k) new -> (Wn dW')'), so the previous S is merged (mpm on positive values: a sorted
+   union) with the small product instead of the whole product being formed again.  Taken
+   only when Wn_prev is a subset of Wn (ones(Wn) - ones(Wn_prev) has no negative entry) and
+   Wn's values are all > 0.  The same pattern, sorted, as the product; interp_lmop then
+   writes every value.  AMGD_SPAT_INC=0 / amgd_spat_set_inc(0): the whole product each time. */
+static dcsr *g_prevS = NULL, *g_prevWn = NULL;   /* the last iteration's S and Wn (values 1) */
+static int g_spat_inc = -1;
+static uint64_t g_spat_stats[3];                  /* incremental, whole, same pattern */
+static int spat_inc_on(void) {
+  if (g_spat_inc < 0) { const char *e = getenv("AMGD_SPAT_INC"); g_spat_inc = e && *e ? atoi(e) : 1; }
+  return g_spat_inc;
+}
+void amgd_spat_set_inc(int on) { g_spat_inc = on; }
+void amgd_spat_stats(uint64_t *out) { for (int q = 0; q < 3; q++) out[q] = g_spat_stats[q]; }
+/* after an unwound setup the kept blocks were released by the rollback: forget them */
+void amgd_spat_forget(void) { g_prevS = NULL; g_prevWn = NULL; }
+static void spat_drop(void) { dcsr_free(&g_prevS); dcsr_free(&g_prevWn); }
+static dcsr *s_pattern(const dcsr *W_skel, const dcsr *Wt) {
+  dcsr *Wn = amgd_drop_zeros(W_skel);
+  dcsr *S = NULL;
+  const int pos = Wn->nnz == 0 || amgd_count_gt(Wn->a, Wn->nnz, 0.0, NULL) == Wn->nnz;
+  if (spat_inc_on() && pos && g_prevS && g_prevWn && g_prevWn->rn == Wn->rn && g_prevWn->cn == Wn->cn &&
+      g_prevS->rn == Wn->rn && Wn->nnz >= g_prevWn->nnz) {
+    dcsr *W1 = dcsr_empty_like_pattern(Wn);
+    amgd_vfill(W1->a, W1->nnz, 1.0);
+    dcsr *dW = amgd_mpm(1.0, W1, -1.0, g_prevWn);      /* new entries +1, lost entries -1 */
+    dcsr_free(&W1);
+    if (dW->nnz == Wn->nnz - g_prevWn->nnz && (dW->nnz == 0 || amgd_count_gt(dW->a, dW->nnz, 0.0, NULL) == dW->nnz)) {
+      if (dW->nnz == 0) {                                /* the same skeleton: the same pattern */
+        S = g_prevS;
+        g_prevS = NULL;
+        g_spat_stats[2]++;
+        amgd_route_hit(AMGD_R_SPAT_INC);
+      } else {
+        dcsr *dWt = amgd_transpose(dW, NULL);
+        dcsr *P = amgd_spgemm_pattern(Wn, dWt);
+        dcsr_free(&dWt);
+        amgd_vfill(P->a, P->nnz, 1.0);
+        dcsr *Pt = amgd_transpose(P, NULL);
+        dcsr *PP = amgd_mpm(1.0, P, 1.0, Pt);
+        dcsr_free(&P); dcsr_free(&Pt);
+        amgd_vfill(g_prevS->a, g_prevS->nnz, 1.0);
+        S = amgd_mpm(1.0, g_prevS, 1.0, PP);
+        dcsr_free(&PP);
+        g_spat_stats[0]++;
+        amgd_route_hit(AMGD_R_SPAT_INC);
+      }
+    }
+    dcsr_free(&dW);
+  }
+  if (!S) {
+    dcsr *Wnt = amgd_drop_zeros(Wt);
+    S = amgd_spgemm_pattern(Wn, Wnt);
+    dcsr_free(&Wnt);
+    g_spat_stats[1]++;
+  }
+  dcsr_free(&g_prevS);                                   /* the caller's S becomes the next one's */
+  dcsr_free(&g_prevWn);
+  if (spat_inc_on() && pos) {
+    amgd_vfill(Wn->a, Wn->nnz, 1.0);
+    g_prevWn = Wn;
+  } else {
+    dcsr_free(&Wn);
+  }
+  return S;
 }
 
 /* solve_constraint (amg_setup.c:1499) */
@@ -373,11 +451,9 @@ static void solve_constraint(double *lam, const dcsr *W_skel, skel_factor *fac, 
        skeleton entries (min_skel's orphans at column 0) contribute +0 products only,
        so the product of the operands without them is the same matrix, values and
        pattern -- without the orphans' dense all-zero block of products. */
-    dcsr *Wn = amgd_drop_zeros(W_skel), *Wnt = amgd_drop_zeros(fac->Wt);
     /* lmop overwrites every value of S (interp_lmop zeroes St first, amg_setup.c:1609): the
        pattern is all that is needed, and the skeleton values are all 1: no sum cancels */
-    fac->S = amgd_spgemm_pattern(Wn, Wnt);
-    dcsr_free(&Wn); dcsr_free(&Wnt);
+    fac->S = s_pattern(W_skel, fac->Wt);
     ph(PH_SPAT);
     amgd_lmop(fac->S, W_skel, fac->kpos, fac->Wt, fac->Q, fac->qoff, au2);
     if (phases_on())
@@ -837,6 +913,7 @@ static dcsr *interpolation(const dcsr *Af, const dcsr *AfT, const dcsr *Ac, cons
     factor_free(&fac);
   }
   dcsr_free(&W_skel); dcsr_free(&Amt);
+  spat_drop();
   amgd_free(Df); amgd_free(Dfinv); amgd_free(uc); amgd_free(tmp); amgd_free(v); amgd_free(b);
   amgd_free(Dc); amgd_free(Dcinv); amgd_free(lam); amgd_free(alpha); amgd_free(Dcs);
   amgd_free(w1); amgd_free(w2); amgd_free(onesc); amgd_free(r); amgd_free(rs1);

@@ -2813,6 +2813,7 @@ extern "C" void amgd_sparse_reset_state(void) {
 static void sym_forget(void);
 extern "C" void amgd_reset_call_state(void) {
   sym_forget();
+  amgd_spat_forget();
   amgd_sparse_reset_state();
   amgd_interp_reset_state();
 }

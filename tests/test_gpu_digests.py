@@ -45,16 +45,16 @@ def _mk():
 # kernel tests (test_gpu_kernels.py, mv_long / fs_long fixtures) cover it.
 EXPECT_ROUTES = {
     "p7_48": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
-              "qf_reuse", "sg_symreuse"),
+              "qf_reuse", "sg_symreuse", "spat_inc"),
     "p7_64": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "sg_tiny", "sg_wwin", "sg_wwin_sym",
-              "qf_reuse", "mv_pair", "fs_amx", "sg_symreuse"),
+              "qf_reuse", "mv_pair", "fs_amx", "sg_symreuse", "spat_inc"),
     "p7_96": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse"),
+              "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse", "spat_inc"),
     "p7_128": ("cs_inc", "fs_inc", "spmv_pipe", "mv_rw4", "mv_rw16", "sg_tiny", "sg_wwin",
-               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse"),
+               "sg_wwin_sym", "qf_reuse", "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "sg_symreuse", "spat_inc"),
     "aniso_20": ("fs_inc",),
     "aniso_32": ("fs_inc", "spmv_pipe"),
-    "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin", "sg_wwin_sym", "sg_symreuse"),
+    "p27_20": ("fs_inc", "spmv_pipe", "sg_wwin_sym", "sg_symreuse", "spat_inc"),
     "sem_e3_N7": ("spmv_pipe", "sg_wwin_sym"),
     "sem_e4_N7": ("spmv_pipe", "sg_kseq", "sg_wwin_sym"),
     "sem_e5_N7": ("spmv_pipe", "sg_kseq"),
@@ -97,6 +97,28 @@ def test_gpu_matches_digest_unfused_selection(case):
     finally:
         oa.fs_amx(-1)
     assert oa.route_stats(reset=True)["fs_amx"] == 0
+    got = mk.hierarchy_digest(h)
+    exp = d["arrays"]
+    bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
+    assert not bad, f"{len(bad)} arrays differ from the {d['source']}: {bad[:12]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["p7_64", "p27_20"])
+def test_gpu_matches_digest_whole_constraint_pattern(case):
+    """the constraint operator's pattern W_skel W_skel' formed whole in every interpolation
+    iteration instead of grown from the previous iteration's (the default since round 6):
+    the same stored digest either way"""
+    mk = _mk()
+    d = _db()["cases"][case]
+    Ai, Aj, Av = mk.generate(d["gen"])
+    oa.spat_inc(0)
+    oa.route_stats(reset=True)
+    try:
+        h = abi.run_setup(oa.lib(), Ai, Aj, Av)
+    finally:
+        oa.spat_inc(-1)
+    assert oa.route_stats(reset=True)["spat_inc"] == 0
     got = mk.hierarchy_digest(h)
     exp = d["arrays"]
     bad = sorted(k for k in set(got) | set(exp) if got.get(k) != exp.get(k))
