@@ -437,7 +437,7 @@ def qf_stats() -> dict:
 
 ROUTES = ("spmv_pipe", "mv_long", "sg_tiny", "sg_kseq", "sg_wwin", "sg_wwin_sym", "sg_long",
           "cs_inc", "fs_inc", "sg_row", "mv_rw4", "qf_reuse", "lmop_wave", "mv_rw16", "mv_rw64",
-          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab", "sg_symreuse", "spat_inc")
+          "qf_t512", "qf_t1024", "mv_pair", "fs_amx", "mv_tab", "sg_symreuse", "spat_inc", "sg_drsort")
 
 
 def route_stats(reset: bool = True) -> dict:
@@ -462,6 +462,12 @@ def lmop_prune(n: int) -> None:
     components emit same-component contributions only (0: never; -1: default 4096 /
     AMGD_LMOP_PRUNE)"""
     lib().amgd_test_lmop_prune(int(n))
+
+
+def spgemm_dr_sort(on: int) -> None:
+    """SpGEMM rows past the hash bins' capacity by sorting their products (1, default) or by
+    the one-block dense-slab kernel (0); -1: as AMGD_DR_SORT says"""
+    lib().amgd_test_spgemm_dr_sort(int(on))
 
 
 def spat_inc(on: int) -> None:

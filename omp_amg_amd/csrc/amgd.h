@@ -94,7 +94,7 @@ dcsr *dcsr_empty_like_pattern(const dcsr *A);   /* same ro/col, fresh a */
 enum { AMGD_R_SPMV_PIPE, AMGD_R_MV_LONG, AMGD_R_SG_TINY, AMGD_R_SG_KSEQ, AMGD_R_SG_WWIN,
        AMGD_R_SG_WWIN_SYM, AMGD_R_SG_LONG, AMGD_R_CS_INC, AMGD_R_FS_INC, AMGD_R_SG_ROW,
        AMGD_R_MV_RW4, AMGD_R_QF_REUSE, AMGD_R_LMOP_WAVE, AMGD_R_MV_RW16, AMGD_R_MV_RW64,
-       AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_MV_PAIR, AMGD_R_FS_AMX, AMGD_R_MV_TAB, AMGD_R_SG_SYMREUSE, AMGD_R_SPAT_INC, AMGD_R_N };
+       AMGD_R_QF_T512, AMGD_R_QF_T1024, AMGD_R_MV_PAIR, AMGD_R_FS_AMX, AMGD_R_MV_TAB, AMGD_R_SG_SYMREUSE, AMGD_R_SPAT_INC, AMGD_R_SG_DRSORT, AMGD_R_N };
 extern uint64_t amgd_route_ctr[32];
 #define amgd_route_hit(r) (amgd_route_ctr[(r)]++)
 

@@ -2772,6 +2772,178 @@ __global__ __launch_bounds__(256) void k_spgemm_long(
 
 void amgd_compact_rows(const uint64_t *sro, const uint32_t *scol, const double *sa,
                        const uint64_t *dro, uint32_t rn, uint32_t *dcol, double *da);
+// Dense rows (past the hash bins' capacity) by sorting, one row at a time (round 6).
+// k_spgemm_long gives such a row one work-group: its layers (A entries) run one after the
+// other with a barrier each, then a block scan walks the row's whole column span to emit
+// -- on the anisotropic grids' orphan rows (10^4 - 10^5 layers, spans of millions of
+// columns) 58 ms a call, 1.7 s of configs[4].  Here every product of the row is written in
+// layer order (A entries ascending, the last of duplicate columns, each B row ascending),
+// a stable radix sort by column keeps that order within every column, and each column's
+// run is summed from +0.0 left to right by one thread: the same sums as the layer walk
+// (`acc[j] = acc[j] + b * a` in ascending k), exact zeros dropped, columns ascending.
+__global__ void k_dr_len(const uint64_t *aro, const uint32_t *acol, const uint64_t *bro, uint32_t i,
+                         uint64_t *len) {
+  const uint64_t a0 = aro[i], n = aro[i + 1] - a0;
+  GRID_STRIDE(e, n) {
+    const uint32_t k = acol[a0 + e];
+    len[e] = (e + 1 < n && acol[a0 + e + 1] == k) ? 0 : bro[k + 1] - bro[k];
+  }
+}
+template <int MODE>
+__global__ void k_dr_gen(const uint64_t *aro, const uint32_t *acol, const double *aa, const uint64_t *bro,
+                         const uint32_t *bcol, const double *ba, uint32_t i, const uint64_t *off, uint32_t *key,
+                         double *val) {
+  const uint64_t a0 = aro[i], n = aro[i + 1] - a0;
+  const int lane = threadIdx.x & 63;
+  for (uint64_t e = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < n;
+       e += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t k = acol[a0 + e];
+    if (e + 1 < n && acol[a0 + e + 1] == k) continue;        // duplicate column: the last one wins
+    const double av = MODE == 1 ? aa[a0 + e] : 0.0;
+    const uint64_t b0 = bro[k], b1 = bro[k + 1], o = off[e] - b0;
+    for (uint64_t kb = b0 + lane; kb < b1; kb += 64) {
+      key[o + kb] = bcol[kb];
+      if (MODE == 1) val[o + kb] = ba[kb] * av;
+    }
+  }
+}
+__global__ void k_dr_heads(const uint32_t *key, uint64_t n, uint64_t *flag) {
+  GRID_STRIDE(p, n) flag[p] = (p == 0 || key[p] != key[p - 1]) ? 1 : 0;
+}
+__global__ void k_dr_headpos(const uint32_t *key, uint64_t n, const uint64_t *run, uint64_t *head) {
+  GRID_STRIDE(p, n) if (p == 0 || key[p] != key[p - 1]) head[run[p]] = p;
+  if (blockIdx.x == 0 && threadIdx.x == 0) head[run[n]] = n;     // run[n] = number of runs
+}
+__global__ void k_dr_sum(const double *val, const uint64_t *head, uint64_t nruns, double *sum, uint64_t *nzf) {
+  GRID_STRIDE(r, nruns) {
+    double acc = 0.0;
+    for (uint64_t p = head[r]; p < head[r + 1]; p++) acc = acc + val[p];
+    sum[r] = acc;
+    nzf[r] = acc != 0.0 ? 1 : 0;
+  }
+}
+__global__ void k_dr_emit(const uint32_t *key, const uint64_t *head, const double *sum, const uint64_t *pos,
+                          uint64_t nruns, const uint64_t *xro, uint32_t i, uint32_t *xcol, double *xa,
+                          uint64_t *cnt) {
+  const uint64_t base = xro[i];
+  GRID_STRIDE(r, nruns) if (pos[r + 1] != pos[r]) {
+    xcol[base + pos[r]] = key[head[r]];
+    xa[base + pos[r]] = sum[r];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[i] = pos[nruns];
+}
+__global__ void k_dr_count(const uint64_t *run, uint64_t n, uint32_t i, uint64_t *cnt) { cnt[i] = run[n]; }
+#define DR_MAX_PRODUCTS (1ull << 28)
+// rows[0..nrows) (device list) by sorting; false (nothing done) when a row's products pass
+// DR_MAX_PRODUCTS -- the caller then takes the block kernel.  MODE 0: cnt[i] := distinct
+// columns (only for rows marked OVERFLOW_MARK); MODE 1: nonzero sums at xro[i], cnt[i] := count.
+// the rows to process (MODE 0: only those whose count overflowed) with their A-row bounds,
+// gathered on the device: one readback instead of one per row
+__global__ void k_dr_pick(const uint32_t *rows, unsigned nrows, const uint64_t *cnt, int mode, const uint64_t *aro,
+                          uint32_t *prow, uint64_t *pab, unsigned *np) {
+  GRID_STRIDE(r, nrows) {
+    const uint32_t i = rows[r];
+    if (mode == 0 && cnt[i] != OVERFLOW_MARK) continue;
+    const unsigned q = atomicAdd(np, 1u);
+    prow[q] = i;
+    pab[2 * q] = aro[i];
+    pab[2 * q + 1] = aro[i + 1];
+  }
+}
+static bool dense_rows_sorted(int mode, const uint32_t *rows, unsigned nrows_all, const dcsr *A, const dcsr *B,
+                              uint64_t *cnt, const uint64_t *xro, uint32_t *xcol, double *xa) {
+  hipStream_t s = amgd_s();
+  unsigned nrows = 0;
+  std::vector<uint32_t> hr;
+  std::vector<uint64_t> ne;
+  {
+    uint32_t *prow = (uint32_t *)amgd_alloc((size_t)nrows_all * 4 + 4);
+    uint64_t *pab = (uint64_t *)amgd_alloc((size_t)nrows_all * 16 + 16);
+    unsigned *np = (unsigned *)amgd_alloc(16);
+    amgd_memset(np, 0, 4);
+    k_dr_pick<<<grid_for(nrows_all), 256, 0, s>>>(rows, nrows_all, cnt, mode, A->ro, prow, pab, np);
+    KCHECK();
+    amgd_d2h(&nrows, np, 4);
+    hr.resize(nrows);
+    ne.resize(nrows);
+    if (nrows) {
+      std::vector<uint64_t> ab(2 * (size_t)nrows);
+      amgd_d2h(hr.data(), prow, (size_t)nrows * 4);
+      amgd_d2h(ab.data(), pab, (size_t)nrows * 16);
+      for (unsigned q = 0; q < nrows; q++) ne[q] = ab[2 * q + 1] - ab[2 * q];
+    }
+    amgd_free(prow); amgd_free(pab); amgd_free(np);
+  }
+  std::vector<uint64_t *> offs(nrows, nullptr);
+  std::vector<uint64_t> np(nrows, 0);
+  bool ok = true;
+  for (unsigned q = 0; q < nrows && ok; q++) {
+    offs[q] = (uint64_t *)amgd_alloc((ne[q] + 1) * 8);
+    if (ne[q]) k_dr_len<<<grid_for(ne[q]), 256, 0, s>>>(A->ro, A->col, B->ro, hr[q], offs[q]);
+    np[q] = amgd_scan_u64(offs[q], ne[q]);
+    if (np[q] > DR_MAX_PRODUCTS) ok = false;
+  }
+  if (ok) {
+    for (unsigned q = 0; q < nrows; q++) {
+      if (!offs[q]) continue;
+      const uint32_t i = hr[q];
+      const uint64_t n = np[q];
+      uint32_t *k1 = (uint32_t *)amgd_alloc(n * 4 + 4), *k2 = (uint32_t *)amgd_alloc(n * 4 + 4);
+      double *v1 = mode ? (double *)amgd_alloc_f64(n * 8 + 8) : nullptr;
+      double *v2 = mode ? (double *)amgd_alloc_f64(n * 8 + 8) : nullptr;
+      if (ne[q]) {
+        if (mode)
+          k_dr_gen<1><<<grid_for(ne[q] * 64, 256, 16384), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a,
+                                                                        i, offs[q], k1, v1);
+        else
+          k_dr_gen<0><<<grid_for(ne[q] * 64, 256, 16384), 256, 0, s>>>(A->ro, A->col, A->a, B->ro, B->col, B->a,
+                                                                        i, offs[q], k1, nullptr);
+      }
+      KCHECK();
+      size_t tb = 0;
+      const int eb = bits_for(B->cn);
+      void *tmp;
+      if (mode) {
+        HIPCK(rocprim::radix_sort_pairs(nullptr, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
+        tmp = amgd_alloc(tb + 16);
+        HIPCK(rocprim::radix_sort_pairs(tmp, tb, k1, k2, v1, v2, (size_t)n, 0, eb, s));
+      } else {
+        HIPCK(rocprim::radix_sort_keys(nullptr, tb, k1, k2, (size_t)n, 0, eb, s));
+        tmp = amgd_alloc(tb + 16);
+        HIPCK(rocprim::radix_sort_keys(tmp, tb, k1, k2, (size_t)n, 0, eb, s));
+      }
+      amgd_free(tmp);
+      uint64_t *run = (uint64_t *)amgd_alloc((n + 1) * 8);
+      if (n) k_dr_heads<<<grid_for(n), 256, 0, s>>>(k2, n, run);
+      const uint64_t nruns = amgd_scan_u64(run, n);
+      if (mode == 0) {
+        k_dr_count<<<1, 1, 0, s>>>(run, n, i, cnt);
+      } else {
+        uint64_t *head = (uint64_t *)amgd_alloc((nruns + 1) * 8);
+        k_dr_headpos<<<grid_for(n ? n : 1), 256, 0, s>>>(k2, n, run, head);
+        double *sum = (double *)amgd_alloc_f64(nruns * 8 + 8);
+        uint64_t *pos = (uint64_t *)amgd_alloc((nruns + 1) * 8);
+        if (nruns) k_dr_sum<<<grid_for(nruns), 256, 0, s>>>(v2, head, nruns, sum, pos);
+        amgd_scan_u64(pos, nruns);
+        k_dr_emit<<<grid_for(nruns ? nruns : 1), 256, 0, s>>>(k2, head, sum, pos, nruns, xro, i, xcol, xa, cnt);
+        KCHECK();
+        amgd_free(head); amgd_free(sum); amgd_free(pos);
+      }
+      KCHECK();
+      amgd_free(run); amgd_free(k1); amgd_free(k2);
+      if (v1) { amgd_free(v1); amgd_free(v2); }
+    }
+  }
+  for (unsigned q = 0; q < nrows; q++) amgd_free(offs[q]);
+  return ok;
+}
+static int g_dr_sort = -1;        // AMGD_DR_SORT=0 / amgd_spgemm_set_dr_sort(0): dense rows by the block kernel
+static bool dr_sort_on() {
+  if (g_dr_sort < 0) { const char *e = getenv("AMGD_DR_SORT"); g_dr_sort = e && *e ? atoi(e) : 1; }
+  return g_dr_sort != 0;
+}
+extern "C" void amgd_spgemm_set_dr_sort(int on) { g_dr_sort = on < 0 ? -1 : on; }
+
 
 // event timing of the numeric SpGEMM kernels (the RAP products) + algorithmic bytes:
 // A (12 B/nnz + 8 B/row), B (12 B/nnz + 8 B/row) and X (12 B/nnz + 8 B/row) once each.
@@ -3294,7 +3466,9 @@ static SgSym *sg_symbolic(const dcsr *A, const dcsr *B) {
     for (int q = 1; q < 5; q++) sort_list(lists + q * L, hn[q], rn);
   }
   y->nlb = (int)std::min<unsigned>(hn[4], LONG_BLOCKS);
-  if (hn[4]) {                    // recount (rows past the hash capacity carry OVERFLOW_MARK)
+  if (hn[4] && dr_sort_on() && dense_rows_sorted(0, lists + 4 * L, hn[4], A, B, cnt, nullptr, nullptr, nullptr)) {
+    amgd_route_hit(AMGD_R_SG_DRSORT);
+  } else if (hn[4]) {             // recount (rows past the hash capacity carry OVERFLOW_MARK)
     double *slab_v = (double *)amgd_alloc_f64((size_t)y->nlb * B->cn * 8 + 8);
     uint32_t *slab_s = (uint32_t *)amgd_alloc((size_t)y->nlb * B->cn * 4 + 4);
     HIPCK(hipMemsetAsync(slab_s, 0, (size_t)y->nlb * B->cn * 4, s));
@@ -3359,7 +3533,8 @@ static dcsr *sg_numeric(const dcsr *A, const dcsr *B, const SgSym *y) {
   const uint32_t *densel = lists + 4 * L;
   double *slab_v = nullptr;
   uint32_t *slab_s = nullptr;
-  if (hn[4]) {
+  const bool drs = hn[4] && dr_sort_on();
+  if (hn[4] && !drs) {
     slab_v = (double *)amgd_alloc_f64((size_t)nlb * B->cn * 8 + 8);
     slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
     HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
@@ -3423,7 +3598,17 @@ static dcsr *sg_numeric(const dcsr *A, const dcsr *B, const SgSym *y) {
   // against 987 ms for the interpolation's windowed products, profiles/r04/ab_sym_ww)
   if (win && wn[0]) SG_WW(1024, wlists, wn[0]);
   if (win && wn[2]) SG_WW(1024, wlists + L, wn[2]);
-  if (hn[4]) {
+  bool dr_done = false;
+  if (drs) {
+    dr_done = dense_rows_sorted(1, densel, hn[4], A, B, cnt2, cnt, tcol, ta);
+    if (dr_done) amgd_route_hit(AMGD_R_SG_DRSORT);
+    else {                        // a row past DR_MAX_PRODUCTS: the block kernel for all
+      slab_v = (double *)amgd_alloc_f64((size_t)nlb * B->cn * 8 + 8);
+      slab_s = (uint32_t *)amgd_alloc((size_t)nlb * B->cn * 4 + 4);
+      HIPCK(hipMemsetAsync(slab_s, 0, (size_t)nlb * B->cn * 4, s));
+    }
+  }
+  if (hn[4] && !dr_done) {
     if (rap)
       k_spgemm_long<1, 1><<<nlb, 256, 0, s>>>(densel, hn[4], A->ro, A->col, A->a, B->ro, B->col,
                                                B->a, B->cn, slab_v, slab_s, cnt2, cnt, tcol, ta);

@@ -56,12 +56,85 @@ def test_spgemm_long_rows_and_cancellation():
     assert refops.same(X, R)
 
 
-def test_spgemm_dense_overflow_rows():
-    """rows with more than 4096 distinct columns take the dense-slab path"""
+@pytest.mark.parametrize("sort", [1, 0])
+def test_spgemm_dense_overflow_rows(sort):
+    """rows with more than 4096 distinct columns: their products sorted by column (stable:
+    ascending k within a column) and each column summed from +0 (sort=1, the default), or the
+    one-block dense-slab kernel (sort=0)"""
     rng = np.random.default_rng(8)
     A = refops.rand_csr(rng, 12, 1500, 0.5)
     B = refops.rand_csr(rng, 1500, 7000, 0.02)
-    assert refops.same(oa.test_csr_op(0, A, B), refops.spgemm(A, B))
+    R = refops.spgemm(A, B)
+    for flat in (False, True):
+        oa.route_stats(reset=True)
+        oa.spgemm_dr_sort(sort)
+        oa.spgemm_win(0)            # wide rows stay in the hash / dense bins (no windows)
+        oa.spgemm_flat(flat)
+        try:
+            X = oa.test_csr_op(0, A, B)
+        finally:
+            oa.spgemm_dr_sort(-1)
+            oa.spgemm_win(-1)
+            oa.spgemm_flat(False)
+        routes = oa.route_stats(reset=True)
+        assert routes["sg_long"] > 0
+        assert (routes["sg_drsort"] > 0) == bool(sort)
+        assert refops.same(X, R)
+
+
+@pytest.mark.parametrize("sort", [1, 0])
+@pytest.mark.parametrize("case", ["cancel_dups", "kseq_wide", "empty_mix"])
+def test_spgemm_dense_rows_sorted(case, sort):
+    """dense rows with duplicate A columns (the last one wins), exact cancellation to +0 /
+    -0 (dropped), rows of both k-sequential and flat products, dense rows next to empty and
+    short rows: the sorted path against the host restatement, bit for bit"""
+    rng = np.random.default_rng({"cancel_dups": 71, "kseq_wide": 72, "empty_mix": 73}[case])
+    if case == "cancel_dups":
+        A = refops.rand_csr(rng, 10, 900, 0.6, ints=True)
+        B = refops.rand_csr(rng, 900, 9000, 0.01, ints=True)
+        cols, vals, ro = [], [], [0]
+        for i in range(A.rn):
+            for k in range(A.row_off[i], A.row_off[i + 1]):
+                cols.append(A.col[k]); vals.append(A.a[k])
+                if k % 5 == 0:
+                    cols.append(A.col[k]); vals.append(-A.a[k])
+            ro.append(len(cols))
+        A = refops.Csr(A.rn, A.cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+    elif case == "kseq_wide":
+        A = refops.rand_csr(rng, 16, 300, 0.5, ints=True)
+        B = refops.rand_csr(rng, 300, 20000, 0.01, ints=True)
+    else:
+        A = refops.rand_csr(rng, 60, 1200, 0.02, ints=True)
+        ro = A.row_off.copy()
+        # rows 7 and 31 dense, row 8 emptied
+        dense = {7: np.arange(0, 1200, 2), 31: np.arange(1, 1200, 3)}
+        cols, vals, ro = [], [], [0]
+        for i in range(A.rn):
+            if i in dense:
+                c = dense[i]
+                v = rng.integers(-2, 3, size=c.size).astype(float)
+            elif i == 8:
+                c, v = np.array([], dtype=np.int64), np.array([])
+            else:
+                c = A.col[A.row_off[i]:A.row_off[i + 1]]
+                v = A.a[A.row_off[i]:A.row_off[i + 1]]
+            cols += list(c); vals += list(v); ro.append(len(cols))
+        A = refops.Csr(A.rn, A.cn, np.array(ro), np.array(cols, dtype=np.int64), np.array(vals))
+        B = refops.rand_csr(rng, 1200, 15000, 0.006, ints=True)
+    R = refops.spgemm(A, B)
+    for win in (0, -1):
+        oa.route_stats(reset=True)
+        oa.spgemm_dr_sort(sort)
+        oa.spgemm_win(win)
+        try:
+            X = oa.test_csr_op(0, A, B)
+        finally:
+            oa.spgemm_dr_sort(-1)
+            oa.spgemm_win(-1)
+        routes = oa.route_stats(reset=True)
+        if win == 0:
+            assert routes["sg_long"] > 0 and (routes["sg_drsort"] > 0) == bool(sort)
+        assert refops.same(X, R)
 
 
 @pytest.mark.parametrize("win", [0, 4096, 8192, 16384])
