@@ -296,6 +296,12 @@ def resolve_wave(on: int) -> None:
     lib().amgd_test_resolve_wave(int(on))
 
 
+def seg_split(on: int) -> None:
+    """long-row exact sums: a chunk with one binade crossing resolved from its split record
+    (1, default) or re-summed by the binade scan (0); -1: as AMGD_SEG_SPLIT says"""
+    lib().amgd_test_seg_split(int(on))
+
+
 def spmv_tab(on: int) -> None:
     """gather tables for pinned long-row matrices (1 default, 0 off, -1 environment)"""
     lib().amgd_test_spmv_tab_on(int(on))

@@ -1090,15 +1090,205 @@ __global__ __launch_bounds__(256) void k_seg_prefix(const unsigned *nl, const ui
     }
   }
 }
+// One binade crossing inside a chunk (round 6).  On the anisotropic orphan rows a strong
+// entry jumps the running sum by ~10^3 -- into a higher binade -- so its chunk fails the
+// whole-chunk record and was re-summed by binade_range (a tile load and 2-3 block rounds).
+// The split record describes such a chunk as part 1 = [0, j) in the guessed binade e1, the
+// crossing product p_j, and part 2 = (j, len) in the binade e2 of the guessed sum after it:
+// the resolve checks part 1 against the exact running sum as a whole-chunk record is
+// checked (s1 = (S + M1) u1 exactly), adds p_j the ordinary way (s2 = fl(s1 + p_j), the
+// sequential loop's own step), checks part 2 against s2 in e2 and takes s3 = (S2 + M2) u2 --
+// the sequential sum, O(1) per chunk.  A second crossing, a tie or a failed check: the
+// chunk goes to binade_range as before.
+struct SegSplit { long long M1, mn1, mx1, M2, mn2, mx2; double pj; int e1, e2, ok; };
+__device__ __forceinline__ long long blk4_excl_scan(long long v, long long *sm, long long *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sm[w] = x;
+  __syncthreads();
+  long long before = 0;
+  for (int q = 0; q < w; q++) before += sm[q];
+  *total = sm[0] + sm[1] + sm[2] + sm[3];
+  __syncthreads();
+  return before + x - v;
+}
+__device__ __forceinline__ void blk4_minmax(long long &mn, long long &mx, long long *sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) { sm[w] = mn; sm[4 + w] = mx; }
+  __syncthreads();
+  mn = sm[0]; mx = sm[4];
+  for (int q = 1; q < 4; q++) { mn = sm[q] < mn ? sm[q] : mn; mx = sm[4 + q] > mx ? sm[4 + q] : mx; }
+  __syncthreads();
+}
+// the split record of a chunk whose products are tile[0, tlen) (SP_T threads, SEG_PER each)
+__device__ void seg_split(const double *tile, int tlen, double gs, SegSplit *out, long long *sm, int *jsh) {
+  const int tid = threadIdx.x;
+  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll, NONE_MX = -0x7fffffffffffffffll;
+  SegSplit r;
+  r.ok = 0;
+  const bool normal = fabs(gs) >= 2.2250738585072014e-308 && fabs(gs) < 1e300;
+  if (!normal) {                                  // uniform: no split record
+    if (tid == 0) *out = r;
+    return;
+  }
+  const int e1 = ilogb(gs);
+  const double u1 = ldexp(1.0, e1 - 52);
+  const long long Sg = (long long)ldexp(gs, 52 - e1);
+  const int first = tid * SEG_PER;
+  long long m[SEG_PER];
+  bool bad[SEG_PER];
+  long long loc = 0;
+#pragma unroll
+  for (int q = 0; q < SEG_PER; q++) {
+    const int idx = first + q;
+    m[q] = 0;
+    bad[q] = false;
+    if (idx < tlen) {
+      const double v = tile[idx] / u1, rr = rint(v);
+      if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) bad[q] = true;
+      else m[q] = (long long)rr;
+    }
+    loc += m[q];
+  }
+  long long tot;
+  const long long pre = blk4_excl_scan(loc, sm, &tot);
+  // the first index whose element is bad or whose guessed running value leaves the binade
+  if (tid == 0) *jsh = 0x7fffffff;
+  __syncthreads();
+  {
+    long long run = pre;
+#pragma unroll
+    for (int q = 0; q < SEG_PER; q++) {
+      const int idx = first + q;
+      if (idx >= tlen) break;
+      if (bad[q]) { atomicMin(jsh, idx); break; }
+      run += m[q];
+      const long long g = Sg + run;
+      const bool inside = Sg > 0 ? (g > LO && g < HI) : (g < -LO && g > -HI);
+      if (!inside) { atomicMin(jsh, idx); break; }
+    }
+  }
+  __syncthreads();
+  const int j = *jsh;
+  __syncthreads();
+  if (j >= tlen) {                               // no crossing under the guess
+    if (tid == 0) *out = r;
+    return;
+  }
+  // part 1: [0, j) relative to the entry value
+  long long mn1 = NONE_MN, mx1 = NONE_MX, M1 = 0;
+  {
+    long long run = pre;
+#pragma unroll
+    for (int q = 0; q < SEG_PER; q++) {
+      const int idx = first + q;
+      if (idx >= j) break;
+      run += m[q];
+      mn1 = run < mn1 ? run : mn1;
+      mx1 = run > mx1 ? run : mx1;
+    }
+  }
+  // M1 = sum of m over [0, j): the thread owning j - 1 knows it
+  if (tid == 0) sm[8] = 0;
+  __syncthreads();
+  if (j > 0 && first <= j - 1 && j - 1 < first + SEG_PER) {
+    long long run = pre;
+    for (int q = 0; first + q < j; q++) run += m[q];
+    sm[8] = run;
+  }
+  __syncthreads();
+  M1 = sm[8];
+  __syncthreads();
+  blk4_minmax(mn1, mx1, sm);
+  const double pj = tile[j];
+  const double gs2 = (double)(Sg + M1) * u1 + pj;   // a guess of the sum after the crossing
+  const bool normal2 = fabs(gs2) >= 2.2250738585072014e-308 && fabs(gs2) < 1e300;
+  const int e2 = normal2 ? ilogb(gs2) : 0;
+  const double u2 = ldexp(1.0, e2 - 52);
+  // part 2: (j, tlen) relative to the value after the crossing
+  long long loc2 = 0;
+  int bad2 = normal2 ? 0 : 1;
+#pragma unroll
+  for (int q = 0; q < SEG_PER; q++) {
+    const int idx = first + q;
+    m[q] = 0;
+    if (idx > j && idx < tlen) {
+      const double v = tile[idx] / u2, rr = rint(v);
+      if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) bad2 = 1;
+      else m[q] = (long long)rr;
+    }
+    loc2 += m[q];
+  }
+  long long tot2;
+  const long long pre2 = blk4_excl_scan(loc2, sm, &tot2);
+  long long mn2 = NONE_MN, mx2 = NONE_MX;
+  {
+    long long run = pre2;
+#pragma unroll
+    for (int q = 0; q < SEG_PER; q++) {
+      const int idx = first + q;
+      if (idx <= j || idx >= tlen) continue;
+      run += m[q];
+      mn2 = run < mn2 ? run : mn2;
+      mx2 = run > mx2 ? run : mx2;
+    }
+  }
+  blk4_minmax(mn2, mx2, sm);
+  if (tid == 0) *jsh = 0;
+  __syncthreads();
+  if (bad2) atomicOr(jsh, 1);
+  __syncthreads();
+  const int anybad2 = *jsh;
+  if (tid == 0) {
+    r.M1 = M1; r.mn1 = mn1; r.mx1 = mx1;
+    r.M2 = tot2; r.mn2 = mn2; r.mx2 = mx2;
+    r.pj = pj; r.e1 = e1; r.e2 = e2;
+    r.ok = anybad2 ? 0 : 1;
+    *out = r;
+  }
+  __syncthreads();
+}
+// the split chunk from the exact running sum s: the sum after it in *out, false if a check fails
+__device__ __forceinline__ bool seg_split_apply(const SegSplit &r, double s, double *out) {
+  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll;
+  if (!r.ok || !(fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1e300) || ilogb(s) != r.e1) return false;
+  const long long S = (long long)ldexp(s, 52 - r.e1);
+  if (r.mn1 != NONE_MN) {                          // part 1 non-empty: every partial sum inside
+    const bool in1 = S > 0 ? (S + r.mn1 > LO && S + r.mx1 < HI) : (S + r.mx1 < -LO && S + r.mn1 > -HI);
+    if (!in1) return false;
+  }
+  const double s1 = ldexp((double)(S + r.M1), r.e1 - 52);
+  const double s2 = s1 + r.pj;                     // the crossing step, as the loop adds it
+  if (r.mn2 == NONE_MN) { *out = s2; return true; }   // nothing after the crossing
+  if (!(fabs(s2) >= 2.2250738585072014e-308 && fabs(s2) < 1e300) || ilogb(s2) != r.e2) return false;
+  const long long S2 = (long long)ldexp(s2, 52 - r.e2);
+  const bool in2 = S2 > 0 ? (S2 + r.mn2 > LO && S2 + r.mx2 < HI) : (S2 + r.mx2 < -LO && S2 + r.mn2 > -HI);
+  if (!in2) return false;
+  *out = ldexp((double)(S2 + r.M2), r.e2 - 52);
+  return true;
+}
 template <int MODE>
 __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, const double *x,
                                                    const uint32_t *list, const unsigned *nl,
                                                    const uint64_t *choff, const double *approx,
-                                                   SpecRec *rec) {
+                                                   SpecRec *rec, SegSplit *rec2) {
   __shared__ double tile[SEG_TILE];
   __shared__ long long ssum[SP_T / 64], smin[SP_T / 64], smax[SP_T / 64];
   __shared__ int sflag;
+  __shared__ long long ssm[9];
+  __shared__ int sj, sneed;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const unsigned n = *nl;
   const uint64_t G = choff[n];
@@ -1155,7 +1345,17 @@ __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uin
       SpecRec rc;
       rc.M = run; rc.mn = gmn; rc.mx = gmx; rc.e = e; rc.flag = sflag;
       rec[g] = rc;
+      // under the guess, would the whole-chunk record fail?  then a split record
+      const bool gnormal = fabs(gs) >= 1e-290 && fabs(gs) < 1e300;
+      const long long Sg = gnormal ? (long long)ldexp(gs, 52 - e) : 0;
+      const long long LO = (1ll << 52), HI = (1ll << 53);
+      const bool inside = !sflag && gnormal &&
+                          (Sg > 0 ? (Sg + gmn > LO && Sg + gmx < HI) : (Sg + gmx < -LO && Sg + gmn > -HI));
+      sneed = rec2 && !inside;
     }
+    __syncthreads();
+    if (sneed) seg_split(tile, tlen, gs, rec2 + g, ssm, &sj);
+    else if (rec2 && tid == 0) rec2[g].ok = 0;
     __syncthreads();
   }
 }
@@ -1166,7 +1366,7 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
                                                             const double *a, const double *x,
                                                             const uint32_t *list, const unsigned *nl,
                                                             const uint64_t *choff, const SpecRec *rec,
-                                                            double *z) {
+                                                            const SegSplit *rec2, double *z) {
   __shared__ double tile[BN_TILE];
   __shared__ long long sh[BN_THREADS / 64 + 1];
   __shared__ double s_sh;
@@ -1210,8 +1410,22 @@ __global__ __launch_bounds__(BN_THREADS) void k_seg_resolve(const uint64_t *ro, 
       c = run_end;
       if (c < ce) {
         if (d_segstat_on && tid == 0) atomicAdd(&d_segstat[2], 1ull);
-        const uint64_t lo = k0 + (c - c0) * SEG_TILE, hi = min(k1, lo + SEG_TILE);
-        s = binade_range<MODE>(a, x, lo, hi, s, tile, sh, &s_sh, &viol_sh, col);
+        // one crossing inside the chunk: its split record, O(1) (thread 0)
+        if (tid == 0) {
+          double s3;
+          const bool okk = rec2 && seg_split_apply(rec2[c], s, &s3);
+          viol_sh = okk ? 1 : 0;
+          if (okk) s_sh = s3;
+          if (okk && d_segstat_on) atomicAdd(&d_segstat[6], 1ull);
+        }
+        __syncthreads();
+        const bool split_done = viol_sh == 1;
+        if (split_done) s = s_sh;
+        __syncthreads();
+        if (!split_done) {
+          const uint64_t lo = k0 + (c - c0) * SEG_TILE, hi = min(k1, lo + SEG_TILE);
+          s = binade_range<MODE>(a, x, lo, hi, s, tile, sh, &s_sh, &viol_sh, col);
+        }
         c++;
       }
     }
@@ -1375,8 +1589,8 @@ static bool resolve_wave() {
 static void segstat_report() {
   unsigned long long h[8];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(d_segstat), sizeof h) != hipSuccess) return;
-  fprintf(stderr, "segstat rows %llu chunks %llu failed %llu rounds %llu serial %llu zeroskip %llu\n", h[0], h[1],
-          h[2], h[3], h[4], h[5]);
+  fprintf(stderr, "segstat rows %llu chunks %llu failed %llu rounds %llu serial %llu zeroskip %llu split %llu\n", h[0],
+          h[1], h[2], h[3], h[4], h[5], h[6]);
 }
 static void segstat_init() {
   static int done = 0;
@@ -1388,6 +1602,12 @@ static void segstat_init() {
   HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(d_segstat_on), &one, sizeof one));
   atexit(segstat_report);
 }
+static int g_seg_split = -1;   // AMGD_SEG_SPLIT=0 / amgd_set_seg_split(0): no split records
+static bool seg_split_on() {
+  if (g_seg_split < 0) { const char *e = getenv("AMGD_SEG_SPLIT"); g_seg_split = e && *e ? atoi(e) : 1; }
+  return g_seg_split != 0;
+}
+extern "C" void amgd_set_seg_split(int on) { g_seg_split = on < 0 ? -1 : on; }
 extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
                                 const double *x, const uint32_t *list, const unsigned *nlist,
                                 uint32_t nmax, uint64_t max_entries, double *z) {
@@ -1398,28 +1618,30 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
   uint64_t *choff = (uint64_t *)amgd_alloc(((size_t)nmax + 1) * 8);
   double *csum = (double *)amgd_alloc_f64(gmax * 8);
   SpecRec *rec = (SpecRec *)amgd_alloc(gmax * sizeof(SpecRec));
+  SegSplit *rec2 = seg_split_on() ? (SegSplit *)amgd_alloc(gmax * sizeof(SegSplit)) : nullptr;
   const int G = (int)std::min<uint64_t>(gmax, 1024);
   const int R = (int)std::min<uint32_t>(nmax, 256);
   k_seg_prep<<<1, BN_THREADS, 0, st>>>(ro, list, nlist, choff);
   if (x) {
     k_seg_csum<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
     k_seg_prefix<<<(int)std::min<uint32_t>(nmax, 1024), 256, 0, st>>>(nlist, choff, csum);
-    k_seg_spec<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
+    k_seg_spec<3><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec, rec2);
     if (resolve_wave())
       k_seg_resolve_w<3><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
     else
-      k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+      k_seg_resolve<3><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, rec2, z);
   } else {
     k_seg_csum<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum);
     k_seg_prefix<<<(int)std::min<uint32_t>(nmax, 1024), 256, 0, st>>>(nlist, choff, csum);
-    k_seg_spec<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec);
+    k_seg_spec<4><<<G, SP_T, 0, st>>>(ro, col, a, x, list, nlist, choff, csum, rec, rec2);
     if (resolve_wave())
       k_seg_resolve_w<4><<<(R + 3) / 4, 256, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
     else
-      k_seg_resolve<4><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, z);
+      k_seg_resolve<4><<<R, BN_THREADS, 0, st>>>(ro, col, a, x, list, nlist, choff, rec, rec2, z);
   }
   KCHECK();
   amgd_free(choff); amgd_free(csum); amgd_free(rec);
+  if (rec2) amgd_free(rec2);
 }
 #define SP_MIN_N (16ull * BN_TILE)
 template <int MODE>

@@ -375,7 +375,8 @@ static void factor_free(skel_factor *f) {
    Wn(i,k) new -> (Wn dW')'), so the previous S is merged (mpm on positive values: a sorted
    union) with the small product instead of the whole product being formed again.  Taken
    only when Wn_prev is a subset of Wn (ones(Wn) - ones(Wn_prev) has no negative entry) and
-   Wn's values are all > 0.  The same pattern, sorted, as the product; interp_lmop then
+   Wn's values are all > 0, and only when the new entries are at most 1/16 of Wn.  The same
+   pattern, sorted, as the product; interp_lmop then
    writes every value.  AMGD_SPAT_INC=0 / amgd_spat_set_inc(0): the whole product each time. */
 static dcsr *g_prevS = NULL, *g_prevWn = NULL;   /* the last iteration's S and Wn (values 1) */
 static int g_spat_inc = -1;
@@ -394,12 +395,16 @@ static dcsr *s_pattern(const dcsr *W_skel, const dcsr *Wt) {
   dcsr *S = NULL;
   const int pos = Wn->nnz == 0 || amgd_count_gt(Wn->a, Wn->nnz, 0.0, NULL) == Wn->nnz;
   if (spat_inc_on() && pos && g_prevS && g_prevWn && g_prevWn->rn == Wn->rn && g_prevWn->cn == Wn->cn &&
-      g_prevS->rn == Wn->rn && Wn->nnz >= g_prevWn->nnz) {
+      g_prevS->rn == Wn->rn && Wn->nnz >= g_prevWn->nnz && Wn->nnz - g_prevWn->nnz <= Wn->nnz / 16) {
     dcsr *W1 = dcsr_empty_like_pattern(Wn);
     amgd_vfill(W1->a, W1->nnz, 1.0);
     dcsr *dW = amgd_mpm(1.0, W1, -1.0, g_prevWn);      /* new entries +1, lost entries -1 */
     dcsr_free(&W1);
-    if (dW->nnz == Wn->nnz - g_prevWn->nnz && (dW->nnz == 0 || amgd_count_gt(dW->a, dW->nnz, 0.0, NULL) == dW->nnz)) {
+    /* only for small growth: past 1/16 of the skeleton the product with the new entries, its
+       transpose and the merge cost more than the whole product (256^3, level 1: the early
+       iterations grow the skeleton 2-4x) */
+    if (dW->nnz <= Wn->nnz / 16 && dW->nnz == Wn->nnz - g_prevWn->nnz &&
+        (dW->nnz == 0 || amgd_count_gt(dW->a, dW->nnz, 0.0, NULL) == dW->nnz)) {
       if (dW->nnz == 0) {                                /* the same skeleton: the same pattern */
         S = g_prevS;
         g_prevS = NULL;

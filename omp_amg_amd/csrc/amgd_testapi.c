@@ -313,6 +313,8 @@ extern void amgd_spgemm_force_flat(int on);
 API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
 /* windowed (k_sg_wwin) routing of wide rows: 0 = hash kernels only; > 0 = every wide row windowed
    (routing width 1024..16384); -1 = default (2048, rows with >= 48 products per window) */
+extern void amgd_set_seg_split(int on);
+API void amgd_test_seg_split(int on) { amgd_set_seg_split(on); }
 extern void amgd_spgemm_set_dr_sort(int on);
 API void amgd_test_spgemm_dr_sort(int on) { amgd_spgemm_set_dr_sort(on); }
 API void amgd_test_spat_inc(int on) { amgd_spat_set_inc(on); }

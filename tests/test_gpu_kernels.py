@@ -733,12 +733,68 @@ def _seq(p):
     return s
 
 
-@pytest.fixture(params=[1, 0], ids=["wave_resolve", "block_resolve"])
+@pytest.fixture(params=[1, 0, 2], ids=["wave_resolve", "block_resolve", "block_nosplit"])
 def resolve(request):
-    """the speculation's resolution walk: one wavefront per sum (default) or one block"""
-    oa.resolve_wave(request.param)
+    """the speculation's resolution walk: one wavefront per sum, one block (default) with the
+    long rows' split records, or one block without them"""
+    oa.resolve_wave(1 if request.param == 1 else 0)
+    oa.seg_split(0 if request.param == 2 else 1)
     yield request.param
     oa.resolve_wave(-1)
+    oa.seg_split(-1)
+
+
+def test_spmv_rows_binade_jumps(resolve):
+    """long listed rows whose running sum jumps into higher binades now and then (the
+    anisotropic orphan rows: a strong entry ~10^3 x the sum so far), jumps at and next to
+    512-entry chunk boundaries, two jumps in one chunk, negative sums, a jump that lands on
+    a tie: the split records (one crossing per chunk, O(1)) and the binade scan give the
+    sequential loop's bits"""
+    rng = np.random.default_rng(97)
+    cn = 400000
+    rows = []
+    for q in range(8):
+        L = int(rng.integers(20000, 140000))
+        v = np.abs(rng.standard_normal(L)) * 1e-3
+        pos = np.sort(rng.choice(L, size=max(4, L // 700), replace=False))
+        if q == 1:
+            pos = np.unique(np.concatenate([pos, [511, 512, 1023, 1024, 1535, 1600]]))
+        if q == 2:
+            pos = np.unique(np.concatenate([pos, [5000, 5100, 5200]]))   # several in one chunk
+        run = 0.0
+        last = 0
+        for t, p in enumerate(pos):
+            run += v[last:p].sum()
+            if t % 2 == 0:                            # up: ~10^3 x the sum so far
+                v[p] = (run + 1e-3) * rng.uniform(500.0, 3000.0)
+            else:                                     # down again (no overflow over many jumps)
+                v[p] = -run * (1.0 - 1.0 / rng.uniform(500.0, 3000.0))
+            run += v[p]
+            last = p + 1
+        if q == 3:
+            v = -v
+        if q == 4:
+            v[pos[len(pos) // 2]] = 2.0 ** 40        # exact power of two: ties near the jump
+            v[pos[len(pos) // 2] + 1: pos[len(pos) // 2] + 50] = 2.0 ** -13
+        rows.append(v)
+    ro, cols, vals = [0], [], []
+    for v in rows:
+        c = np.sort(rng.choice(cn, size=v.size, replace=False))
+        cols.extend(c.tolist()); vals.extend(v.tolist()); ro.append(len(cols))
+    A = refops.Csr(len(rows), cn, np.array(ro, dtype=np.int64), np.array(cols, dtype=np.int64),
+                   np.array(vals))
+    x = np.where(rng.random(cn) < 0.5, 1.0, 0.75)
+    want = refops.spmv(A, x)
+    want_s = _rowsums(A)
+    order = np.arange(A.rn, dtype=np.uint32)[::-1].copy()
+    oa.mv_long(64)                    # every listed row past 64 entries: the exact grid path
+    try:
+        got = oa.test_spmv_rows(A, order, x, np.zeros(A.rn))
+        got_s = oa.test_spmv_rows(A, order, None, np.zeros(A.rn))
+    finally:
+        oa.mv_long(-1)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+    assert np.array_equal(got_s.view(np.uint64), want_s.view(np.uint64))
 
 
 @pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel",
