@@ -15,6 +15,12 @@ from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
+# heavy variants whose paths the default suite already covers at another size or rank count
+# (kept for full runs: AMGD_TESTS_EXTENDED=1); the round-end GPU suite must stay well inside
+# the driver's time limit (round 6: 892 s for the whole suite with them)
+EXT = pytest.mark.skipif(os.environ.get("AMGD_TESTS_EXTENDED", "0") != "1",
+                         reason="extended variant (AMGD_TESTS_EXTENDED=1)")
+
 
 def _free_port():
     s = socket.socket()
@@ -75,18 +81,25 @@ def test_partitioned_matches_reference_fixture(size, case):
     _run(size, case)
 
 
-@pytest.mark.parametrize("size,case", [(3, "digest:p7_48"), (2, "digest:p27_20"), (3, "digest:sem_e4_N7"),
-                                       (2, "digest:aniso_20"), (4, "digest:p7_64")],
-                         ids=lambda v: str(v).replace("digest:", ""))
-@pytest.mark.parametrize("inc", ["1", "0"], ids=["inc", "full_sweeps"])
+_DIGEST_CASES = [(3, "digest:p7_48"), (2, "digest:p27_20"), (3, "digest:sem_e4_N7"), (2, "digest:aniso_20"),
+                 (4, "digest:p7_64")]
+
+
+@pytest.mark.parametrize("size,case,inc",
+                         [pytest.param(s, c, i, id=f"{'inc' if i == '1' else 'full_sweeps'}-{s}-{c[7:]}",
+                                       marks=[EXT] if i == "0" and s >= 3 and c.startswith("digest:p7") else [])
+                          for i in ("1", "0") for s, c in _DIGEST_CASES])
 def test_partitioned_matches_digest(size, case, inc):
     """larger grids: the gathered partitioned hierarchy hashes to the stored oracle /
     reference digest (every array of every level); incremental coarsening / find_support
-    sweeps across the ranks (default) and full sweeps"""
+    sweeps across the ranks (default) and full sweeps (the 7-point 48^3 / 64^3 full-sweep
+    variants on 3-4 ranks are extended-only: full sweeps stay covered on 2 ranks here and
+    the 8-rank 27-point case)"""
     _run(size, case, timeout=170, extra_env={"AMGD_CS_INC": inc, "AMGD_FS_INC": inc})
 
 
-@pytest.mark.parametrize("case", ["gold:amgdmp", "gold:p27_8", "digest:p7_48", "digest:p27_20"],
+@pytest.mark.parametrize("case", ["gold:amgdmp", pytest.param("gold:p27_8", marks=EXT),
+                                  pytest.param("digest:p7_48", marks=EXT), "digest:p27_20"],
                          ids=lambda v: v.split(":")[1])
 def test_partitioned_eight_ranks(case):
     """8 ranks -- the north_star's GPU count -- on small fixtures (coarse levels leave
