@@ -291,8 +291,8 @@ def test_spmv_tab(A: abi.Csr, x, alpha=0.0, y=None, beta=1.0, f=None, amx=False)
 
 
 def resolve_wave(on: int) -> None:
-    """exact sums' (dots, long rows) resolution walk: 1 one wavefront (default), 0 one
-    1024-thread block, -1 environment (AMGD_RESOLVE)"""
+    """exact sums' (dots, long rows) resolution walk: 1 one wavefront, 0 one 1024-thread
+    block (default), -1 environment (AMGD_RESOLVE=wave: the wavefront)"""
     lib().amgd_test_resolve_wave(int(on))
 
 
@@ -300,6 +300,12 @@ def seg_split(on: int) -> None:
     """long-row exact sums: a chunk with one binade crossing resolved from its split record
     (1, default) or re-summed by the binade scan (0); -1: as AMGD_SEG_SPLIT says"""
     lib().amgd_test_seg_split(int(on))
+
+
+def dot_split(on: int) -> None:
+    """exact dots: a chunk with one binade crossing resolved from its split record (1, default)
+    or re-summed by the binade scan (0); -1: as AMGD_DOT_SPLIT says (seg_split(0) turns off both)"""
+    lib().amgd_test_dot_split(int(on))
 
 
 def spmv_tab(on: int) -> None:

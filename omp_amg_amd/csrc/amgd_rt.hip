@@ -687,8 +687,9 @@ __device__ __forceinline__ double bn_product(const double *a, const double *b, u
 // AMGD_SEGSTAT=1 (analysis): exact-sum counters -- [0] k_seg_resolve rows, [1] chunks,
 // [2] chunks that failed their speculation (binade_range), [3] binade_range rounds,
 // [4] elements summed one by one (rounds > 48 or subnormal sums), [5] zero-skip steps;
-// printed at process exit
-__device__ unsigned long long d_segstat[8];
+// [6] chunks resolved by their split records; the exact dots: [7] chunks that failed their
+// speculation, [8] of them resolved by their split records; printed at process exit
+__device__ unsigned long long d_segstat[10];
 __device__ int d_segstat_on = 0;
 template <int MODE>
 __device__ double binade_range(const double *a, const double *b, uint64_t lo, uint64_t hi, double s,
@@ -822,8 +823,10 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_binade(const double *a, cons
 // of its prefixes (or a flag: tie, huge, no usable guess).  (4) one block walks
 // the chunks in order with the exact running sum s: if s lies in binade e_c and
 // s/u + every prefix stays strictly inside the binade, the chunk is exactly
-// s + u*M_c (the same integer argument as above); otherwise that chunk is
-// added by binade_range.  The result is the sequential sum, bit for bit.
+// s + u*M_c (the same integer argument as above); otherwise its split record
+// (one binade crossing inside the chunk, below -- a sum of squares crosses one at
+// every 2^k-th chunk) is tried, and failing that the chunk is added by
+// binade_range.  The result is the sequential sum, bit for bit.
 // ---------------------------------------------------------------------------
 #define SP_T 256
 #define SP_PER (BN_TILE / SP_T)
@@ -846,30 +849,206 @@ __global__ __launch_bounds__(SP_T) void k_dot_csum(const double *a, const double
     __syncthreads();
   }
 }
-// exclusive prefix of the chunk sums (any order: it is only a guess)
+// exclusive prefix of the chunk sums (any order: it is only a guess) -- wave scans of the
+// 1024 threads' parts, then of the 16 wave totals
 __global__ __launch_bounds__(1024) void k_dot_approx_prefix(double *csum, uint64_t G) {
-  __shared__ double part[1024];
+  __shared__ double wtot[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t per = (G + 1023) / 1024;
-  uint64_t lo = threadIdx.x * per, hi = min(G, lo + per);
+  uint64_t lo = tid * per, hi = min(G, lo + per);
   double t = 0;
   for (uint64_t c = lo; c < hi; c++) t += csum[c];
-  part[threadIdx.x] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double r = 0;
-    for (int q = 0; q < 1024; q++) { double v = part[q]; part[q] = r; r += v; }
+  double x = t;
+  for (int o = 1; o < 64; o <<= 1) {
+    const double y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) wtot[w] = x;
   __syncthreads();
-  double r = part[threadIdx.x];
+  double ex = __shfl_up(x, 1, 64);
+  if (lane == 0) ex = 0;
+  double r = 0;
+  for (int q = 0; q < w; q++) r += wtot[q];
+  r += ex;
   for (uint64_t c = lo; c < hi; c++) { double v = csum[c]; csum[c] = r; r += v; }
 }
 struct SpecRec { long long M, mn, mx; int e, flag; };
+// One binade crossing inside a chunk (round 6).  On the anisotropic orphan rows a strong
+// entry jumps the running sum by ~10^3 -- into a higher binade -- so its chunk fails the
+// whole-chunk record and was re-summed by binade_range (a tile load and 2-3 block rounds).
+// The split record describes such a chunk as part 1 = [0, j) in the guessed binade e1, the
+// crossing product p_j, and part 2 = (j, len) in the binade e2 of the guessed sum after it:
+// the resolve checks part 1 against the exact running sum as a whole-chunk record is
+// checked (s1 = (S + M1) u1 exactly), adds p_j the ordinary way (s2 = fl(s1 + p_j), the
+// sequential loop's own step), checks part 2 against s2 in e2 and takes s3 = (S2 + M2) u2 --
+// the sequential sum, O(1) per chunk.  A second crossing, a tie or a failed check: the
+// chunk goes to binade_range as before.
+struct SegSplit { long long M1, mn1, mx1, M2, mn2, mx2; double pj; int e1, e2, ok; };
+__device__ __forceinline__ long long blk4_excl_scan(long long v, long long *sm, long long *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sm[w] = x;
+  __syncthreads();
+  long long before = 0;
+  for (int q = 0; q < w; q++) before += sm[q];
+  *total = sm[0] + sm[1] + sm[2] + sm[3];
+  __syncthreads();
+  return before + x - v;
+}
+__device__ __forceinline__ void blk4_minmax(long long &mn, long long &mx, long long *sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) { sm[w] = mn; sm[4 + w] = mx; }
+  __syncthreads();
+  mn = sm[0]; mx = sm[4];
+  for (int q = 1; q < 4; q++) { mn = sm[q] < mn ? sm[q] : mn; mx = sm[4 + q] > mx ? sm[4 + q] : mx; }
+  __syncthreads();
+}
+// the split record of a chunk whose products are tile[0, tlen) (SP_T threads, PER each).
+// The integer steps m = rint(p/u) are recomputed from the LDS tile on every pass instead of
+// held per thread (PER = 16 for the dots' 4096-product chunks: arrays would spill)
+__device__ __forceinline__ long long split_step(double p, double u, bool *bad) {
+  const double v = p / u, rr = rint(v);           // exact: power-of-two scaling
+  if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) { *bad = true; return 0; }   // huge or tie
+  return (long long)rr;
+}
+template <int PER>
+__device__ void seg_split(const double *tile, int tlen, double gs, SegSplit *out, long long *sm, int *jsh) {
+  const int tid = threadIdx.x;
+  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll, NONE_MX = -0x7fffffffffffffffll;
+  SegSplit r;
+  r.ok = 0;
+  const bool normal = fabs(gs) >= 2.2250738585072014e-308 && fabs(gs) < 1e300;
+  if (!normal) {                                  // uniform: no split record
+    if (tid == 0) *out = r;
+    return;
+  }
+  const int e1 = ilogb(gs);
+  const double u1 = ldexp(1.0, e1 - 52);
+  const long long Sg = (long long)ldexp(gs, 52 - e1);
+  const int first = tid * PER, last = min(first + PER, tlen);
+  long long loc = 0;
+  for (int idx = first; idx < last; idx++) {
+    bool b = false;
+    loc += split_step(tile[idx], u1, &b);
+  }
+  long long tot;
+  const long long pre = blk4_excl_scan(loc, sm, &tot);
+  // the first index whose element is bad or whose guessed running value leaves the binade
+  if (tid == 0) *jsh = 0x7fffffff;
+  __syncthreads();
+  {
+    long long run = pre;
+    for (int idx = first; idx < last; idx++) {
+      bool b = false;
+      const long long m = split_step(tile[idx], u1, &b);
+      if (b) { atomicMin(jsh, idx); break; }
+      run += m;
+      const long long g = Sg + run;
+      const bool inside = Sg > 0 ? (g > LO && g < HI) : (g < -LO && g > -HI);
+      if (!inside) { atomicMin(jsh, idx); break; }
+    }
+  }
+  __syncthreads();
+  const int j = *jsh;
+  __syncthreads();
+  if (j >= tlen) {                               // no crossing under the guess
+    if (tid == 0) *out = r;
+    return;
+  }
+  // part 1: [0, j) relative to the entry value; M1 = its sum (the thread owning j - 1 knows it)
+  long long mn1 = NONE_MN, mx1 = NONE_MX;
+  if (tid == 0) sm[8] = 0;
+  __syncthreads();
+  {
+    long long run = pre;
+    for (int idx = first; idx < min(last, j); idx++) {
+      bool b = false;
+      run += split_step(tile[idx], u1, &b);
+      mn1 = run < mn1 ? run : mn1;
+      mx1 = run > mx1 ? run : mx1;
+    }
+    if (j > 0 && first <= j - 1 && j - 1 < last) sm[8] = run;
+  }
+  __syncthreads();
+  const long long M1 = sm[8];
+  __syncthreads();
+  blk4_minmax(mn1, mx1, sm);
+  const double pj = tile[j];
+  const double gs2 = (double)(Sg + M1) * u1 + pj;   // a guess of the sum after the crossing
+  const bool normal2 = fabs(gs2) >= 2.2250738585072014e-308 && fabs(gs2) < 1e300;
+  const int e2 = normal2 ? ilogb(gs2) : 0;
+  const double u2 = ldexp(1.0, e2 - 52);
+  // part 2: (j, tlen) relative to the value after the crossing
+  const int f2 = max(first, j + 1);
+  long long loc2 = 0;
+  bool bad2 = !normal2;
+  for (int idx = f2; idx < last; idx++) loc2 += split_step(tile[idx], u2, &bad2);
+  long long tot2;
+  const long long pre2 = blk4_excl_scan(loc2, sm, &tot2);
+  long long mn2 = NONE_MN, mx2 = NONE_MX;
+  {
+    long long run = pre2;
+    for (int idx = f2; idx < last; idx++) {
+      bool b = false;
+      run += split_step(tile[idx], u2, &b);
+      mn2 = run < mn2 ? run : mn2;
+      mx2 = run > mx2 ? run : mx2;
+    }
+  }
+  blk4_minmax(mn2, mx2, sm);
+  if (tid == 0) *jsh = 0;
+  __syncthreads();
+  if (bad2) atomicOr(jsh, 1);
+  __syncthreads();
+  const int anybad2 = *jsh;
+  if (tid == 0) {
+    r.M1 = M1; r.mn1 = mn1; r.mx1 = mx1;
+    r.M2 = tot2; r.mn2 = mn2; r.mx2 = mx2;
+    r.pj = pj; r.e1 = e1; r.e2 = e2;
+    r.ok = anybad2 ? 0 : 1;
+    *out = r;
+  }
+  __syncthreads();
+}
+// the split chunk from the exact running sum s: the sum after it in *out, false if a check fails
+__device__ __forceinline__ bool seg_split_apply(const SegSplit &r, double s, double *out) {
+  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll;
+  if (!r.ok || !(fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1e300) || ilogb(s) != r.e1) return false;
+  const long long S = (long long)ldexp(s, 52 - r.e1);
+  if (r.mn1 != NONE_MN) {                          // part 1 non-empty: every partial sum inside
+    const bool in1 = S > 0 ? (S + r.mn1 > LO && S + r.mx1 < HI) : (S + r.mx1 < -LO && S + r.mn1 > -HI);
+    if (!in1) return false;
+  }
+  const double s1 = ldexp((double)(S + r.M1), r.e1 - 52);
+  const double s2 = s1 + r.pj;                     // the crossing step, as the loop adds it
+  if (r.mn2 == NONE_MN) { *out = s2; return true; }   // nothing after the crossing
+  if (!(fabs(s2) >= 2.2250738585072014e-308 && fabs(s2) < 1e300) || ilogb(s2) != r.e2) return false;
+  const long long S2 = (long long)ldexp(s2, 52 - r.e2);
+  const bool in2 = S2 > 0 ? (S2 + r.mn2 > LO && S2 + r.mx2 < HI) : (S2 + r.mx2 < -LO && S2 + r.mn2 > -HI);
+  if (!in2) return false;
+  *out = ldexp((double)(S2 + r.M2), r.e2 - 52);
+  return true;
+}
 template <int MODE>
 __global__ __launch_bounds__(SP_T) void k_dot_spec(const double *a, const double *b, uint64_t n,
-                                                   const double *approx, SpecRec *rec) {
+                                                   const double *approx, SpecRec *rec,
+                                                   SegSplit *rec2) {
   __shared__ double tile[BN_TILE];
   __shared__ long long ssum[SP_T / 64], smin[SP_T / 64], smax[SP_T / 64];
   __shared__ int sflag;
+  __shared__ long long ssm[9];
+  __shared__ int sj, sneed;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint64_t G = (n + BN_TILE - 1) / BN_TILE;
   for (uint64_t c = blockIdx.x; c < G; c += gridDim.x) {
@@ -924,7 +1103,18 @@ __global__ __launch_bounds__(SP_T) void k_dot_spec(const double *a, const double
       SpecRec r;
       r.M = run; r.mn = gmn; r.mx = gmx; r.e = e; r.flag = sflag;
       rec[c] = r;
+      // the whole-chunk record fails under the guess (a binade crossing of the running
+      // sum, e.g. every 2^k-th chunk of a sum of squares): a split record as well
+      const bool gnormal = fabs(g) >= 1e-290 && fabs(g) < 1e300;
+      const long long Sg = gnormal ? (long long)ldexp(g, 52 - e) : 0;
+      const long long LO = (1ll << 52), HI = (1ll << 53);
+      const bool inside = !sflag && gnormal &&
+                          (Sg > 0 ? (Sg + gmn > LO && Sg + gmx < HI) : (Sg + gmx < -LO && Sg + gmn > -HI));
+      sneed = rec2 && !inside;
     }
+    __syncthreads();
+    if (sneed) seg_split<SP_PER>(tile, tlen, g, rec2 + c, ssm, &sj);
+    else if (rec2 && tid == 0) rec2[c].ok = 0;
     __syncthreads();
   }
 }
@@ -932,7 +1122,7 @@ __global__ __launch_bounds__(SP_T) void k_dot_spec(const double *a, const double
 template <int MODE>
 __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, const double *b,
                                                             uint64_t n, const SpecRec *rec,
-                                                            double *out) {
+                                                            const SegSplit *rec2, double *out) {
   __shared__ double tile[BN_TILE];
   __shared__ long long sh[BN_THREADS / 64 + 1];
   __shared__ double s_sh;
@@ -982,8 +1172,22 @@ __global__ __launch_bounds__(BN_THREADS) void k_dot_resolve(const double *a, con
       __syncthreads();
       c = run_end;
       if (c < ce) {                         // speculation failed: add this chunk exactly
-        uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
-        s = binade_range<MODE>(a, b, lo, hi, s, tile, sh, &s_sh, &viol_sh);
+        // one crossing inside the chunk: its split record, O(1) (thread 0)
+        if (tid == 0) {
+          double s3;
+          const bool okk = rec2 && seg_split_apply(rec2[c], s, &s3);
+          viol_sh = okk ? 1 : 0;
+          if (okk) s_sh = s3;
+        }
+        __syncthreads();
+        const bool split_done = viol_sh == 1;
+        if (split_done) s = s_sh;
+        if (d_segstat_on && tid == 0) { atomicAdd(&d_segstat[7], 1ull); if (split_done) atomicAdd(&d_segstat[8], 1ull); }
+        __syncthreads();
+        if (!split_done) {
+          uint64_t lo = c * BN_TILE, hi = min(n, lo + BN_TILE);
+          s = binade_range<MODE>(a, b, lo, hi, s, tile, sh, &s_sh, &viol_sh);
+        }
         c++;
       }
     }
@@ -1090,194 +1294,6 @@ __global__ __launch_bounds__(256) void k_seg_prefix(const unsigned *nl, const ui
     }
   }
 }
-// One binade crossing inside a chunk (round 6).  On the anisotropic orphan rows a strong
-// entry jumps the running sum by ~10^3 -- into a higher binade -- so its chunk fails the
-// whole-chunk record and was re-summed by binade_range (a tile load and 2-3 block rounds).
-// The split record describes such a chunk as part 1 = [0, j) in the guessed binade e1, the
-// crossing product p_j, and part 2 = (j, len) in the binade e2 of the guessed sum after it:
-// the resolve checks part 1 against the exact running sum as a whole-chunk record is
-// checked (s1 = (S + M1) u1 exactly), adds p_j the ordinary way (s2 = fl(s1 + p_j), the
-// sequential loop's own step), checks part 2 against s2 in e2 and takes s3 = (S2 + M2) u2 --
-// the sequential sum, O(1) per chunk.  A second crossing, a tie or a failed check: the
-// chunk goes to binade_range as before.
-struct SegSplit { long long M1, mn1, mx1, M2, mn2, mx2; double pj; int e1, e2, ok; };
-__device__ __forceinline__ long long blk4_excl_scan(long long v, long long *sm, long long *total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  long long x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sm[w] = x;
-  __syncthreads();
-  long long before = 0;
-  for (int q = 0; q < w; q++) before += sm[q];
-  *total = sm[0] + sm[1] + sm[2] + sm[3];
-  __syncthreads();
-  return before + x - v;
-}
-__device__ __forceinline__ void blk4_minmax(long long &mn, long long &mx, long long *sm) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const long long a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
-  if (lane == 0) { sm[w] = mn; sm[4 + w] = mx; }
-  __syncthreads();
-  mn = sm[0]; mx = sm[4];
-  for (int q = 1; q < 4; q++) { mn = sm[q] < mn ? sm[q] : mn; mx = sm[4 + q] > mx ? sm[4 + q] : mx; }
-  __syncthreads();
-}
-// the split record of a chunk whose products are tile[0, tlen) (SP_T threads, SEG_PER each)
-__device__ void seg_split(const double *tile, int tlen, double gs, SegSplit *out, long long *sm, int *jsh) {
-  const int tid = threadIdx.x;
-  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll, NONE_MX = -0x7fffffffffffffffll;
-  SegSplit r;
-  r.ok = 0;
-  const bool normal = fabs(gs) >= 2.2250738585072014e-308 && fabs(gs) < 1e300;
-  if (!normal) {                                  // uniform: no split record
-    if (tid == 0) *out = r;
-    return;
-  }
-  const int e1 = ilogb(gs);
-  const double u1 = ldexp(1.0, e1 - 52);
-  const long long Sg = (long long)ldexp(gs, 52 - e1);
-  const int first = tid * SEG_PER;
-  long long m[SEG_PER];
-  bool bad[SEG_PER];
-  long long loc = 0;
-#pragma unroll
-  for (int q = 0; q < SEG_PER; q++) {
-    const int idx = first + q;
-    m[q] = 0;
-    bad[q] = false;
-    if (idx < tlen) {
-      const double v = tile[idx] / u1, rr = rint(v);
-      if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) bad[q] = true;
-      else m[q] = (long long)rr;
-    }
-    loc += m[q];
-  }
-  long long tot;
-  const long long pre = blk4_excl_scan(loc, sm, &tot);
-  // the first index whose element is bad or whose guessed running value leaves the binade
-  if (tid == 0) *jsh = 0x7fffffff;
-  __syncthreads();
-  {
-    long long run = pre;
-#pragma unroll
-    for (int q = 0; q < SEG_PER; q++) {
-      const int idx = first + q;
-      if (idx >= tlen) break;
-      if (bad[q]) { atomicMin(jsh, idx); break; }
-      run += m[q];
-      const long long g = Sg + run;
-      const bool inside = Sg > 0 ? (g > LO && g < HI) : (g < -LO && g > -HI);
-      if (!inside) { atomicMin(jsh, idx); break; }
-    }
-  }
-  __syncthreads();
-  const int j = *jsh;
-  __syncthreads();
-  if (j >= tlen) {                               // no crossing under the guess
-    if (tid == 0) *out = r;
-    return;
-  }
-  // part 1: [0, j) relative to the entry value
-  long long mn1 = NONE_MN, mx1 = NONE_MX, M1 = 0;
-  {
-    long long run = pre;
-#pragma unroll
-    for (int q = 0; q < SEG_PER; q++) {
-      const int idx = first + q;
-      if (idx >= j) break;
-      run += m[q];
-      mn1 = run < mn1 ? run : mn1;
-      mx1 = run > mx1 ? run : mx1;
-    }
-  }
-  // M1 = sum of m over [0, j): the thread owning j - 1 knows it
-  if (tid == 0) sm[8] = 0;
-  __syncthreads();
-  if (j > 0 && first <= j - 1 && j - 1 < first + SEG_PER) {
-    long long run = pre;
-    for (int q = 0; first + q < j; q++) run += m[q];
-    sm[8] = run;
-  }
-  __syncthreads();
-  M1 = sm[8];
-  __syncthreads();
-  blk4_minmax(mn1, mx1, sm);
-  const double pj = tile[j];
-  const double gs2 = (double)(Sg + M1) * u1 + pj;   // a guess of the sum after the crossing
-  const bool normal2 = fabs(gs2) >= 2.2250738585072014e-308 && fabs(gs2) < 1e300;
-  const int e2 = normal2 ? ilogb(gs2) : 0;
-  const double u2 = ldexp(1.0, e2 - 52);
-  // part 2: (j, tlen) relative to the value after the crossing
-  long long loc2 = 0;
-  int bad2 = normal2 ? 0 : 1;
-#pragma unroll
-  for (int q = 0; q < SEG_PER; q++) {
-    const int idx = first + q;
-    m[q] = 0;
-    if (idx > j && idx < tlen) {
-      const double v = tile[idx] / u2, rr = rint(v);
-      if (!(fabs(v) < 4.6e18) || fabs(rr - v) == 0.5) bad2 = 1;
-      else m[q] = (long long)rr;
-    }
-    loc2 += m[q];
-  }
-  long long tot2;
-  const long long pre2 = blk4_excl_scan(loc2, sm, &tot2);
-  long long mn2 = NONE_MN, mx2 = NONE_MX;
-  {
-    long long run = pre2;
-#pragma unroll
-    for (int q = 0; q < SEG_PER; q++) {
-      const int idx = first + q;
-      if (idx <= j || idx >= tlen) continue;
-      run += m[q];
-      mn2 = run < mn2 ? run : mn2;
-      mx2 = run > mx2 ? run : mx2;
-    }
-  }
-  blk4_minmax(mn2, mx2, sm);
-  if (tid == 0) *jsh = 0;
-  __syncthreads();
-  if (bad2) atomicOr(jsh, 1);
-  __syncthreads();
-  const int anybad2 = *jsh;
-  if (tid == 0) {
-    r.M1 = M1; r.mn1 = mn1; r.mx1 = mx1;
-    r.M2 = tot2; r.mn2 = mn2; r.mx2 = mx2;
-    r.pj = pj; r.e1 = e1; r.e2 = e2;
-    r.ok = anybad2 ? 0 : 1;
-    *out = r;
-  }
-  __syncthreads();
-}
-// the split chunk from the exact running sum s: the sum after it in *out, false if a check fails
-__device__ __forceinline__ bool seg_split_apply(const SegSplit &r, double s, double *out) {
-  const long long LO = (1ll << 52), HI = (1ll << 53), NONE_MN = 0x7fffffffffffffffll;
-  if (!r.ok || !(fabs(s) >= 2.2250738585072014e-308 && fabs(s) < 1e300) || ilogb(s) != r.e1) return false;
-  const long long S = (long long)ldexp(s, 52 - r.e1);
-  if (r.mn1 != NONE_MN) {                          // part 1 non-empty: every partial sum inside
-    const bool in1 = S > 0 ? (S + r.mn1 > LO && S + r.mx1 < HI) : (S + r.mx1 < -LO && S + r.mn1 > -HI);
-    if (!in1) return false;
-  }
-  const double s1 = ldexp((double)(S + r.M1), r.e1 - 52);
-  const double s2 = s1 + r.pj;                     // the crossing step, as the loop adds it
-  if (r.mn2 == NONE_MN) { *out = s2; return true; }   // nothing after the crossing
-  if (!(fabs(s2) >= 2.2250738585072014e-308 && fabs(s2) < 1e300) || ilogb(s2) != r.e2) return false;
-  const long long S2 = (long long)ldexp(s2, 52 - r.e2);
-  const bool in2 = S2 > 0 ? (S2 + r.mn2 > LO && S2 + r.mx2 < HI) : (S2 + r.mx2 < -LO && S2 + r.mn2 > -HI);
-  if (!in2) return false;
-  *out = ldexp((double)(S2 + r.M2), r.e2 - 52);
-  return true;
-}
 template <int MODE>
 __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uint32_t *col,
                                                    const double *a, const double *x,
@@ -1354,7 +1370,7 @@ __global__ __launch_bounds__(SP_T) void k_seg_spec(const uint64_t *ro, const uin
       sneed = rec2 && !inside;
     }
     __syncthreads();
-    if (sneed) seg_split(tile, tlen, gs, rec2 + g, ssm, &sj);
+    if (sneed) seg_split<SEG_PER>(tile, tlen, gs, rec2 + g, ssm, &sj);
     else if (rec2 && tid == 0) rec2[g].ok = 0;
     __syncthreads();
   }
@@ -1587,10 +1603,10 @@ static bool resolve_wave() {
 // max_entries: an upper bound on the listed rows' total length (the matrix's nnz),
 // nmax on their count: sizes the chunk records
 static void segstat_report() {
-  unsigned long long h[8];
+  unsigned long long h[10];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(d_segstat), sizeof h) != hipSuccess) return;
-  fprintf(stderr, "segstat rows %llu chunks %llu failed %llu rounds %llu serial %llu zeroskip %llu split %llu\n", h[0],
-          h[1], h[2], h[3], h[4], h[5], h[6]);
+  fprintf(stderr, "segstat rows %llu chunks %llu failed %llu rounds %llu serial %llu zeroskip %llu split %llu"
+          " dot_failed %llu dot_split %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]);
 }
 static void segstat_init() {
   static int done = 0;
@@ -1608,6 +1624,14 @@ static bool seg_split_on() {
   return g_seg_split != 0;
 }
 extern "C" void amgd_set_seg_split(int on) { g_seg_split = on < 0 ? -1 : on; }
+// the exact dots' split records (A/B): AMGD_DOT_SPLIT=0 / amgd_set_dot_split(0) turns them off
+// there alone; AMGD_SEG_SPLIT=0 turns off both
+static int g_dot_split = -1;
+static bool dot_split_on() {
+  if (g_dot_split < 0) { const char *e = getenv("AMGD_DOT_SPLIT"); g_dot_split = e && *e ? atoi(e) : 1; }
+  return g_dot_split != 0 && seg_split_on();
+}
+extern "C" void amgd_set_dot_split(int on) { g_dot_split = on < 0 ? -1 : on; }
 extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const double *a,
                                 const double *x, const uint32_t *list, const unsigned *nlist,
                                 uint32_t nmax, uint64_t max_entries, double *z) {
@@ -1651,17 +1675,21 @@ static void dot_exact_launch(const double *a, const double *b, uint64_t n, doubl
     k_dot_binade<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, out);
     return;
   }
+  segstat_init();
   uint64_t G = (n + BN_TILE - 1) / BN_TILE;
   double *csum = (double *)amgd_alloc_f64(G * 8 + 8);
   SpecRec *rec = (SpecRec *)amgd_alloc(G * sizeof(SpecRec) + 64);
   int g = (int)std::min<uint64_t>(G, 8192);
   k_dot_csum<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum);
   k_dot_approx_prefix<<<1, 1024, 0, st>>>(csum, G);
-  k_dot_spec<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum, rec);
+  // split records for the block walk (the wavefront walk does not read them)
+  SegSplit *rec2 = dot_split_on() && !resolve_wave() ? (SegSplit *)amgd_alloc(G * sizeof(SegSplit) + 64) : nullptr;
+  k_dot_spec<MODE><<<g, SP_T, 0, st>>>(a, b, n, csum, rec, rec2);
   if (resolve_wave()) k_dot_resolve_w<MODE><<<1, 64, 0, st>>>(a, b, n, rec, out);
-  else k_dot_resolve<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, rec, out);
+  else k_dot_resolve<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, rec, rec2, out);
   amgd_free(csum);
   amgd_free(rec);
+  if (rec2) amgd_free(rec2);
 }
 
 static int g_exact = -1;

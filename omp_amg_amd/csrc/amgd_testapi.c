@@ -315,6 +315,8 @@ API void amgd_test_spgemm_flat(int on) { amgd_spgemm_force_flat(on); }
    (routing width 1024..16384); -1 = default (2048, rows with >= 48 products per window) */
 extern void amgd_set_seg_split(int on);
 API void amgd_test_seg_split(int on) { amgd_set_seg_split(on); }
+extern void amgd_set_dot_split(int on);
+API void amgd_test_dot_split(int on) { amgd_set_dot_split(on); }
 extern void amgd_spgemm_set_dr_sort(int on);
 API void amgd_test_spgemm_dr_sort(int on) { amgd_spgemm_set_dr_sort(on); }
 API void amgd_test_spat_inc(int on) { amgd_spat_set_inc(on); }

@@ -798,13 +798,13 @@ def test_spmv_rows_binade_jumps(resolve):
 
 
 @pytest.mark.parametrize("kind", ["normal", "positive", "ints", "ties", "zeros", "range", "cancel",
-                                  "hover", "big", "pos_big", "spikes"])
+                                  "hover", "big", "pos_big", "spikes", "jumps"])
 def test_exact_dot_matches_sequential(kind, resolve):
     """The binade-parallel exact sum (single block below 64K products, chunk
     speculation over all CUs above, resolved by one wavefront or one block) equals the
     left-to-right loop bit for bit."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
-    n = 3000000 if kind in ("big", "pos_big", "spikes") else 300000
+    n = 3000000 if kind in ("big", "pos_big", "spikes", "jumps") else 300000
     if kind == "normal":
         a, b = rng.standard_normal(n), rng.standard_normal(n)
     elif kind == "positive":
@@ -823,6 +823,18 @@ def test_exact_dot_matches_sequential(kind, resolve):
         a = np.abs(rng.standard_normal(n)) + 1e-3; b = np.abs(rng.standard_normal(n)) + 1e-3
     elif kind == "spikes":    # products far above the running sum now and then (huge grid steps)
         a = rng.standard_normal(n) * 1e-6; a[rng.integers(0, n, 40)] = 1e12; b = np.ones(n)
+    elif kind == "jumps":     # one binade jump (up or back down) in most 4096-chunks, some on the
+        # chunk's first / last product: the dots' split records, O(1) per chunk
+        a = np.abs(rng.standard_normal(n)) * 1e-3
+        pos = np.concatenate([np.arange(1, 73) * 4096 + rng.integers(0, 4096, 72), [4096 * 80, 4096 * 81 - 1]])
+        run = 0.0
+        last = 0
+        for t, p in enumerate(np.sort(pos)):
+            run += a[last:p].sum()
+            a[p] = (run + 1e-3) * rng.uniform(2.0, 3000.0) if t % 3 != 2 else -run * (1.0 - 1.0 / rng.uniform(2.0, 50.0))
+            run += a[p]
+            last = p + 1
+        b = np.ones(n)
     elif kind == "range":
         a = rng.standard_normal(n) * 10.0 ** rng.integers(-40, 40, n); b = rng.standard_normal(n)
     else:
