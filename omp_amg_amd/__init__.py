@@ -308,6 +308,12 @@ def dot_split(on: int) -> None:
     lib().amgd_test_dot_split(int(on))
 
 
+def dot_spec_min(chunks: int) -> None:
+    """exact dots: the length (in 4096-product chunks) from which the chunk speculation runs
+    instead of one block's binade scan; -1: as AMGD_DOT_SPEC_MIN says (default 16)"""
+    lib().amgd_test_dot_spec_min(int(chunks))
+
+
 def spmv_tab(on: int) -> None:
     """gather tables for pinned long-row matrices (1 default, 0 off, -1 environment)"""
     lib().amgd_test_spmv_tab_on(int(on))

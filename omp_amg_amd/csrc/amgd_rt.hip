@@ -1667,11 +1667,18 @@ extern "C" void amgd_rows_exact(const uint64_t *ro, const uint32_t *col, const d
   amgd_free(choff); amgd_free(csum); amgd_free(rec);
   if (rec2) amgd_free(rec2);
 }
-#define SP_MIN_N (16ull * BN_TILE)
+// dots of fewer than g_sp_min chunks: one block's binade scan (k_dot_binade); longer ones the
+// chunk speculation (AMGD_DOT_SPEC_MIN / amgd_set_dot_spec_min: the threshold in chunks, A/B)
+static int g_sp_min = -1;
+static uint64_t sp_min_n() {
+  if (g_sp_min < 0) { const char *e = getenv("AMGD_DOT_SPEC_MIN"); g_sp_min = e && *e ? atoi(e) : 16; }
+  return (uint64_t)g_sp_min * BN_TILE;
+}
+extern "C" void amgd_set_dot_spec_min(int chunks) { g_sp_min = chunks; }
 template <int MODE>
 static void dot_exact_launch(const double *a, const double *b, uint64_t n, double *out) {
   hipStream_t st = amgd_s();
-  if (n < SP_MIN_N) {
+  if (n < sp_min_n()) {
     k_dot_binade<MODE><<<1, BN_THREADS, 0, st>>>(a, b, n, out);
     return;
   }

@@ -317,6 +317,8 @@ extern void amgd_set_seg_split(int on);
 API void amgd_test_seg_split(int on) { amgd_set_seg_split(on); }
 extern void amgd_set_dot_split(int on);
 API void amgd_test_dot_split(int on) { amgd_set_dot_split(on); }
+extern void amgd_set_dot_spec_min(int chunks);
+API void amgd_test_dot_spec_min(int chunks) { amgd_set_dot_spec_min(chunks); }
 extern void amgd_spgemm_set_dr_sort(int on);
 API void amgd_test_spgemm_dr_sort(int on) { amgd_spgemm_set_dr_sort(on); }
 API void amgd_test_spat_inc(int on) { amgd_spat_set_inc(on); }

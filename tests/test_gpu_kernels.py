@@ -852,6 +852,26 @@ def test_exact_dot_matches_sequential(kind, resolve):
         assert np.float64(plain).view(np.uint64) == np.float64(ref).view(np.uint64), (mode, plain, ref)
 
 
+@pytest.mark.parametrize("n", [4096, 4097, 8191, 20000, 65535, 65536])
+def test_exact_dot_short_speculation(n):
+    """the chunk speculation forced down to one-chunk dots (dot_spec_min(1)), with and without
+    the split records: the left-to-right loop's bits on sums that cross binades in most chunks"""
+    rng = np.random.default_rng(n)
+    a = np.abs(rng.standard_normal(n)) + 1e-3
+    a[rng.integers(0, n, 6)] *= 1e4
+    b = rng.standard_normal(n)
+    oa.dot_spec_min(1)
+    try:
+        for split in (1, 0):
+            oa.dot_split(split)
+            for mode, ref in ((0, _seq(a * b)), (1, _seq(a * a)), (2, _seq((a * b) * b))):
+                got = oa.test_dot(mode, a, b)
+                assert np.float64(got).view(np.uint64) == np.float64(ref).view(np.uint64), (split, mode, got, ref)
+    finally:
+        oa.dot_spec_min(-1)
+        oa.dot_split(-1)
+
+
 def _dup_cols(A, rng, frac=0.1):
     """duplicate some entries of A's rows (the reference's mxm: the last one wins)"""
     ro, cols, vals = [0], [], []

@@ -22,7 +22,7 @@ import omp_amg_amd as oa  # noqa: E402
 from omp_amg_amd import parity, problems  # noqa: E402
 
 HOOKS = {"win": oa.spgemm_win, "rw": oa.spmv_rw, "qfr": oa.qf_reuse, "pat": oa.sg_pattern,
-         "lw": oa.lmop_wave, "lsm": oa.lmop_small, "pair": oa.spmv_pair, "rwb": oa.spmv_rw_bounds, "poll": oa.d2h_poll, "qat": oa.qa_tile, "slm": oa.spmv_sl_min, "amx": oa.fs_amx, "spat": oa.spat_inc, "drs": oa.spgemm_dr_sort, "dsp": oa.dot_split}
+         "lw": oa.lmop_wave, "lsm": oa.lmop_small, "pair": oa.spmv_pair, "rwb": oa.spmv_rw_bounds, "poll": oa.d2h_poll, "qat": oa.qa_tile, "slm": oa.spmv_sl_min, "amx": oa.fs_amx, "spat": oa.spat_inc, "drs": oa.spgemm_dr_sort, "dsp": oa.dot_split, "dsm": oa.dot_spec_min}
 
 
 def digest(h):
